@@ -1,0 +1,53 @@
+"""Seeded synthetic JPEG generator, shared by tests, smoke and bench.
+
+Each image: x,y grids; R = 127+100 sin(x/(20+40u)+6u), G = 127+100 cos(y/(20+40u)+6u),
+B = 127+60 sin((x+y)/(30+30u)), plus N(0, 8) noise, clipped to uint8, with the three u ~ U[0,1)
+drawn in that order from ``numpy.random.default_rng(seed)``.  Encoded by
+``PIL.Image.save(format='JPEG', quality=q)`` defaults: baseline, 4:2:0, Annex-K tables, no DRI.
+"""
+from __future__ import annotations
+
+import io
+
+import numpy as np
+
+
+def synth_rgb(rng: np.random.Generator, w: int = 640, h: int = 480) -> np.ndarray:
+    y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+    u = rng.random()
+    r = 127 + 100 * np.sin(x / (20 + 40 * u) + 6 * u)
+    u = rng.random()
+    g = 127 + 100 * np.cos(y / (20 + 40 * u) + 6 * u)
+    u = rng.random()
+    b = 127 + 60 * np.sin((x + y) / (30 + 30 * u))
+    img = np.stack([r, g, b], -1) + rng.normal(0, 8, (h, w, 3))
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def encode_jpeg(rgb: np.ndarray, quality: int = 90, **kw) -> bytes:
+    from PIL import Image, ImageFile
+
+    ImageFile.MAXBLOCK = max(ImageFile.MAXBLOCK, 1 << 24)
+    buf = io.BytesIO()
+    Image.fromarray(rgb).save(buf, format="JPEG", quality=quality, **kw)
+    return buf.getvalue()
+
+
+def synth_jpegs(n: int, seed: int = 1234, w: int = 640, h: int = 480, quality: int = 90, **kw) -> list[bytes]:
+    rng = np.random.default_rng(seed)
+    return [encode_jpeg(synth_rgb(rng, w, h), quality, **kw) for _ in range(n)]
+
+
+# Config 3 size pool: landscape sizes and their portrait transposes.
+MIXED_SIZES = [(640, 480), (1280, 720), (1366, 768), (1920, 1080), (2560, 1440), (3840, 2160)]
+MIXED_SIZES = MIXED_SIZES + [(h, w) for (w, h) in MIXED_SIZES]
+
+
+def synth_mixed(n: int, seed: int = 4321, quality: int = 90, max_side: int = 3840) -> list[bytes]:
+    rng = np.random.default_rng(seed)
+    pool = [s for s in MIXED_SIZES if max(s) <= max_side]
+    out = []
+    for _ in range(n):
+        w, h = pool[int(rng.integers(0, len(pool)))]
+        out.append(encode_jpeg(synth_rgb(rng, w, h), quality))
+    return out

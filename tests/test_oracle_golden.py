@@ -1,0 +1,52 @@
+"""Pins the CPU oracle (oracle/) against the reference's golden vectors (CPU only)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import goldens as G
+
+G1 = list(G.g1())
+
+
+@pytest.mark.parametrize("case,jpg,arrs", G1, ids=[c["name"] for c, _, _ in G1])
+def test_g1_decode_and_pipeline(case, jpg, arrs):
+    name = case["name"]
+    if case["decode"] != "ok":
+        with pytest.raises(O.OracleError):
+            O.decode(jpg)
+        return
+    if name.startswith("progressive"):
+        # the reference decodes it through PIL; the oracle (like the MI355X path) reports UNSUPPORTED
+        st, _ = O.probe(jpg)
+        assert st == O.UNSUPPORTED
+        return
+    np.testing.assert_array_equal(O.decode(jpg), arrs["rgb"])
+    for key, out in case["outputs"].items():
+        res = tuple(int(v) for v in key.split("x"))
+        if out["status"] != "ok":
+            with pytest.raises(O.OracleError):
+                O.pipeline(jpg, res)
+            continue
+        np.testing.assert_array_equal(O.pipeline(jpg, res), arrs[f"out_{key}"])
+        assert G.sha(O.pipeline(jpg, res, normalize=True)) == out["norm_sha256"]
+
+
+def test_g2_synthetic_vga():
+    meta, jpgs = G.g2_jpegs()
+    full0 = np.load(f"{G.GOLDEN}/g2_full0.npy")
+    for im, jpg in zip(meta["images"], jpgs):
+        assert G.sha(jpg) == im["jpg_sha256"], "PIL encoder output changed; regenerate goldens"
+        assert G.sha(O.decode(jpg)) == im["rgb_sha256"]
+        out = O.pipeline(jpg, (256, 256))
+        assert G.sha(out) == im["u8_256_sha256"]
+        assert G.sha(O.pipeline(jpg, (256, 256), normalize=True)) == im["f32_256_sha256"]
+        if im["index"] == 0:
+            np.testing.assert_array_equal(out, full0)
+
+
+def test_g3_mixed_sizes_flip_normalize():
+    meta, jpgs = G.g3_jpegs()
+    for im, jpg in zip(meta["images"], jpgs):
+        assert G.sha(jpg) == im["jpg_sha256"]
+        assert G.sha(O.pipeline(jpg, (512, 512), flip=im["flip"])) == im["u8_512_sha256"]
+        assert G.sha(O.pipeline(jpg, (512, 512), flip=im["flip"], normalize=True)) == im["f32_512_sha256"]
