@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""Device-resident JPEG decode + resize@256 throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): synthetic 640x480 q90 baseline JPEGs
+(4:2:0, Annex-K tables, no DRI) resident in HBM -- 100,000 rows per GPU, row i holding the
+encoded bytes of pool image i % POOL (each row is its own copy in HBM, so every launch reads its
+compressed bytes from HBM) -- decoded, centre-cropped and bilinear-resized to 256x256 uint8 CHW
+by the C-ABI engine.  One step = one batch of ``--batch`` rows.  Multi-GPU: one process per GPU,
+rank r owns rows [r*N, (r+1)*N) of an R*N-row index (sds/index.py:227-246 INTER_NODE slicing),
+no collective on the data path ("scaling": "weak").
+
+Prints ONE JSON line (rank 0).  ``roofline`` prices the dominant kernel: algorithmic bytes per
+launch (compressed bytes in + output bytes out) / that kernel's mean device time
+from HIP events recorded around it on the launch stream during the timed region.
+``cpu_baseline`` times the reference's PIL/libjpeg-turbo pipeline (functional.py:94-110 op order)
+on a bounded sample of the same workload on this host's cores (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+
+
+def _make_pool_image(i: int) -> bytes:
+    from tests.golden.synth import encode_jpeg, synth_rgb
+    return encode_jpeg(synth_rgb(np.random.default_rng(1234 + i), 640, 480), 90)
+
+
+def make_pool(n: int, workers: int) -> list[bytes]:
+    if workers <= 1:
+        return [_make_pool_image(i) for i in range(n)]
+    with mp.get_context("spawn").Pool(workers) as p:
+        return p.map(_make_pool_image, range(n), chunksize=8)
+
+
+# ---------------------------------------------------------------- CPU baseline (reference ops)
+def _pil_pipeline(jpg: bytes):
+    """functional.py:94-110 + presets.py:716-733 op order: open/convert, crop, resize, to tensor."""
+    import io
+
+    import torch
+    from PIL import Image
+    img = Image.open(io.BytesIO(jpg)).convert("RGB")
+    w, h = img.size
+    ar = 256 / 256
+    if w / h > ar:
+        nw = int(h * ar)
+        left = (w - nw) // 2
+        img = img.crop((left, 0, left + nw, h))
+    else:
+        nh = int(w / ar)
+        top = (h - nh) // 2
+        img = img.crop((0, top, w, top + nh))
+    if img.size != (256, 256):
+        img = img.resize((256, 256), Image.BILINEAR)
+    return torch.from_numpy(np.array(img)).permute(2, 0, 1)
+
+
+def _cpu_worker(args):
+    jpgs, seconds = args
+    import torch
+    torch.set_num_threads(1)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        _pil_pipeline(jpgs[n % len(jpgs)])
+        n += 1
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline(pool: list[bytes], procs: int, seconds: float) -> float:
+    if procs <= 1:
+        n, dt = _cpu_worker((pool, seconds))
+        return n / dt
+    with mp.get_context("spawn").Pool(procs) as p:
+        res = p.map(_cpu_worker, [(pool[k::procs] or pool, seconds) for k in range(procs)])
+    return sum(n for n, _ in res) / max(dt for _, dt in res)
+
+
+def host_cores() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+# ---------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--rows", type=int, default=100_000, help="rows resident per GPU")
+    ap.add_argument("--pool", type=int, default=1024, help="distinct encoded images")
+    ap.add_argument("--res", type=int, default=256)
+    ap.add_argument("--cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    rank, world, local_rank = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), \
+        int(os.environ.get("LOCAL_RANK", 0))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    from sds_amd.distributed import compute_index_slice
+    from sds_amd.engine import JpegEngine
+
+    workers = max(1, min(16, host_cores()) // max(1, world))
+    pool = make_pool(args.pool, workers)
+
+    # this rank's slice of the R*N-row index: row i holds pool image i % POOL.  The slice is laid
+    # out as a repeated template of one pool period (16-byte aligned rows), tiled on the device, so
+    # every row is its own copy in HBM.
+    total_rows = args.rows * world
+    r0, r1, _ = compute_index_slice(total_rows, rank, world)
+    nrows = r1 - r0
+    period = [(r0 + k) % args.pool for k in range(min(args.pool, nrows))]
+    t_lens = np.array([len(pool[p]) for p in period], np.int64)
+    t_aligned = (t_lens + 15) // 16 * 16
+    t_offs = np.zeros(len(period), np.int64)
+    t_offs[1:] = np.cumsum(t_aligned)[:-1]
+    T = int(t_offs[-1] + t_aligned[-1])
+    template = np.zeros(T, np.uint8)
+    for k, p in enumerate(period):
+        template[t_offs[k]:t_offs[k] + t_lens[k]] = np.frombuffer(pool[p], np.uint8)
+    reps = (nrows + len(period) - 1) // len(period)
+    d_tmpl = torch.from_numpy(template).to(dev)
+    blob = torch.empty(reps * T, dtype=torch.uint8, device=dev)
+    for r in range(reps):
+        blob[r * T:(r + 1) * T].copy_(d_tmpl)
+    j = np.arange(nrows)
+    offs = (j // len(period)) * T + t_offs[j % len(period)]
+    lens = t_lens[j % len(period)]
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    del d_tmpl
+    torch.cuda.synchronize()
+
+    B = args.batch
+    eng = JpegEngine(dev, max_batch=B, scratch_bytes=int(B * 3.2e6) + (256 << 20))
+    out = torch.empty((B, 3, args.res, args.res), dtype=torch.uint8, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    cursor = [0]
+
+    def step():
+        s = cursor[0]
+        if s + B > nrows:
+            s = 0
+        eng.decode_resize_device(blob, d_offs[s:s + B], d_lens[s:s + B], (args.res, args.res), out=out,
+                                 status=status)
+        cursor[0] = s + B
+
+    # correctness gate before timing: the first batch's statuses are all OK
+    step()
+    torch.cuda.synchronize()
+    n_bad = int((status != 0).sum().item())
+    if n_bad:
+        raise SystemExit(f"rank {rank}: {n_bad} samples failed to decode")
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    stages = eng.stage_times()  # summed over the timed steps (HIP events on the launch stream)
+    eng.set_timing(False)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    imgs = B * args.steps * world
+    value = imgs / elapsed
+    if args.profile_steps and rank == 0:
+        print(json.dumps({"stage_ms_per_step": {k: v / args.steps for k, v in stages.items()}}), file=sys.stderr)
+
+    mean_in = float(np.mean(t_lens))
+    out_bytes = 3 * args.res * args.res
+    alg_bytes_per_img = mean_in + out_bytes
+    dom = max(stages, key=stages.get)
+    dom_ms = stages[dom] / args.steps  # mean duration of the dominant kernel per launch (1 launch / step)
+    achieved = B * alg_bytes_per_img / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+    pipeline_ms = sum(stages.values()) / args.steps
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        procs = min(16, host_cores())
+        sample = pool[:256]
+        v1 = cpu_baseline(sample, 1, args.cpu_seconds / 2)
+        vp = cpu_baseline(sample, procs, args.cpu_seconds)
+        import platform
+        cpu = {"value": round(vp, 1), "unit": "images/s", "cores": procs, "kind": "reference",
+               "sample": f"PIL {__import__('PIL').__version__}/libjpeg-turbo pipeline (functional.py:94-110 op order: "
+                         f"open+convert RGB, centre crop, BILINEAR resize 256x256, to CHW tensor) over 256 of the "
+                         f"same 640x480 q90 JPEGs from host memory, {procs} processes x {args.cpu_seconds:.0f} s "
+                         f"(single process: {v1:.1f} images/s)",
+               "single_core_value": round(v1, 1), "host": platform.processor() or platform.machine()}
+
+    if rank == 0:
+        line = {
+            "metric": "images/s device-resident JPEG decode+resize@256, 1/2/4/8 MI355X; %HBM roofline",
+            "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "configs[1]: synthetic 640x480 q90 4:2:0 baseline JPEGs resident in HBM -> "
+                                   f"centre crop + bilinear resize {args.res}x{args.res} uint8 CHW",
+                       "rows_per_gpu": nrows, "distinct_images": args.pool, "global_batch": B * world,
+                       "mean_jpeg_bytes": round(mean_in, 1), "parallelism": f"index-sharded x{world}, no collective"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "algorithmic_bytes_per_image": round(alg_bytes_per_img, 1),
+                         "pipeline_achieved": round(B * alg_bytes_per_img / (pipeline_ms * 1e-3) / 1e9, 2)
+                         if pipeline_ms > 0 else None},
+            "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

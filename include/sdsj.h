@@ -1,0 +1,133 @@
+/*
+ * sdsj.h -- C-ABI of the MI355X-native JPEG decode + crop/resize/flip/normalise path.
+ *
+ * The reference (snap-research/sds) has no native boundary: its image hot path is the Python
+ * transform list built by create_standard_image_pipeline (sds/transforms/presets.py:716-744),
+ * whose arithmetic runs in Pillow/libjpeg-turbo.  Each entry point below replaces one piece of
+ * that list; the Python drop-in (sds_amd/presets.py) binds them with ctypes, exactly as a
+ * maintainer would add a ctypes stub to sds (INTEGRATION.md shows that binding):
+ *
+ *   sdsj_probe                      <- PIL.Image.open() header parse inside
+ *                                      load_image_from_bytes (functional.py:94-100)
+ *   sdsj_decode_resize_batch        <- DecodeImageTransform (presets.py:39-45) +
+ *                                      ResizeImageTransform (presets.py:47-58 -> functional.py:38-86,
+ *                                      crop functional.py:118-147) +
+ *                                      ConvertImageToByteTensorTransform (presets.py:68-74 ->
+ *                                      functional.py:102-110) + optional
+ *                                      NormalizeFramesTransform (presets.py:154-162) and the
+ *                                      user hflip (README.md:99-108), inputs in host memory
+ *   sdsj_decode_resize_batch_device <- the same, inputs already resident in device memory
+ *                                      (the device-resident benchmark, configs 2-4)
+ *   sdsj_engine_create/destroy      <- (no reference counterpart: per-process GPU state that the
+ *                                      transform creates lazily, presets.py:1-5 pickling rule)
+ *
+ * Conventions: plain C types only; every function returns an int status (0 = SDSJ_OK, < 0 an
+ * error) and never throws; pointers are borrowed for the duration of the call.  All device work
+ * is enqueued on the caller's HIP stream (hipStream_t passed as void*).
+ */
+#ifndef SDSJ_H
+#define SDSJ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDSJ_ABI_VERSION 1
+
+/* status codes (per call and per sample) */
+#define SDSJ_OK 0
+#define SDSJ_EINVAL (-1)      /* bad argument */
+#define SDSJ_UNSUPPORTED (-2) /* valid JPEG the MI355X path does not decode (progressive, CMYK, ...) */
+#define SDSJ_CORRUPT (-3)     /* malformed / truncated stream (PIL raises OSError) */
+#define SDSJ_ENOMEM (-4)      /* allocation failed */
+#define SDSJ_EHIP (-5)        /* HIP runtime error (see sdsj_last_error) */
+#define SDSJ_ECAPACITY (-6)   /* sample did not fit the engine's scratch; resubmit in a smaller batch */
+
+/* resampling filters (Pillow Image.Resampling numbering is not used; see sds_amd/presets.py) */
+#define SDSJ_FILTER_BOX 0
+#define SDSJ_FILTER_BILINEAR 1
+#define SDSJ_FILTER_HAMMING 2
+#define SDSJ_FILTER_BICUBIC 3
+#define SDSJ_FILTER_LANCZOS 4
+
+#define SDSJ_DTYPE_U8 0  /* uint8 samples, as ConvertImageToByteTensorTransform */
+#define SDSJ_DTYPE_F32 1 /* float32 x/127.5-1, as NormalizeFramesTransform */
+
+#define SDSJ_LAYOUT_CHW 0 /* [3][H][W] contiguous */
+#define SDSJ_LAYOUT_HWC 1 /* [H][W][3] contiguous (the reference's storage order, functional.py:104-108) */
+
+typedef struct sdsj_info {
+    int32_t width, height; /* image size (PIL Image.size order: width, height) */
+    int32_t ncomp;         /* 1 (grayscale) or 3 (YCbCr) */
+    int32_t h_samp[3], v_samp[3];
+    int32_t restart_interval;
+    int32_t supported; /* 1 if the MI355X path decodes it */
+    int64_t entropy_offset;
+} sdsj_info;
+
+typedef struct sdsj_cfg {
+    int32_t abi_version;     /* must be SDSJ_ABI_VERSION */
+    int32_t max_batch;       /* images per internal launch (0 = default 4096) */
+    int64_t scratch_bytes;   /* device scratch capacity; 0 = grow on demand (host API) / 2 GiB */
+} sdsj_cfg;
+
+typedef struct sdsj_op {
+    int32_t out_h, out_w;        /* target resolution, the reference's (h, w) tuple (functional.py:76) */
+    int32_t crop_before_resize;  /* functional.py:45 (default 1): centre crop to out_w/out_h first */
+    int32_t filter;              /* SDSJ_FILTER_*; the reference default is bilinear (functional.py:48) */
+    int32_t out_dtype;           /* SDSJ_DTYPE_* */
+    int32_t layout;              /* SDSJ_LAYOUT_* */
+} sdsj_op;
+
+typedef struct sdsj_engine sdsj_engine;
+
+int sdsj_abi_version(void);
+
+/* Host-side header parse of one JPEG (no GPU needed). */
+int sdsj_probe(const uint8_t* jpg, size_t n, sdsj_info* out);
+
+/* Creates an engine bound to HIP device `hip_device`.  Scratch memory is owned by the engine. */
+int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out);
+int sdsj_engine_destroy(sdsj_engine* eng);
+
+/* Decode + crop + resize (+flip, +normalise) of n JPEGs held in HOST memory.
+ *   jpg[i], len[i]  : encoded bytes of sample i (borrowed)
+ *   flip            : host array of n bytes (1 = horizontal flip) or NULL
+ *   out             : device pointer to n * out_h * out_w * 3 elements of op->out_dtype, laid
+ *                     out per op->layout, sample-major; allocated by the caller (torch)
+ *   status          : host array of n ints, per-sample SDSJ_* code (filled before return)
+ * Synchronises `hip_stream` before returning (status is host memory). */
+int sdsj_decode_resize_batch(sdsj_engine* eng, int n, const uint8_t* const* jpg, const size_t* len,
+                             const sdsj_op* op, const uint8_t* flip, void* out, int32_t* status,
+                             void* hip_stream);
+
+/* Same with inputs already in DEVICE memory: sample i is d_blob[d_offsets[i] .. + d_lengths[i]).
+ * d_flip (n bytes) may be NULL; d_status is a device array of n ints.  Fully asynchronous on
+ * `hip_stream` (no host synchronisation, capturable into a hipGraph for a fixed n). */
+int sdsj_decode_resize_batch_device(sdsj_engine* eng, int n, const uint8_t* d_blob, const int64_t* d_offsets,
+                                    const int32_t* d_lengths, const sdsj_op* op, const uint8_t* d_flip,
+                                    void* d_out, int32_t* d_status, void* hip_stream);
+
+/* Stage timing: sdsj_engine_set_timing(e, 1) starts (and restarts) accumulation; every chunk launched
+ * afterwards records HIP events around each kernel on the caller's stream.  sdsj_engine_stage_times
+ * waits for the last recorded chunk and returns, per stage, the summed device milliseconds. */
+int sdsj_engine_set_timing(sdsj_engine* eng, int enable);
+int sdsj_engine_stage_times(const sdsj_engine* eng, float* ms, int cap, int* n_stages);
+
+const char* sdsj_last_error(const sdsj_engine* eng);
+
+/* Diagnostics for tests: device pointers of the engine's scratch and per-image descriptor array of the
+ * most recent chunk, and the byte size of one descriptor (layout: sds_amd/csrc/sdsj_common.h ImgDesc). */
+int sdsj_engine_debug_buffers(const sdsj_engine* eng, void** scratch, void** descs, int64_t* desc_bytes,
+                              int64_t* scratch_bytes);
+
+/* Name of stage k of sdsj_engine_stage_times ("parse", "unstuff", "entropy", ...). */
+const char* sdsj_stage_name(int k);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDSJ_H */

@@ -1,0 +1,385 @@
+// sdsj_common.h -- structures and the JPEG header parser shared by host (probe) and device
+// (parse kernel).  One implementation, compiled for both sides.
+//
+// The parser restates libjpeg-turbo's jdmarker.c for the subset this path decodes (SOF0/SOF1
+// 8-bit, one interleaved scan holding every component, Huffman coding, optional DRI) -- the
+// decoder Pillow calls from sds/transforms/functional.py:100.  Everything else is reported as
+// SDSJ_UNSUPPORTED (progressive, lossless, arithmetic, 12-bit, CMYK, Adobe-RGB, multi-scan).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/sdsj.h"
+
+#if defined(__HIPCC__)
+#define SDSJ_HD __host__ __device__
+#else
+#define SDSJ_HD
+#endif
+
+namespace sdsj {
+
+constexpr int kMaxComp = 3;
+constexpr int kMaxBlocksPerMcu = 10;  // D_MAX_BLOCKS_IN_MCU
+constexpr int kLutBits = 9;           // first-level Huffman lookup width
+constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
+constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
+constexpr int kUPad = 64;             // zero bytes after each unstuffed stream
+
+// Raw DHT content (bits[1..16], huffval) -- jdmarker.c get_dht.
+struct HuffSpec {
+  uint8_t bits[17];
+  uint8_t defined;
+  uint8_t pad[14];
+  uint8_t vals[256];
+};
+
+// Per-image table block in device scratch: quantisation tables (natural order) + Huffman specs
+// + derived decode tables (jdhuff.c jpeg_make_d_derived_tbl + a 2^kLutBits lookahead table).
+struct HuffDerived {
+  int32_t maxcode[18];    // maxcode[l] for l = 1..16, maxcode[17] sentinel
+  int32_t valoffset[18];
+  uint16_t lut[1 << kLutBits];  // (len << 8) | symbol, len = 0 -> slow path
+  uint8_t vals[256];
+};
+
+struct ImgTables {
+  uint16_t qt[4][64];
+  uint8_t qt_defined[4];
+  uint8_t pad[12];
+  HuffSpec dc_spec[4], ac_spec[4];
+  HuffDerived dc[4], ac[4];
+};
+
+struct CompDesc {
+  int32_t h, v, tq, td, ta;
+  int32_t rh, rv;     // upsampling ratio hmax/h, vmax/v (1 or 2)
+  int32_t dw, dh;     // downsampled width / height (jdinput.c)
+  int32_t bw, bh;     // coded blocks per row / column (MCU padded when interleaved)
+  int32_t pitch;      // plane row pitch in bytes (bw * 8)
+  int64_t plane_off;  // byte offset of this plane inside the image's plane area
+};
+
+enum GeoMode : int32_t { kGeoResize = 0, kGeoIdentity = 1, kGeoZeros = 2 };
+
+struct ImgDesc {
+  int32_t status;
+  int32_t width, height, ncomp;
+  int32_t hmax, vmax, mcux, mcuy, bpm;
+  int32_t restart_interval, nseg;
+  int32_t saw_jfif, saw_adobe, adobe_transform;
+  int32_t comp_id[kMaxComp];
+  int64_t entropy_off;   // relative to the image's first byte
+  int64_t entropy_len;   // bytes from entropy_off to the end of the input
+  int64_t total_blocks;  // blocks in the scan (mcux*mcuy*bpm)
+  int32_t blk_comp[kMaxBlocksPerMcu], blk_dx[kMaxBlocksPerMcu], blk_dy[kMaxBlocksPerMcu];
+  CompDesc comp[kMaxComp];
+  // pipeline geometry (functional.py:42-86, :118-147; Pillow ImagingResampleInner)
+  int32_t geo;                  // GeoMode
+  int32_t cx0, cy0, cw, ch;     // crop box (image coordinates)
+  int32_t need_h, need_v;
+  int32_t ksh, ksv;             // resampling kernel sizes
+  int32_t yf, yl;               // crop rows [yf, yl) feeding the vertical pass
+  int32_t src_y0, src_y1;       // image rows whose RGB is materialised
+  int32_t src_x0, src_w;        // image columns whose RGB is materialised
+  // entropy subsequences
+  int32_t sub_bits;
+  int32_t nsub_cap;
+  // scratch layout (bytes from the scratch base)
+  int64_t off_ustream, ustream_cap;
+  int64_t off_seg;      // int32 [nseg + 2]: segment start bytes, then the stream length
+  int64_t off_sub;      // SubState [nsub_cap]
+  int64_t off_coef;     // int16 [total_blocks * 64]
+  int64_t off_planes;
+  int64_t off_rgb;      // uint8 RGB rows [src_y0, src_y1) x [src_x0, src_x0 + src_w)
+  int64_t off_tmp;      // uint8 horizontal-pass output (yl - yf) x out_w x 3
+  int64_t off_kh, off_kv;  // int32 resampling tables: [2 * out] bounds then [out * ks] coefficients
+  int64_t need;         // total scratch bytes for this image
+  int32_t nsub;         // actual subsequences (set by the entropy kernel)
+  int32_t useg_found;   // segments found by the unstuff kernel
+  int64_t ulen;         // unstuffed entropy bytes
+};
+
+// Entropy decoder state at a subsequence boundary (Weissenberger & Schmidt style self-sync).
+struct SubState {
+  uint32_t entry_p;   // bit position of the first symbol decoded (entry state)
+  uint32_t exit_p;    // bit position after the last symbol that starts inside the subsequence
+  uint32_t exit_p2;   // double buffer for the sync rounds
+  uint16_t entry_bz;  // (blk << 8) | z
+  uint16_t exit_bz;
+  uint16_t exit_bz2;
+  uint16_t seg;       // segment id (low 16 bits; diagnostics only)
+  uint32_t start_bit; // first bit of the subsequence
+  uint32_t end_bit;   // one past its last bit
+  int32_t nblk;       // blocks completed while decoding it from the entry state
+  int32_t dc[kMaxComp];
+  int32_t nblk2;
+  int32_t dc2[kMaxComp];
+  int32_t first;      // 1 if it starts a segment (entry state known exactly)
+  int32_t pad;
+};
+
+SDSJ_HD inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+SDSJ_HD inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// jutils.c jpeg_natural_order (+16 guard entries)
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int natural_order(int k) {
+  constexpr int8_t t[80] = {
+      0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+      41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+      30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63,
+      63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+  return t[k];
+}
+
+// Parses markers up to the first SOS (jdmarker.c subset).  `rd(i)` returns byte i.
+template <class Reader>
+SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t) {
+  d->status = SDSJ_OK;
+  d->width = d->height = d->ncomp = 0;
+  d->restart_interval = 0;
+  d->saw_jfif = d->saw_adobe = d->adobe_transform = 0;
+  if (t) {
+    for (int q = 0; q < 4; q++) {
+      t->qt_defined[q] = 0;
+      t->dc_spec[q].defined = 0;
+      t->ac_spec[q].defined = 0;
+    }
+  }
+  if (n < 4 || rd(0) != 0xFF || rd(1) != 0xD8) return SDSJ_CORRUPT;
+  int64_t i = 2;
+  bool saw_sof = false;
+  for (;;) {
+    while (i < n && rd(i) != 0xFF) i++;  // next_marker: skip garbage
+    while (i < n && rd(i) == 0xFF) i++;  // and fill bytes
+    if (i >= n) return SDSJ_CORRUPT;
+    int m = rd(i++);
+    if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+    if (m == 0xD9) return SDSJ_CORRUPT;  // EOI before SOS
+    if (i + 2 > n) return SDSJ_CORRUPT;
+    int len = (rd(i) << 8) | rd(i + 1);
+    if (len < 2 || i + len > n) return SDSJ_CORRUPT;
+    int64_t s = i + 2;
+    int sl = len - 2;
+    switch (m) {
+      case 0xC0:
+      case 0xC1: {
+        if (saw_sof) return SDSJ_CORRUPT;
+        saw_sof = true;
+        if (sl < 6) return SDSJ_CORRUPT;
+        if (rd(s) != 8) return SDSJ_UNSUPPORTED;
+        d->height = (rd(s + 1) << 8) | rd(s + 2);
+        d->width = (rd(s + 3) << 8) | rd(s + 4);
+        d->ncomp = rd(s + 5);
+        if (d->height == 0 || d->width == 0) return SDSJ_UNSUPPORTED;  // DNL
+        if (d->ncomp != 1 && d->ncomp != 3) return SDSJ_UNSUPPORTED;
+        if (sl < 6 + 3 * d->ncomp) return SDSJ_CORRUPT;
+        d->hmax = d->vmax = 1;
+        for (int c = 0; c < d->ncomp; c++) {
+          CompDesc& cp = d->comp[c];
+          d->comp_id[c] = rd(s + 6 + 3 * c);
+          int hv = rd(s + 7 + 3 * c);
+          cp.h = hv >> 4;
+          cp.v = hv & 15;
+          cp.tq = rd(s + 8 + 3 * c);
+          if (cp.h < 1 || cp.h > 4 || cp.v < 1 || cp.v > 4 || cp.tq > 3) return SDSJ_CORRUPT;
+          if (cp.h > d->hmax) d->hmax = cp.h;
+          if (cp.v > d->vmax) d->vmax = cp.v;
+        }
+        break;
+      }
+      case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9:
+      case 0xCA: case 0xCB: case 0xCD: case 0xCE: case 0xCF:
+        return SDSJ_UNSUPPORTED;
+      case 0xC4: {  // DHT
+        int k = 0;
+        while (k < sl) {
+          if (k + 17 > sl) return SDSJ_CORRUPT;
+          int tc = rd(s + k) >> 4, th = rd(s + k) & 15;
+          if (tc > 1 || th > 3) return SDSJ_CORRUPT;
+          int cnt = 0;
+          HuffSpec* h = t ? (tc ? &t->ac_spec[th] : &t->dc_spec[th]) : nullptr;
+          for (int l = 1; l <= 16; l++) {
+            int b = rd(s + k + l);
+            cnt += b;
+            if (h) h->bits[l] = (uint8_t)b;
+          }
+          if (cnt > 256 || k + 17 + cnt > sl) return SDSJ_CORRUPT;
+          if (h) {
+            h->bits[0] = 0;
+            for (int q = 0; q < 256; q++) h->vals[q] = q < cnt ? (uint8_t)rd(s + k + 17 + q) : 0;
+            h->defined = 1;
+          }
+          k += 17 + cnt;
+        }
+        break;
+      }
+      case 0xDB: {  // DQT
+        int k = 0;
+        while (k < sl) {
+          int pq = rd(s + k) >> 4, tq = rd(s + k) & 15;
+          if (tq > 3 || pq > 1) return SDSJ_CORRUPT;
+          int need = 1 + 64 * (pq ? 2 : 1);
+          if (k + need > sl) return SDSJ_CORRUPT;
+          if (t) {
+            for (int q = 0; q < 64; q++) {
+              int v = pq ? ((rd(s + k + 1 + 2 * q) << 8) | rd(s + k + 2 + 2 * q)) : rd(s + k + 1 + q);
+              t->qt[tq][natural_order(q)] = (uint16_t)v;
+            }
+            t->qt_defined[tq] = 1;
+          }
+          k += need;
+        }
+        break;
+      }
+      case 0xDD:
+        if (sl < 2) return SDSJ_CORRUPT;
+        d->restart_interval = (rd(s) << 8) | rd(s + 1);
+        break;
+      case 0xE0:
+        if (sl >= 5 && rd(s) == 'J' && rd(s + 1) == 'F' && rd(s + 2) == 'I' && rd(s + 3) == 'F' && rd(s + 4) == 0)
+          d->saw_jfif = 1;
+        break;
+      case 0xEE:
+        if (sl >= 12 && rd(s) == 'A' && rd(s + 1) == 'd' && rd(s + 2) == 'o' && rd(s + 3) == 'b' && rd(s + 4) == 'e') {
+          d->saw_adobe = 1;
+          d->adobe_transform = rd(s + 11);
+        }
+        break;
+      case 0xDC:
+        return SDSJ_UNSUPPORTED;  // DNL
+      case 0xDA: {  // SOS
+        if (!saw_sof || sl < 1) return SDSJ_CORRUPT;
+        int ns = rd(s);
+        if (sl < 1 + 2 * ns + 3) return SDSJ_CORRUPT;
+        if (ns != d->ncomp) return SDSJ_UNSUPPORTED;  // multi-scan sequential
+        for (int q = 0; q < ns; q++) {
+          int cid = rd(s + 1 + 2 * q);
+          int c = 0;
+          while (c < d->ncomp && d->comp_id[c] != cid) c++;
+          if (c != q) return SDSJ_UNSUPPORTED;
+          int tt = rd(s + 2 + 2 * q);
+          d->comp[c].td = tt >> 4;
+          d->comp[c].ta = tt & 15;
+          if (d->comp[c].td > 3 || d->comp[c].ta > 3) return SDSJ_CORRUPT;
+        }
+        int ss = rd(s + 1 + 2 * ns), se = rd(s + 2 + 2 * ns), ahal = rd(s + 3 + 2 * ns);
+        if (ss != 0 || se != 63 || ahal != 0) return SDSJ_UNSUPPORTED;
+        d->entropy_off = i + len;
+        d->entropy_len = n - d->entropy_off;
+        return SDSJ_OK;
+      }
+      default:
+        break;
+    }
+    i += len;
+  }
+}
+
+// Colour space (jdapimin.c default_decompress_parms) and geometry (jdinput.c).
+SDSJ_HD inline int setup_geometry(ImgDesc* d, const ImgTables* t) {
+  if (d->ncomp == 3) {
+    if (!d->saw_jfif) {
+      if (d->saw_adobe) {
+        if (d->adobe_transform == 0) return SDSJ_UNSUPPORTED;  // Adobe RGB
+      } else if (d->comp_id[0] == 82 && d->comp_id[1] == 71 && d->comp_id[2] == 66) {
+        return SDSJ_UNSUPPORTED;  // 'R','G','B' component ids
+      }
+    }
+  }
+  int bpm = 0;
+  for (int c = 0; c < d->ncomp; c++) {
+    CompDesc& cp = d->comp[c];
+    if (d->hmax % cp.h || d->vmax % cp.v) return SDSJ_UNSUPPORTED;
+    cp.rh = d->hmax / cp.h;
+    cp.rv = d->vmax / cp.v;
+    if (cp.rh > 2 || cp.rv > 2) return SDSJ_UNSUPPORTED;
+    cp.dw = ceil_div(d->width * cp.h, d->hmax);
+    cp.dh = ceil_div(d->height * cp.v, d->vmax);
+    if (t) {
+      if (!t->qt_defined[cp.tq]) return SDSJ_CORRUPT;
+      if (!t->dc_spec[cp.td].defined || !t->ac_spec[cp.ta].defined) return SDSJ_CORRUPT;
+    }
+  }
+  if (d->ncomp == 1) {
+    CompDesc& cp = d->comp[0];
+    cp.bw = ceil_div(cp.dw, 8);
+    cp.bh = ceil_div(cp.dh, 8);
+    d->mcux = cp.bw;
+    d->mcuy = cp.bh;
+    d->bpm = 1;
+    d->blk_comp[0] = 0;
+    d->blk_dx[0] = 0;
+    d->blk_dy[0] = 0;
+  } else {
+    d->mcux = ceil_div(d->width, 8 * d->hmax);
+    d->mcuy = ceil_div(d->height, 8 * d->vmax);
+    for (int c = 0; c < d->ncomp; c++) {
+      d->comp[c].bw = d->mcux * d->comp[c].h;
+      d->comp[c].bh = d->mcuy * d->comp[c].v;
+      for (int v = 0; v < d->comp[c].v; v++)
+        for (int h = 0; h < d->comp[c].h; h++) {
+          if (bpm >= kMaxBlocksPerMcu) return SDSJ_CORRUPT;
+          d->blk_comp[bpm] = c;
+          d->blk_dx[bpm] = h;
+          d->blk_dy[bpm] = v;
+          bpm++;
+        }
+    }
+    d->bpm = bpm;
+  }
+  int64_t plane = 0;
+  for (int c = 0; c < d->ncomp; c++) {
+    CompDesc& cp = d->comp[c];
+    cp.pitch = cp.bw * 8;
+    cp.plane_off = plane;
+    plane += align_up((int64_t)cp.pitch * cp.bh * 8, 256);
+  }
+  d->total_blocks = (int64_t)d->mcux * d->mcuy * d->bpm;
+  int64_t mcus = (int64_t)d->mcux * d->mcuy;
+  d->nseg = d->restart_interval ? (int32_t)((mcus + d->restart_interval - 1) / d->restart_interval) : 1;
+  return SDSJ_OK;
+}
+
+// functional.py:118-140 crop_to_aspect_ratio (Python doubles, int() truncation, floor-div).
+SDSJ_HD inline void crop_box(int w, int h, int out_h, int out_w, int* x0, int* y0, int* cw, int* ch) {
+  double cur = (double)w / (double)h;
+  double tgt = (double)out_w / (double)out_h;
+  if (cur > tgt) {
+    int nw = (int)((double)h * tgt);
+    *x0 = (w - nw) / 2;
+    *y0 = 0;
+    *cw = nw;
+    *ch = h;
+  } else {
+    int nh = (int)((double)w / tgt);
+    *x0 = 0;
+    *y0 = (h - nh) / 2;
+    *cw = w;
+    *ch = nh;
+  }
+}
+
+// Pillow Resample.c precompute_coeffs: kernel size for a 1-D resample in -> out.
+SDSJ_HD inline int resample_ksize(int in_size, int out_size, double filter_support) {
+  double scale = (double)in_size / out_size;
+  double fs = scale < 1.0 ? 1.0 : scale;
+  double support = filter_support * fs;
+  int c = (int)support;
+  if ((double)c < support) c++;  // ceil
+  return c * 2 + 1;
+}
+
+SDSJ_HD inline double filter_support(int filter) {
+  switch (filter) {
+    case SDSJ_FILTER_BOX: return 0.5;
+    case SDSJ_FILTER_BILINEAR: return 1.0;
+    case SDSJ_FILTER_HAMMING: return 1.0;
+    case SDSJ_FILTER_BICUBIC: return 2.0;
+    default: return 3.0;
+  }
+}
+
+}  // namespace sdsj

@@ -1,0 +1,390 @@
+// sdsj_engine.hip -- the C-ABI (include/sdsj.h): engine state, scratch management, batch driver.
+//
+// One engine per process and device (sds transforms are created lazily per DataLoader worker,
+// presets.py:1-5).  The engine owns device scratch, per-image descriptor/table arrays, pinned
+// staging for the host-bytes entry point and the 256-entry normalisation LUT.  Every batch is a
+// fixed sequence of kernel launches on the caller's stream: no host synchronisation inside the
+// device-resident entry point.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "sdsj_common.h"
+#include "sdsj_kernels.h"
+
+using namespace sdsj;
+
+namespace {
+constexpr int kStages = 9;
+const char* kStageNames[kStages] = {"parse", "plan", "unstuff", "entropy", "idct", "color", "coeffs", "hpass", "vpass"};
+}  // namespace
+
+struct sdsj_engine {
+  int device = 0;
+  int max_batch = 4096;
+  int64_t capacity = 0;
+  bool grow = true;
+  uint8_t* scratch = nullptr;
+  ImgDesc* descs = nullptr;
+  ImgTables* tables = nullptr;
+  int64_t* d_total = nullptr;
+  float* d_lut = nullptr;
+  // host-bytes path
+  uint8_t* h_stage = nullptr;
+  size_t h_stage_cap = 0;
+  uint8_t* d_blob = nullptr;
+  size_t d_blob_cap = 0;
+  int64_t* h_offsets = nullptr;
+  int32_t* h_lengths = nullptr;
+  uint8_t* h_flip = nullptr;
+  int64_t* d_offsets = nullptr;
+  int32_t* d_lengths = nullptr;
+  uint8_t* d_flip = nullptr;
+  int32_t* d_status = nullptr;
+  int32_t* h_status = nullptr;
+  int io_cap = 0;
+  // timing: one event set per chunk launched since the last sdsj_engine_set_timing(e, 1)
+  bool timing = false;
+  std::vector<std::vector<hipEvent_t>> ev_sets;
+  size_t ev_used = 0;
+  std::string err;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int fail(sdsj_engine* e, int code, const std::string& msg) {
+  if (e) e->err = msg;
+  return code;
+}
+
+int hip_fail(sdsj_engine* e, hipError_t st, const char* what) {
+  return fail(e, SDSJ_EHIP, std::string(what) + ": " + hipGetErrorString(st));
+}
+
+#define SDSJ_HIP(e, call)                                  \
+  do {                                                     \
+    hipError_t _st = (call);                               \
+    if (_st != hipSuccess) return hip_fail((e), _st, #call); \
+  } while (0)
+
+int ensure_io(sdsj_engine* e, int n) {
+  if (n <= e->io_cap) return SDSJ_OK;
+  int cap = std::max(n, 64);
+  (void)hipFree(e->d_offsets);
+  (void)hipFree(e->d_lengths);
+  (void)hipFree(e->d_flip);
+  (void)hipFree(e->d_status);
+  (void)hipHostFree(e->h_offsets);
+  (void)hipHostFree(e->h_lengths);
+  (void)hipHostFree(e->h_flip);
+  (void)hipHostFree(e->h_status);
+  e->io_cap = 0;
+  SDSJ_HIP(e, hipMalloc(&e->d_offsets, sizeof(int64_t) * cap));
+  SDSJ_HIP(e, hipMalloc(&e->d_lengths, sizeof(int32_t) * cap));
+  SDSJ_HIP(e, hipMalloc(&e->d_flip, cap));
+  SDSJ_HIP(e, hipMalloc(&e->d_status, sizeof(int32_t) * cap));
+  SDSJ_HIP(e, hipHostMalloc(&e->h_offsets, sizeof(int64_t) * cap));
+  SDSJ_HIP(e, hipHostMalloc(&e->h_lengths, sizeof(int32_t) * cap));
+  SDSJ_HIP(e, hipHostMalloc(&e->h_flip, cap));
+  SDSJ_HIP(e, hipHostMalloc(&e->h_status, sizeof(int32_t) * cap));
+  e->io_cap = cap;
+  return SDSJ_OK;
+}
+
+int ensure_scratch(sdsj_engine* e, int64_t need) {
+  if (need <= e->capacity && e->scratch) return SDSJ_OK;
+  int64_t cap = std::max<int64_t>(need, e->capacity * 3 / 2);
+  cap = std::max<int64_t>(cap, 64 << 20);
+  (void)hipFree(e->scratch);
+  e->scratch = nullptr;
+  e->capacity = 0;
+  SDSJ_HIP(e, hipMalloc(&e->scratch, cap));
+  e->capacity = cap;
+  return SDSJ_OK;
+}
+
+bool valid_op(const sdsj_op* op) {
+  return op && op->out_h > 0 && op->out_w > 0 && op->out_h <= 65535 && op->out_w <= 65535 && op->filter >= 0 &&
+         op->filter <= SDSJ_FILTER_LANCZOS && (op->out_dtype == SDSJ_DTYPE_U8 || op->out_dtype == SDSJ_DTYPE_F32) &&
+         (op->layout == SDSJ_LAYOUT_CHW || op->layout == SDSJ_LAYOUT_HWC);
+}
+
+// Runs the kernel sequence for one chunk (n <= max_batch) of device-resident inputs.
+int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_offsets, const int32_t* d_lengths,
+              const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status, hipStream_t s) {
+  std::vector<hipEvent_t>* evs = nullptr;
+  if (e->timing) {
+    if (e->ev_used == e->ev_sets.size()) {
+      std::vector<hipEvent_t> set(kStages + 1);
+      for (auto& ev : set) SDSJ_HIP(e, hipEventCreate(&ev));
+      e->ev_sets.push_back(set);
+    }
+    evs = &e->ev_sets[e->ev_used++];
+  }
+  auto mark = [&](int k) {
+    if (evs) (void)hipEventRecord((*evs)[k], s);
+  };
+  mark(0);
+  SDSJ_HIP(e, launch_parse(n, d_blob, d_offsets, d_lengths, op, e->descs, e->tables, s));
+  mark(1);
+  SDSJ_HIP(e, launch_plan(n, e->descs, e->capacity, e->d_total, s));
+  mark(2);
+  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, e->descs, e->scratch, s));
+  mark(3);
+  SDSJ_HIP(e, launch_entropy(n, e->descs, e->tables, e->scratch, s));
+  mark(4);
+  SDSJ_HIP(e, launch_idct(n, e->descs, e->tables, e->scratch, s));
+  mark(5);
+  SDSJ_HIP(e, launch_color(n, e->descs, e->scratch, s));
+  mark(6);
+  SDSJ_HIP(e, launch_coeffs(n, e->descs, op, e->scratch, s));
+  mark(7);
+  SDSJ_HIP(e, launch_hpass(n, e->descs, op, e->scratch, s));
+  mark(8);
+  SDSJ_HIP(e, launch_vpass(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_lut, s));
+  mark(9);
+  return SDSJ_OK;
+}
+
+int64_t out_bytes_per_image(const sdsj_op& op) {
+  return (int64_t)op.out_h * op.out_w * 3 * (op.out_dtype == SDSJ_DTYPE_F32 ? 4 : 1);
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdsj_abi_version(void) { return SDSJ_ABI_VERSION; }
+
+int sdsj_probe(const uint8_t* jpg, size_t n, sdsj_info* out) {
+  if (!jpg || !out) return SDSJ_EINVAL;
+  memset(out, 0, sizeof(*out));
+  ImgDesc d;
+  static thread_local ImgTables t;
+  struct R {
+    const uint8_t* p;
+    int operator()(int64_t i) const { return p[i]; }
+  } rd{jpg};
+  int st = parse_headers(rd, (int64_t)n, &d, &t);
+  out->width = d.width;
+  out->height = d.height;
+  out->ncomp = d.ncomp;
+  if (st == SDSJ_OK) st = setup_geometry(&d, &t);
+  for (int c = 0; c < d.ncomp && c < 3; c++) {
+    out->h_samp[c] = d.comp[c].h;
+    out->v_samp[c] = d.comp[c].v;
+  }
+  out->restart_interval = d.restart_interval;
+  out->entropy_offset = st == SDSJ_OK ? d.entropy_off : 0;
+  out->supported = st == SDSJ_OK;
+  return st;
+}
+
+int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
+  if (!out) return SDSJ_EINVAL;
+  *out = nullptr;
+  if (cfg && cfg->abi_version != SDSJ_ABI_VERSION) return SDSJ_EINVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || hip_device < 0 || hip_device >= ndev) return SDSJ_EHIP;
+  sdsj_engine* e = new (std::nothrow) sdsj_engine();
+  if (!e) return SDSJ_ENOMEM;
+  e->device = hip_device;
+  if (cfg && cfg->max_batch > 0) e->max_batch = cfg->max_batch;
+  DeviceGuard g(hip_device);
+  int st = SDSJ_OK;
+  auto cleanup = [&](int code) {
+    sdsj_engine_destroy(e);
+    return code;
+  };
+  if (hipMalloc(&e->descs, sizeof(ImgDesc) * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMalloc(&e->tables, sizeof(ImgTables) * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMalloc(&e->d_total, sizeof(int64_t)) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMalloc(&e->d_lut, sizeof(float) * 256) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  {
+    // presets.py:161 `x.float() / 127.5 - 1.0` in float32 (IEEE division then subtraction)
+    float lut[256];
+    volatile float div = 127.5f, one = 1.0f;
+    for (int v = 0; v < 256; v++) {
+      float q = (float)v / div;
+      lut[v] = q - one;
+    }
+    if (hipMemcpy(e->d_lut, lut, sizeof(lut), hipMemcpyHostToDevice) != hipSuccess) return cleanup(SDSJ_EHIP);
+  }
+  if (cfg && cfg->scratch_bytes > 0) {
+    e->grow = false;
+    st = ensure_scratch(e, cfg->scratch_bytes);
+    if (st != SDSJ_OK) return cleanup(st);
+  }
+  *out = e;
+  return SDSJ_OK;
+}
+
+int sdsj_engine_destroy(sdsj_engine* e) {
+  if (!e) return SDSJ_EINVAL;
+  DeviceGuard g(e->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(e->scratch);
+  (void)hipFree(e->descs);
+  (void)hipFree(e->tables);
+  (void)hipFree(e->d_total);
+  (void)hipFree(e->d_lut);
+  (void)hipFree(e->d_blob);
+  (void)hipFree(e->d_offsets);
+  (void)hipFree(e->d_lengths);
+  (void)hipFree(e->d_flip);
+  (void)hipFree(e->d_status);
+  (void)hipHostFree(e->h_stage);
+  (void)hipHostFree(e->h_offsets);
+  (void)hipHostFree(e->h_lengths);
+  (void)hipHostFree(e->h_flip);
+  (void)hipHostFree(e->h_status);
+  for (auto& set : e->ev_sets)
+    for (auto ev : set) (void)hipEventDestroy(ev);
+  delete e;
+  return SDSJ_OK;
+}
+
+int sdsj_decode_resize_batch_device(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_offsets,
+                                    const int32_t* d_lengths, const sdsj_op* op, const uint8_t* d_flip, void* d_out,
+                                    int32_t* d_status, void* hip_stream) {
+  if (!e) return SDSJ_EINVAL;
+  if (n < 0 || (n > 0 && (!d_blob || !d_offsets || !d_lengths || !d_out || !d_status)) || !valid_op(op))
+    return fail(e, SDSJ_EINVAL, "invalid argument");
+  if (n == 0) return SDSJ_OK;
+  DeviceGuard g(e->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
+  if (!e->scratch) {
+    int st = ensure_scratch(e, (int64_t)2 << 30);
+    if (st != SDSJ_OK) return st;
+  }
+  const int64_t ob = out_bytes_per_image(*op);
+  for (int c0 = 0; c0 < n; c0 += e->max_batch) {
+    int m = std::min(e->max_batch, n - c0);
+    int st = run_chunk(e, m, d_blob, d_offsets + c0, d_lengths + c0, *op, d_flip ? d_flip + c0 : nullptr,
+                       reinterpret_cast<uint8_t*>(d_out) + c0 * ob, d_status + c0, s);
+    if (st != SDSJ_OK) return st;
+  }
+  return SDSJ_OK;
+}
+
+int sdsj_decode_resize_batch(sdsj_engine* e, int n, const uint8_t* const* jpg, const size_t* len, const sdsj_op* op,
+                             const uint8_t* flip, void* out, int32_t* status, void* hip_stream) {
+  if (!e) return SDSJ_EINVAL;
+  if (n < 0 || (n > 0 && (!jpg || !len || !out || !status)) || !valid_op(op))
+    return fail(e, SDSJ_EINVAL, "invalid argument");
+  if (n == 0) return SDSJ_OK;
+  DeviceGuard g(e->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
+  const int64_t ob = out_bytes_per_image(*op);
+  int rc = ensure_io(e, std::min(n, e->max_batch));
+  if (rc != SDSJ_OK) return rc;
+  for (int c0 = 0; c0 < n; c0 += e->max_batch) {
+    int m = std::min(e->max_batch, n - c0);
+    // host planning: exact scratch need of this chunk (same code as k_parse / k_plan)
+    int64_t need = 0, bytes = 0;
+    for (int i = 0; i < m; i++) {
+      int st = SDSJ_OK;
+      if (len[c0 + i] > (size_t)INT32_MAX) return fail(e, SDSJ_EINVAL, "sample larger than 2 GiB");
+      int64_t ni = host_plan_need(jpg[c0 + i], (int64_t)len[c0 + i], *op, &st);
+      if (st == SDSJ_OK) need += align_up(ni, 256);
+      bytes += align_up((int64_t)len[c0 + i], 16);
+    }
+    if (need > e->capacity) {
+      if (!e->grow) return fail(e, SDSJ_ECAPACITY, "batch exceeds the configured scratch capacity");
+      SDSJ_HIP(e, hipStreamSynchronize(s));
+      rc = ensure_scratch(e, need);
+      if (rc != SDSJ_OK) return rc;
+    }
+    if ((size_t)bytes > e->h_stage_cap) {
+      SDSJ_HIP(e, hipStreamSynchronize(s));
+      (void)hipHostFree(e->h_stage);
+      (void)hipFree(e->d_blob);
+      e->h_stage = nullptr;
+      e->d_blob = nullptr;
+      e->h_stage_cap = e->d_blob_cap = 0;
+      size_t cap = std::max<size_t>((size_t)bytes * 3 / 2, 1 << 20);
+      SDSJ_HIP(e, hipHostMalloc(&e->h_stage, cap));
+      SDSJ_HIP(e, hipMalloc(&e->d_blob, cap));
+      e->h_stage_cap = e->d_blob_cap = cap;
+    }
+    // the staging buffers are reused: wait for the previous chunk's H2D to finish
+    SDSJ_HIP(e, hipStreamSynchronize(s));
+    int64_t off = 0;
+    for (int i = 0; i < m; i++) {
+      memcpy(e->h_stage + off, jpg[c0 + i], len[c0 + i]);
+      e->h_offsets[i] = off;
+      e->h_lengths[i] = (int32_t)len[c0 + i];
+      e->h_flip[i] = flip ? flip[c0 + i] : 0;
+      off += align_up((int64_t)len[c0 + i], 16);
+    }
+    SDSJ_HIP(e, hipMemcpyAsync(e->d_blob, e->h_stage, off, hipMemcpyHostToDevice, s));
+    SDSJ_HIP(e, hipMemcpyAsync(e->d_offsets, e->h_offsets, sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
+    SDSJ_HIP(e, hipMemcpyAsync(e->d_lengths, e->h_lengths, sizeof(int32_t) * m, hipMemcpyHostToDevice, s));
+    SDSJ_HIP(e, hipMemcpyAsync(e->d_flip, e->h_flip, m, hipMemcpyHostToDevice, s));
+    rc = run_chunk(e, m, e->d_blob, e->d_offsets, e->d_lengths, *op, e->d_flip,
+                   reinterpret_cast<uint8_t*>(out) + c0 * ob, e->d_status, s);
+    if (rc != SDSJ_OK) return rc;
+    SDSJ_HIP(e, hipMemcpyAsync(e->h_status, e->d_status, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s));
+    SDSJ_HIP(e, hipStreamSynchronize(s));
+    memcpy(status + c0, e->h_status, sizeof(int32_t) * m);
+  }
+  return SDSJ_OK;
+}
+
+int sdsj_engine_set_timing(sdsj_engine* e, int enable) {
+  if (!e) return SDSJ_EINVAL;
+  e->timing = enable != 0;
+  e->ev_used = 0;  // restart accumulation
+  return SDSJ_OK;
+}
+
+int sdsj_engine_stage_times(const sdsj_engine* e, float* ms, int cap, int* n_stages) {
+  if (!e || !n_stages || (cap > 0 && !ms)) return SDSJ_EINVAL;
+  *n_stages = kStages;
+  for (int k = 0; k < cap && k < kStages; k++) ms[k] = 0.f;
+  if (!e->timing || e->ev_used == 0) return SDSJ_OK;
+  DeviceGuard g(e->device);
+  if (hipEventSynchronize(e->ev_sets[e->ev_used - 1][kStages]) != hipSuccess) return SDSJ_EHIP;
+  for (size_t c = 0; c < e->ev_used; c++) {
+    for (int k = 0; k < cap && k < kStages; k++) {
+      float v = 0.f;
+      if (hipEventElapsedTime(&v, e->ev_sets[c][k], e->ev_sets[c][k + 1]) != hipSuccess) return SDSJ_EHIP;
+      ms[k] += v;
+    }
+  }
+  return SDSJ_OK;
+}
+
+const char* sdsj_last_error(const sdsj_engine* e) {
+  if (!e) return "null engine";
+  return e->err.c_str();
+}
+
+int sdsj_engine_debug_buffers(const sdsj_engine* e, void** scratch, void** descs, int64_t* desc_bytes,
+                              int64_t* scratch_bytes) {
+  if (!e || !scratch || !descs || !desc_bytes || !scratch_bytes) return SDSJ_EINVAL;
+  *scratch = e->scratch;
+  *descs = e->descs;
+  *desc_bytes = (int64_t)sizeof(ImgDesc);
+  *scratch_bytes = e->capacity;
+  return SDSJ_OK;
+}
+
+const char* sdsj_stage_name(int k) { return k >= 0 && k < kStages ? kStageNames[k] : ""; }
+
+}  // extern "C"

@@ -1,0 +1,22 @@
+// sdsj_kernels.h -- launchers of the gfx950 kernels in sdsj_kernels.hip (engine-internal).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "sdsj_common.h"
+
+namespace sdsj {
+hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, const int32_t* lengths, const sdsj_op& op,
+                        ImgDesc* descs, ImgTables* tables, hipStream_t s);
+hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, hipStream_t s);
+hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
+                          hipStream_t s);
+hipError_t launch_entropy(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
+hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
+hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, hipStream_t s);
+hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s);
+hipError_t launch_hpass(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s);
+hipError_t launch_vpass(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
+                        void* out, int32_t* status, const float* lut, hipStream_t s);
+// host-side planning (same code as k_parse): returns the scratch bytes image `jpg` needs, or < 0
+int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status);
+}  // namespace sdsj

@@ -1,0 +1,1272 @@
+// sdsj_kernels.hip -- gfx950 (MI355X) kernels of the batched JPEG decode + crop/resize path.
+//
+// Stage map (reference behaviour each kernel reproduces, see DESIGN.md for the layout/rooflines):
+//   k_parse    markers, tables, geometry          jdmarker.c / jdhuff.c tables / functional.py:118-140
+//   k_plan     per-batch scratch offsets          (no reference counterpart)
+//   k_unstuff  byte unstuffing + RSTn split        jdhuff.c jpeg_fill_bit_buffer / process_restart
+//   k_entropy  self-synchronising Huffman decode  jdhuff.c decode_mcu (parallel restatement)
+//   k_idct     dequant + ISLOW IDCT                jidctint.c jpeg_idct_islow
+//   k_color    fancy upsampling + YCbCr->RGB      jdsample.c / jdmainct.c / jdcolor.c
+//   k_coeffs   resampling tables (doubles)        Pillow Resample.c precompute_coeffs
+//   k_hpass    horizontal pass, uint8 out         Pillow ImagingResampleHorizontal_8bpc
+//   k_vpass    vertical pass + hflip + layout/LUT Pillow ImagingResampleVertical_8bpc,
+//                                                 functional.py:102-110, presets.py:154-162
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sdsj_common.h"
+#include "sdsj_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace sdsj {
+
+// ------------------------------------------------------------------------------------------
+// k_parse: one wave per image.  The first kHdrStage bytes are staged into LDS (coalesced); lane 0
+// walks the markers; all lanes build the derived Huffman tables.
+// ------------------------------------------------------------------------------------------
+constexpr int kHdrStage = 4096;
+
+struct DevReader {
+  const uint8_t* lds;
+  int64_t nlds;
+  const uint8_t* g;
+  __device__ int operator()(int64_t i) const { return i < nlds ? lds[i] : g[i]; }
+};
+
+// Pillow precompute_coeffs bounds for output index xx (doubles, same operation order).
+__device__ __host__ inline void resample_bounds(int in_size, int out_size, double support_base, int xx,
+                                                int* xmin_out, int* xmax_out) {
+  double scale = (double)in_size / out_size;
+  double filterscale = scale < 1.0 ? 1.0 : scale;
+  double support = support_base * filterscale;
+  double center = 0.0 + (xx + 0.5) * scale;
+  int xmin = (int)(center - support + 0.5);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(center + support + 0.5);
+  if (xmax > in_size) xmax = in_size;
+  *xmin_out = xmin;
+  *xmax_out = xmax - xmin;
+}
+
+__device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
+  // Geometry: functional.py:78-80 shortcut, :118-147 crop, Pillow ImagingResampleInner.
+  const int W = d->width, H = d->height;
+  if (W == op.out_w && H == op.out_h) {
+    d->geo = kGeoIdentity;
+    d->cx0 = d->cy0 = 0;
+    d->cw = W;
+    d->ch = H;
+  } else {
+    d->geo = kGeoResize;
+    if (op.crop_before_resize) {
+      crop_box(W, H, op.out_h, op.out_w, &d->cx0, &d->cy0, &d->cw, &d->ch);
+    } else {
+      d->cx0 = d->cy0 = 0;
+      d->cw = W;
+      d->ch = H;
+    }
+    if (d->cw <= 0 || d->ch <= 0) d->geo = kGeoZeros;
+  }
+  d->need_h = d->geo == kGeoResize && d->cw != op.out_w;
+  d->need_v = d->geo == kGeoResize && d->ch != op.out_h;
+  double sup = filter_support(op.filter);
+  d->ksh = d->need_h ? resample_ksize(d->cw, op.out_w, sup) : 0;
+  d->ksv = d->need_v ? resample_ksize(d->ch, op.out_h, sup) : 0;
+  if (d->geo == kGeoZeros) {
+    d->yf = d->yl = 0;
+  } else if (d->need_v) {
+    int a0, a1, b0, b1;
+    resample_bounds(d->ch, op.out_h, sup, 0, &a0, &a1);
+    resample_bounds(d->ch, op.out_h, sup, op.out_h - 1, &b0, &b1);
+    d->yf = a0;
+    d->yl = b0 + b1;
+  } else {
+    d->yf = 0;
+    d->yl = d->ch;
+  }
+  d->src_y0 = d->cy0 + d->yf;
+  d->src_y1 = d->cy0 + d->yl;
+  d->src_x0 = d->cx0;
+  d->src_w = d->geo == kGeoZeros ? 0 : d->cw;
+  d->sub_bits = (int32_t)align_up((d->entropy_len * 8 + kDecodeThreads - 1) / kDecodeThreads, 32);
+  if (d->sub_bits < kMinSubBits) d->sub_bits = kMinSubBits;
+  d->nsub_cap = (int32_t)((d->entropy_len * 8 + d->sub_bits - 1) / d->sub_bits) + d->nseg + 1;
+  // scratch layout (relative offsets; k_plan adds the image base)
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    int64_t r = o;
+    o += align_up(bytes, 256);
+    return r;
+  };
+  d->off_ustream = take(d->entropy_len + kUPad);
+  d->ustream_cap = d->entropy_len + kUPad;
+  d->off_seg = take((int64_t)(d->nseg + 2) * 4);
+  d->off_sub = take((int64_t)d->nsub_cap * sizeof(SubState));
+  d->off_coef = take(d->total_blocks * 128);
+  int64_t planes = 0;
+  for (int c = 0; c < d->ncomp; c++) planes += align_up((int64_t)d->comp[c].pitch * d->comp[c].bh * 8, 256);
+  d->off_planes = take(planes);
+  d->off_rgb = take((int64_t)d->src_w * (d->src_y1 - d->src_y0) * 3);
+  d->off_tmp = take(d->need_h ? (int64_t)(d->yl - d->yf) * op.out_w * 3 : 0);
+  d->off_kh = take(d->need_h ? ((int64_t)2 * op.out_w + (int64_t)op.out_w * d->ksh) * 4 : 0);
+  d->off_kv = take(d->need_v ? ((int64_t)2 * op.out_h + (int64_t)op.out_h * d->ksv) * 4 : 0);
+  d->need = o;
+  return o;
+}
+
+__global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
+                                              const int32_t* __restrict__ lengths, sdsj_op op, ImgDesc* __restrict__ descs,
+                                              ImgTables* __restrict__ tables) {
+  const int img = blockIdx.x;
+  if (img >= n) return;
+  const int lane = threadIdx.x;
+  __shared__ uint8_t hdr[kHdrStage];
+  __shared__ ImgDesc sd;
+  __shared__ ImgTables st;
+  __shared__ int16_t huffsize[257];
+  __shared__ int32_t huffcode[257];
+  __shared__ int s_status;
+
+  const uint8_t* g = blob + offsets[img];
+  const int64_t len = lengths[img];
+  const int64_t nstage = len < kHdrStage ? len : kHdrStage;
+  for (int64_t i = lane; i < nstage; i += 64) hdr[i] = g[i];
+  __syncthreads();
+  if (lane == 0) {
+    DevReader rd{hdr, nstage, g};
+    int status = parse_headers(rd, len, &sd, &st);
+    if (status == SDSJ_OK) status = setup_geometry(&sd, &st);
+    if (status == SDSJ_OK) plan_image(&sd, op);
+    sd.status = status;
+    s_status = status;
+  }
+  __syncthreads();
+  if (s_status == SDSJ_OK) {
+    // Derived Huffman tables for every defined table (jdhuff.c jpeg_make_d_derived_tbl).
+    for (int tix = 0; tix < 8; tix++) {
+      const HuffSpec& hs = tix < 4 ? st.dc_spec[tix] : st.ac_spec[tix - 4];
+      HuffDerived& hd = tix < 4 ? st.dc[tix] : st.ac[tix - 4];
+      if (!hs.defined) continue;
+      if (lane == 0) {
+        int p = 0;
+        for (int l = 1; l <= 16; l++)
+          for (int i = 0; i < hs.bits[l]; i++) huffsize[p++] = (int16_t)l;
+        huffsize[p] = 0;
+        int code = 0, si = huffsize[0];
+        p = 0;
+        bool bad = false;
+        while (huffsize[p]) {
+          while (huffsize[p] == si) huffcode[p++] = code++;
+          if (code >= (1 << si)) bad = true;
+          code <<= 1;
+          si++;
+        }
+        p = 0;
+        for (int l = 1; l <= 16; l++) {
+          if (hs.bits[l]) {
+            hd.valoffset[l] = p - huffcode[p];
+            p += hs.bits[l];
+            hd.maxcode[l] = huffcode[p - 1];
+          } else {
+            hd.maxcode[l] = -1;
+            hd.valoffset[l] = 0;
+          }
+        }
+        hd.maxcode[0] = -1;
+        hd.valoffset[0] = 0;
+        hd.maxcode[17] = 0xFFFFF;
+        hd.valoffset[17] = 0;
+        huffsize[256] = (int16_t)p;  // symbol count
+        if (bad) s_status = SDSJ_CORRUPT;
+      }
+      __syncthreads();
+      for (int i = lane; i < (1 << kLutBits); i += 64) hd.lut[i] = 0;
+      for (int i = lane; i < 256; i += 64) hd.vals[i] = hs.vals[i];
+      __syncthreads();
+      const int nsym = huffsize[256];
+      for (int k = lane; k < nsym; k += 64) {
+        int l = huffsize[k];
+        if (l <= kLutBits) {
+          int base = huffcode[k] << (kLutBits - l);
+          int cnt = 1 << (kLutBits - l);
+          uint16_t e = (uint16_t)((l << 8) | hs.vals[k]);
+          for (int r = 0; r < cnt; r++) hd.lut[base + r] = e;
+        }
+      }
+      __syncthreads();
+    }
+    if (lane == 0) sd.status = s_status;
+  }
+  __syncthreads();
+  // write back
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&st);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&tables[img]);
+    for (int i = lane; i < (int)(sizeof(ImgTables) / 4); i += 64) dst[i] = src[i];
+    const uint32_t* s2 = reinterpret_cast<const uint32_t*>(&sd);
+    uint32_t* d2 = reinterpret_cast<uint32_t*>(&descs[img]);
+    for (int i = lane; i < (int)(sizeof(ImgDesc) / 4); i += 64) d2[i] = s2[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_plan: one workgroup; exclusive scan of per-image scratch needs -> absolute offsets.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ descs, int64_t capacity,
+                                               int64_t* __restrict__ total_out) {
+  __shared__ int64_t part[1024];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    int i = base + threadIdx.x;
+    int64_t need = 0;
+    if (i < n && descs[i].status == SDSJ_OK) need = descs[i].need;
+    part[threadIdx.x] = need;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      int64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    int64_t start = carry + part[threadIdx.x] - need;
+    if (i < n && descs[i].status == SDSJ_OK) {
+      ImgDesc& d = descs[i];
+      if (start + need > capacity) {
+        d.status = SDSJ_ECAPACITY;
+      } else {
+        d.off_ustream += start;
+        d.off_seg += start;
+        d.off_sub += start;
+        d.off_coef += start;
+        d.off_planes += start;
+        d.off_rgb += start;
+        d.off_tmp += start;
+        d.off_kh += start;
+        d.off_kv += start;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total_out = carry;
+}
+
+// ------------------------------------------------------------------------------------------
+// k_unstuff: one 256-thread workgroup per image.  Removes FF00 stuffing and fill bytes, splits at
+// RSTn markers and stops at the first other marker (jdhuff.c jpeg_fill_bit_buffer semantics).
+// Also zero-fills the image's coefficient area for k_entropy.
+// ------------------------------------------------------------------------------------------
+constexpr int kUnstuffThreads = 256;
+constexpr int kUnstuffBytes = 16;
+
+__device__ inline int block_excl_scan_256(int v, int* tmp, int* total) {
+  // Hillis-Steele in LDS; tmp has 256 ints.
+  const int t = threadIdx.x;
+  tmp[t] = v;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    int a = t >= off ? tmp[t - off] : 0;
+    __syncthreads();
+    tmp[t] += a;
+    __syncthreads();
+  }
+  int incl = tmp[t];
+  *total = tmp[255];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_t* __restrict__ blob,
+                                                             const int64_t* __restrict__ offsets,
+                                                             ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.x;
+  if (img >= n) return;
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK) return;
+  __shared__ int scan_tmp[256];
+  __shared__ int s_end;
+  const int t = threadIdx.x;
+  const uint8_t* e = blob + offsets[img] + d->entropy_off;
+  const int64_t L = d->entropy_len;
+  uint8_t* out = scratch + d->off_ustream;
+  int32_t* seg = reinterpret_cast<int32_t*>(scratch + d->off_seg);
+  const int nseg = d->nseg;
+
+  // zero the coefficient area (16 B per store)
+  {
+    uint4* cz = reinterpret_cast<uint4*>(scratch + d->off_coef);
+    const int64_t nz = d->total_blocks * 128 / 16;
+    for (int64_t i = t; i < nz; i += kUnstuffThreads) cz[i] = make_uint4(0, 0, 0, 0);
+  }
+  if (t == 0) seg[0] = 0;
+
+  int64_t out_pos = 0;
+  int rst_count = 0;
+  bool ended = false;
+  for (int64_t base = 0; base < L && !ended; base += kUnstuffThreads * kUnstuffBytes) {
+    if (t == 0) s_end = 0x7fffffff;
+    __syncthreads();
+    const int64_t my0 = base + (int64_t)t * kUnstuffBytes;
+    uint8_t b[kUnstuffBytes];
+    int prev = my0 > 0 && my0 - 1 < L ? e[my0 - 1] : 0;
+    int prev_first = prev;
+    uint32_t kind = 0;  // 2 bits per byte: 0 skip, 1 emit, 2 RST, 3 END
+    for (int k = 0; k < kUnstuffBytes; k++) {
+      int64_t i = my0 + k;
+      int c = i < L ? e[i] : -1;
+      int kd;
+      if (c < 0) kd = 3;
+      else if (prev == 0xFF) {
+        if (c == 0x00) { kd = 1; c = 0xFF; }
+        else if (c == 0xFF) kd = 0;
+        else if (c >= 0xD0 && c <= 0xD7) kd = 2;
+        else kd = 3;
+      } else {
+        kd = c == 0xFF ? 0 : 1;
+      }
+      b[k] = (uint8_t)c;
+      kind |= (uint32_t)kd << (2 * k);
+      prev = i < L ? e[i] : -1;
+    }
+    (void)prev_first;
+    // first END inside this tile
+    int my_end = 0x7fffffff;
+    for (int k = 0; k < kUnstuffBytes; k++)
+      if (((kind >> (2 * k)) & 3) == 3) { my_end = t * kUnstuffBytes + k; break; }
+    if (my_end != 0x7fffffff) atomicMin(&s_end, my_end);
+    __syncthreads();
+    const int tile_end = s_end;
+    int nemit = 0, nrst = 0;
+    for (int k = 0; k < kUnstuffBytes; k++) {
+      if (t * kUnstuffBytes + k >= tile_end) break;
+      int kd = (kind >> (2 * k)) & 3;
+      nemit += kd == 1;
+      nrst += kd == 2;
+    }
+    int emit_total, rst_total;
+    int emit_off = block_excl_scan_256(nemit, scan_tmp, &emit_total);
+    int rst_off = block_excl_scan_256(nrst, scan_tmp, &rst_total);
+    int64_t pos = out_pos + emit_off;
+    int r = rst_count + rst_off;
+    for (int k = 0; k < kUnstuffBytes; k++) {
+      if (t * kUnstuffBytes + k >= tile_end) break;
+      int kd = (kind >> (2 * k)) & 3;
+      if (kd == 1) out[pos++] = b[k];
+      else if (kd == 2) {
+        r++;
+        if (r < nseg) seg[r] = (int32_t)pos;
+      }
+    }
+    out_pos += emit_total;
+    rst_count += rst_total;
+    if (tile_end != 0x7fffffff) ended = true;
+    __syncthreads();
+  }
+  // zero pad after the stream so the bit reader can over-read safely
+  for (int k = t; k < kUPad; k += kUnstuffThreads) out[out_pos + k] = 0;
+  if (t == 0) {
+    seg[nseg] = (int32_t)out_pos;
+    d->ulen = out_pos;
+    d->useg_found = 1 + rst_count;
+    if (1 + rst_count < nseg) d->status = SDSJ_CORRUPT;  // missing restart markers
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_entropy: one 256-thread workgroup per image.  Self-synchronising parallel Huffman decoding:
+//   round 0   every subsequence decodes speculatively from its first bit (state: block 0, DC);
+//   rounds r  subsequence j re-decodes from the exit state of j-1 until all exits agree (Jacobi);
+//   scan      segmented exclusive scan of (blocks completed, DC sums) -> entry block / predictors;
+//   write     every subsequence decodes from its verified entry and scatters coefficients.
+// The decode of one symbol follows jdhuff.c decode_mcu exactly (HUFF_EXTEND, ZRL, EOB, k+r
+// overflow into jpeg_natural_order's guard entries, DC prediction per component).
+// ------------------------------------------------------------------------------------------
+struct LdsEntropy {
+  uint16_t lut[8][1 << kLutBits];
+  int32_t maxcode[8][18];
+  int32_t valoff[8][18];
+  uint8_t vals[8][256];
+  uint8_t blk_dc[kMaxBlocksPerMcu], blk_ac[kMaxBlocksPerMcu], blk_c[kMaxBlocksPerMcu];
+  int32_t scan[5][256];
+  int32_t flag[256];
+  int32_t changed;
+  int32_t nsub;
+  int32_t bad;
+};
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+struct BitReader {
+  const uint32_t* w;
+  uint64_t buf;
+  int nb;
+  uint32_t next;
+  __device__ __forceinline__ void init(uint32_t p) {
+    uint32_t wi = p >> 5;
+    int sh = p & 31;
+    uint64_t a = bswap32(w[wi]), b = bswap32(w[wi + 1]);
+    buf = ((a << 32) | b) << sh;
+    nb = 64 - sh;
+    next = wi + 2;
+  }
+  __device__ __forceinline__ void refill() {
+    if (nb <= 32) {
+      buf |= (uint64_t)bswap32(w[next++]) << (32 - nb);
+      nb += 32;
+    }
+  }
+  __device__ __forceinline__ uint32_t pos() const { return next * 32u - (uint32_t)nb; }
+};
+
+__device__ __forceinline__ int huff_extend(uint32_t x, int s) {
+  return (x < (1u << (s - 1))) ? (int)x + (int)((~0u << s) + 1u) : (int)x;
+}
+
+// Decodes symbols from `entry` until the next symbol would start at or after `end_bit`.
+// WRITE: scatter coefficients of blocks [g, g_end) to `coef`.
+template <bool WRITE>
+__device__ void decode_subseq(const LdsEntropy& L, const uint32_t* words, uint32_t entry_p, int blk, int z,
+                              uint32_t end_bit, int bpm, int* nblk_out, int* dc_out, uint32_t* exit_p, int* exit_blk,
+                              int* exit_z, int64_t g, int64_t g_end, const int* dc_pred_in, int16_t* coef, int* bad,
+                              uint32_t* done_p) {
+  BitReader br;
+  br.w = words;
+  br.init(entry_p);
+  int nblk = 0;
+  int dc0 = 0, dc1 = 0, dc2 = 0;
+  int pred0 = 0, pred1 = 0, pred2 = 0;
+  if (WRITE) {
+    pred0 = dc_pred_in[0];
+    pred1 = dc_pred_in[1];
+    pred2 = dc_pred_in[2];
+  }
+  int comp = L.blk_c[blk];
+  int tdc = L.blk_dc[blk], tac = L.blk_ac[blk];
+  while (br.pos() < end_bit) {
+    br.refill();
+    const uint32_t peek = (uint32_t)(br.buf >> 48);
+    const int tab = z == 0 ? tdc : tac;
+    const uint16_t e = L.lut[tab][peek >> (16 - kLutBits)];
+    int len = e >> 8;
+    int sym = e & 0xFF;
+    if (len == 0) {
+      int l = kLutBits + 1;
+      while (l <= 16 && (int32_t)(peek >> (16 - l)) > L.maxcode[tab][l]) l++;
+      if (l > 16) {
+        // bad code (JWRN_HUFF_BAD_CODE): only a verified decode of a real block counts
+        if (WRITE && g < g_end) *bad = 1;
+        len = 16;
+        sym = 0;
+      } else {
+        len = l;
+        sym = L.vals[tab][((int32_t)(peek >> (16 - l)) + L.valoff[tab][l]) & 0xFF];
+      }
+    }
+    br.buf <<= len;
+    br.nb -= len;
+    int s, r;
+    if (z == 0) {
+      s = sym;
+      r = 0;
+      if (s > 16) {
+        if (WRITE && g < g_end) *bad = 1;
+        s = 16;
+      }
+    } else {
+      s = sym & 15;
+      r = sym >> 4;
+    }
+    int val = 0;
+    if (s) {
+      uint32_t x = (uint32_t)(br.buf >> (64 - s));
+      br.buf <<= s;
+      br.nb -= s;
+      val = huff_extend(x, s);
+    }
+    if (z == 0) {
+      if (WRITE) {
+        int p;
+        if (comp == 0) p = (pred0 += val);
+        else if (comp == 1) p = (pred1 += val);
+        else p = (pred2 += val);
+        if (g < g_end) coef[g * 64] = (int16_t)p;
+      } else {
+        if (comp == 0) dc0 += val;
+        else if (comp == 1) dc1 += val;
+        else dc2 += val;
+      }
+      z = 1;
+    } else if (s) {
+      z += r;
+      if (WRITE && g < g_end) coef[g * 64 + natural_order(z)] = (int16_t)val;
+      z += 1;
+    } else if (r == 15) {
+      z += 16;
+    } else {
+      z = 64;
+    }
+    if (z >= 64) {
+      z = 0;
+      blk = blk + 1 == bpm ? 0 : blk + 1;
+      comp = L.blk_c[blk];
+      tdc = L.blk_dc[blk];
+      tac = L.blk_ac[blk];
+      nblk++;
+      if (WRITE) {
+        g++;
+        if (g == g_end) *done_p = br.pos();
+      }
+    }
+  }
+  *nblk_out = nblk;
+  dc_out[0] = dc0;
+  dc_out[1] = dc1;
+  dc_out[2] = dc2;
+  *exit_p = br.pos();
+  *exit_blk = blk;
+  *exit_z = z;
+}
+
+__global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __restrict__ descs,
+                                                            const ImgTables* __restrict__ tables,
+                                                            uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.x;
+  if (img >= n) return;
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK) return;
+  __shared__ LdsEntropy L;
+  const int t = threadIdx.x;
+  const ImgTables* tb = &tables[img];
+  for (int i = t; i < 8 * (1 << kLutBits); i += kDecodeThreads) {
+    int tix = i >> kLutBits, k = i & ((1 << kLutBits) - 1);
+    L.lut[tix][k] = tix < 4 ? tb->dc[tix].lut[k] : tb->ac[tix - 4].lut[k];
+  }
+  for (int i = t; i < 8 * 18; i += kDecodeThreads) {
+    int tix = i / 18, k = i % 18;
+    L.maxcode[tix][k] = tix < 4 ? tb->dc[tix].maxcode[k] : tb->ac[tix - 4].maxcode[k];
+    L.valoff[tix][k] = tix < 4 ? tb->dc[tix].valoffset[k] : tb->ac[tix - 4].valoffset[k];
+  }
+  for (int i = t; i < 8 * 256; i += kDecodeThreads) {
+    int tix = i >> 8, k = i & 255;
+    L.vals[tix][k] = tix < 4 ? tb->dc[tix].vals[k] : tb->ac[tix - 4].vals[k];
+  }
+  const int bpm = d->bpm;
+  if (t < bpm) {
+    int c = d->blk_comp[t];
+    L.blk_c[t] = (uint8_t)c;
+    L.blk_dc[t] = (uint8_t)d->comp[c].td;
+    L.blk_ac[t] = (uint8_t)(4 + d->comp[c].ta);
+  }
+  if (t == 0) {
+    L.bad = 0;
+    L.nsub = 0;
+  }
+  __syncthreads();
+
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
+  const int32_t* seg = reinterpret_cast<const int32_t*>(scratch + d->off_seg);
+  SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
+  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
+  const int nseg = d->nseg;
+  const uint32_t SB = (uint32_t)d->sub_bits;
+  const int64_t blocks_per_seg = d->restart_interval ? (int64_t)d->restart_interval * bpm : d->total_blocks;
+
+  // --- subsequence layout: segment s covers bytes [seg[s], seg[s+1]) of the unstuffed stream ---
+  // nsub_s = max(1, ceil(bits_s / SB)); exclusive scan over segments (tiles of 256)
+  {
+    int carry = 0;
+    for (int base = 0; base < nseg; base += kDecodeThreads) {
+      int s = base + t;
+      int cnt = 0;
+      uint32_t b0 = 0, b1 = 0;
+      if (s < nseg) {
+        b0 = (uint32_t)seg[s] * 8u;
+        b1 = (uint32_t)seg[s + 1] * 8u;
+        if (s + 1 < nseg && b1 < b0) b1 = b0;
+        cnt = b1 > b0 ? (int)((b1 - b0 + SB - 1) / SB) : 1;
+      }
+      int total;
+      int off = carry + block_excl_scan_256(cnt, L.scan[0], &total);
+      if (s < nseg) {
+        for (int k = 0; k < cnt; k++) {
+          int j = off + k;
+          if (j >= d->nsub_cap) break;
+          SubState& S = sub[j];
+          S.start_bit = b0 + (uint32_t)k * SB;
+          uint32_t e = S.start_bit + SB;
+          S.end_bit = e < b1 ? e : b1;
+          if (S.end_bit < S.start_bit) S.end_bit = S.start_bit;
+          S.first = k == 0;
+          S.seg = (uint16_t)s;
+        }
+      }
+      carry += total;
+    }
+    if (t == 0) L.nsub = carry < d->nsub_cap ? carry : d->nsub_cap;
+  }
+  __syncthreads();
+  const int nsub = L.nsub;
+  int bad = 0;
+
+  // --- round 0: speculative decode from each subsequence start ---
+  for (int j = t; j < nsub; j += kDecodeThreads) {
+    SubState& S = sub[j];
+    int nb, dc[3], eb, ez;
+    uint32_t ep, dp;
+    decode_subseq<false>(L, words, S.start_bit, 0, 0, S.end_bit, bpm, &nb, dc, &ep, &eb, &ez, 0, 0, nullptr,
+                         nullptr, &bad, &dp);
+    S.entry_p = S.start_bit;
+    S.entry_bz = 0;
+    S.exit_p = ep;
+    S.exit_bz = (uint16_t)((eb << 8) | ez);
+    S.nblk = nb;
+    S.dc[0] = dc[0];
+    S.dc[1] = dc[1];
+    S.dc[2] = dc[2];
+  }
+  __syncthreads();
+
+  // --- sync rounds (Jacobi): entry(j) <- exit(j-1) ---
+  for (int round = 0; round < 1 << 20; round++) {
+    if (t == 0) L.changed = 0;
+    __syncthreads();
+    // read phase: compute new values into the *2 fields
+    for (int j = t; j < nsub; j += kDecodeThreads) {
+      SubState& S = sub[j];
+      S.exit_p2 = S.exit_p;
+      S.exit_bz2 = S.exit_bz;
+      S.nblk2 = S.nblk;
+      S.dc2[0] = S.dc[0];
+      S.dc2[1] = S.dc[1];
+      S.dc2[2] = S.dc[2];
+      if (S.first) continue;
+      const SubState& P = sub[j - 1];
+      uint32_t ep = P.exit_p;
+      uint16_t ebz = P.exit_bz;
+      if (ep == S.entry_p && ebz == S.entry_bz) continue;
+      int nb, dc[3], eb, ez;
+      uint32_t xp, dp;
+      decode_subseq<false>(L, words, ep, ebz >> 8, ebz & 0xFF, S.end_bit, bpm, &nb, dc, &xp, &eb, &ez, 0, 0,
+                           nullptr, nullptr, &bad, &dp);
+      S.exit_p2 = xp;
+      S.exit_bz2 = (uint16_t)((eb << 8) | ez);
+      S.nblk2 = nb;
+      S.dc2[0] = dc[0];
+      S.dc2[1] = dc[1];
+      S.dc2[2] = dc[2];
+    }
+    __syncthreads();
+    // commit phase
+    for (int j = t; j < nsub; j += kDecodeThreads) {
+      SubState& S = sub[j];
+      if (!S.first) {
+        const SubState& P = sub[j - 1];
+        // entry becomes the predecessor's exit as read in this round (P.exit_p not yet committed:
+        // P's committed values are exit_p; the read phase used exit_p too)
+        S.entry_p = P.exit_p;
+        S.entry_bz = P.exit_bz;
+      }
+    }
+    __syncthreads();
+    for (int j = t; j < nsub; j += kDecodeThreads) {
+      SubState& S = sub[j];
+      if (S.exit_p2 != S.exit_p || S.exit_bz2 != S.exit_bz) L.changed = 1;
+      S.exit_p = S.exit_p2;
+      S.exit_bz = S.exit_bz2;
+      S.nblk = S.nblk2;
+      S.dc[0] = S.dc2[0];
+      S.dc[1] = S.dc2[1];
+      S.dc[2] = S.dc2[2];
+    }
+    __syncthreads();
+    if (!L.changed) break;
+    __syncthreads();
+  }
+
+  // --- segmented exclusive scan of (nblk, dc0, dc1, dc2) in subsequence order ---
+  // Stored into S.nblk2 (entry block index) and S.dc2 (entry DC predictors).
+  {
+    int carry[4] = {0, 0, 0, 0};
+    int carry_seg = -1;
+    for (int base = 0; base < nsub; base += kDecodeThreads) {
+      int j = base + t;
+      int v[4] = {0, 0, 0, 0};
+      int f = 1;
+      if (j < nsub) {
+        const SubState& S = sub[j];
+        v[0] = S.nblk;
+        v[1] = S.dc[0];
+        v[2] = S.dc[1];
+        v[3] = S.dc[2];
+        f = S.first;
+      }
+      // inclusive segmented scan (Hillis-Steele on (flag, value))
+      for (int q = 0; q < 4; q++) L.scan[q][t] = v[q];
+      L.flag[t] = f;
+      __syncthreads();
+      for (int off = 1; off < kDecodeThreads; off <<= 1) {
+        int a[4], af = 0;
+        bool take = t >= off;
+        if (take) {
+          for (int q = 0; q < 4; q++) a[q] = L.scan[q][t - off];
+          af = L.flag[t - off];
+        }
+        __syncthreads();
+        if (take && !L.flag[t]) {
+          for (int q = 0; q < 4; q++) L.scan[q][t] += a[q];
+        }
+        if (take) L.flag[t] |= af;
+        __syncthreads();
+      }
+      // exclusive value = inclusive - own; add the carry from previous tiles if no segment start
+      // occurred at or before this element inside the tile
+      if (j < nsub) {
+        SubState& S = sub[j];
+        int hit_start = L.flag[t];
+        int ex[4];
+        for (int q = 0; q < 4; q++) ex[q] = L.scan[q][t] - v[q] + (hit_start ? 0 : carry[q]);
+        if (S.first) {
+          for (int q = 0; q < 4; q++) ex[q] = 0;
+        }
+        int sidx = S.seg;
+        (void)sidx;
+        S.nblk2 = ex[0];
+        S.dc2[0] = ex[1];
+        S.dc2[1] = ex[2];
+        S.dc2[2] = ex[3];
+      }
+      __syncthreads();
+      // carry for the next tile: inclusive value of the last element
+      int last = kDecodeThreads - 1;
+      int any_start = L.flag[last];
+      for (int q = 0; q < 4; q++) carry[q] = L.scan[q][last] + (any_start ? 0 : carry[q]);
+      (void)carry_seg;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+
+  // --- write pass ---
+  for (int j = t; j < nsub; j += kDecodeThreads) {
+    const SubState& S = sub[j];
+    const int s = S.seg;
+    const int64_t gseg0 = (int64_t)s * blocks_per_seg;
+    int64_t gend = gseg0 + blocks_per_seg;
+    if (gend > d->total_blocks) gend = d->total_blocks;
+    const int64_t g = gseg0 + S.nblk2;
+    int nb, dc[3], eb, ez;
+    uint32_t xp, dp = 0;
+    const int pred[3] = {S.dc2[0], S.dc2[1], S.dc2[2]};
+    decode_subseq<true>(L, words, S.entry_p, S.entry_bz >> 8, S.entry_bz & 0xFF, S.end_bit, bpm, &nb, dc, &xp, &eb,
+                        &ez, g, gend, pred, coef, &bad, &dp);
+    // completeness: the last subsequence of each segment must reach the segment's block count
+    // using real (not padding) bits
+    const bool last_of_seg = (j + 1 == nsub) || sub[j + 1].first;
+    if (last_of_seg) {
+      if (g + nb < gend) bad = 1;
+      const uint32_t seg_end_bit = (uint32_t)seg[s + 1 <= nseg ? s + 1 : nseg] * 8u;
+      if (dp > seg_end_bit) bad = 1;
+    }
+  }
+  if (bad) atomicOr(&L.bad, 1);
+  __syncthreads();
+  if (t == 0) {
+    d->nsub = nsub;
+    if (L.bad) d->status = SDSJ_CORRUPT;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_idct: dequantisation + jpeg_idct_islow; 8 threads per block, 32 blocks per iteration.
+// ------------------------------------------------------------------------------------------
+constexpr int kIdctThreads = 256;
+constexpr int kIdctBlocks = kIdctThreads / 8;
+constexpr int kWsStride = 72;  // ints per block in LDS (conflict-free column reads per half-wave)
+
+#define SDSJ_FIX_0_298631336 2446
+#define SDSJ_FIX_0_390180644 3196
+#define SDSJ_FIX_0_541196100 4433
+#define SDSJ_FIX_0_765366865 6270
+#define SDSJ_FIX_0_899976223 7373
+#define SDSJ_FIX_1_175875602 9633
+#define SDSJ_FIX_1_501321110 12299
+#define SDSJ_FIX_1_847759065 15137
+#define SDSJ_FIX_1_961570560 16069
+#define SDSJ_FIX_2_053119869 16819
+#define SDSJ_FIX_2_562915447 20995
+#define SDSJ_FIX_3_072711026 25172
+
+// One 1-D ISLOW butterfly (even/odd parts, jidctint.c); inputs x0..x7, outputs scaled sums
+// before the final DESCALE: o[0..7].
+__device__ __forceinline__ void islow_1d(int x0, int x1, int x2, int x3, int x4, int x5, int x6, int x7, int o[8]) {
+  int z2 = x2, z3 = x6;
+  int z1 = (z2 + z3) * SDSJ_FIX_0_541196100;
+  int t2 = z1 + z3 * (-SDSJ_FIX_1_847759065);
+  int t3 = z1 + z2 * SDSJ_FIX_0_765366865;
+  int t0 = (x0 + x4) * (1 << 13);
+  int t1 = (x0 - x4) * (1 << 13);
+  int t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+  t0 = x7;
+  t1 = x5;
+  t2 = x3;
+  t3 = x1;
+  z1 = t0 + t3;
+  z2 = t1 + t2;
+  z3 = t0 + t2;
+  int z4 = t1 + t3;
+  int z5 = (z3 + z4) * SDSJ_FIX_1_175875602;
+  t0 *= SDSJ_FIX_0_298631336;
+  t1 *= SDSJ_FIX_2_053119869;
+  t2 *= SDSJ_FIX_3_072711026;
+  t3 *= SDSJ_FIX_1_501321110;
+  z1 *= -SDSJ_FIX_0_899976223;
+  z2 *= -SDSJ_FIX_2_562915447;
+  z3 *= -SDSJ_FIX_1_961570560;
+  z4 *= -SDSJ_FIX_0_390180644;
+  z3 += z5;
+  z4 += z5;
+  t0 += z1 + z3;
+  t1 += z2 + z4;
+  t2 += z2 + z3;
+  t3 += z1 + z4;
+  o[0] = t10 + t3;
+  o[7] = t10 - t3;
+  o[1] = t11 + t2;
+  o[6] = t11 - t2;
+  o[2] = t12 + t1;
+  o[5] = t12 - t1;
+  o[3] = t13 + t0;
+  o[4] = t13 - t0;
+}
+
+__device__ __forceinline__ uint32_t range_limit(int x) {
+  // IDCT_range_limit: (x & 1023) as a signed 10-bit value, + 128, clamped to [0, 255]
+  int s = ((x & 1023) ^ 512) - 512;
+  s += 128;
+  return (uint32_t)(s < 0 ? 0 : s > 255 ? 255 : s);
+}
+
+__global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __restrict__ descs,
+                                                       const ImgTables* __restrict__ tables,
+                                                       uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.y;
+  if (img >= n) return;
+  const ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
+  __shared__ int ws[kIdctBlocks * kWsStride];
+  __shared__ uint16_t qt[kMaxComp][64];
+  const int t = threadIdx.x;
+  for (int i = t; i < d->ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][i % 64];
+  __syncthreads();
+  const int lb = t >> 3, r = t & 7;
+  const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
+  uint8_t* planes = scratch + d->off_planes;
+  const int64_t nblocks = d->total_blocks;
+  const int bpm = d->bpm, mcux = d->mcux;
+  for (int64_t g0 = (int64_t)blockIdx.x * kIdctBlocks; g0 < nblocks; g0 += (int64_t)gridDim.x * kIdctBlocks) {
+    const int64_t g = g0 + lb;
+    const bool valid = g < nblocks;
+    int c = 0, bx = 0, by = 0;
+    if (valid) {
+      int64_t m = g / bpm;
+      int b = (int)(g - m * bpm);
+      c = d->blk_comp[b];
+      int mx = (int)(m % mcux), my = (int)(m / mcux);
+      if (d->ncomp == 1) {
+        bx = mx;
+        by = my;
+      } else {
+        bx = mx * d->comp[c].h + d->blk_dx[b];
+        by = my * d->comp[c].v + d->blk_dy[b];
+      }
+      // row r of the block, dequantised (DEQUANTIZE: coef * quantval)
+      const int16_t* cp = coef + g * 64 + r * 8;
+      uint4 raw = *reinterpret_cast<const uint4*>(cp);
+      int16_t v[8];
+      *reinterpret_cast<uint4*>(v) = raw;
+      for (int k = 0; k < 8; k++) ws[lb * kWsStride + r * 8 + k] = (int)v[k] * (int)qt[c][r * 8 + k];
+    }
+    __syncthreads();
+    // pass 1: column r
+    int col[8];
+    if (valid) {
+      int x[8];
+      for (int k = 0; k < 8; k++) x[k] = ws[lb * kWsStride + k * 8 + r];
+      if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
+        for (int k = 0; k < 8; k++) col[k] = x[0] * 4;  // << PASS1_BITS
+      } else {
+        int o[8];
+        islow_1d(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], o);
+        for (int k = 0; k < 8; k++) col[k] = (o[k] + (1 << 10)) >> 11;  // DESCALE(, CONST_BITS-PASS1_BITS)
+      }
+    }
+    __syncthreads();
+    if (valid)
+      for (int k = 0; k < 8; k++) ws[lb * kWsStride + k * 8 + r] = col[k];
+    __syncthreads();
+    // pass 2: row r
+    if (valid) {
+      const int* w = &ws[lb * kWsStride + r * 8];
+      int o[8];
+      islow_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+      uint32_t lo = 0, hi = 0;
+      for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
+      for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
+      const CompDesc& cd = d->comp[c];
+      uint8_t* dst = planes + cd.plane_off + (int64_t)(by * 8 + r) * cd.pitch + bx * 8;
+      *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_color: fancy upsampling (jdsample.c, context rows per jdmainct.c) + ycc_rgb_convert.
+// One thread per RGB pixel of rows [src_y0, src_y1) x cols [src_x0, src_x0 + src_w).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int up_sample(const uint8_t* P, const CompDesc& c, int x, int y) {
+  if (c.rh == 1 && c.rv == 1) return P[(int64_t)y * c.pitch + x];
+  const int dw = c.dw, dh = c.dh;
+  if (c.rv == 2) {
+    const int i = y >> 1;
+    int f = (y & 1) ? i + 1 : i - 1;
+    f = f < 0 ? 0 : (f > dh - 1 ? dh - 1 : f);
+    const uint8_t* r0 = P + (int64_t)i * c.pitch;
+    const uint8_t* r1 = P + (int64_t)f * c.pitch;
+    if (c.rh == 2) {
+      const int jx = x >> 1;
+      if (dw <= 2) return P[(int64_t)i * c.pitch + jx];  // h2v2_upsample (box)
+      const int cs = r0[jx] * 3 + r1[jx];
+      if ((x & 1) == 0) {
+        const int k = jx > 0 ? jx - 1 : 0;
+        const int cn = jx > 0 ? r0[k] * 3 + r1[k] : cs;
+        return (cs * 3 + cn + 8) >> 4;
+      } else {
+        const int k = jx < dw - 1 ? jx + 1 : dw - 1;
+        const int cn = jx < dw - 1 ? r0[k] * 3 + r1[k] : cs;
+        return (cs * 3 + cn + 7) >> 4;
+      }
+    }
+    // h1v2_fancy_upsample
+    return (r0[x] * 3 + r1[x] + ((y & 1) ? 2 : 1)) >> 2;
+  }
+  // rh == 2, rv == 1: h2v1
+  const uint8_t* row = P + (int64_t)y * c.pitch;
+  const int jx = x >> 1;
+  const int a = row[jx];
+  if (dw <= 2) return a;
+  if ((x & 1) == 0) return jx == 0 ? a : (a * 3 + row[jx - 1] + 1) >> 2;
+  return jx == dw - 1 ? a : (a * 3 + row[jx + 1] + 2) >> 2;
+}
+
+__device__ __forceinline__ uint32_t clamp255(int v) { return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+__device__ __forceinline__ void ycc_to_rgb(int y, int cb, int cr, uint32_t* r, uint32_t* g, uint32_t* b) {
+  // jdcolor.c tables evaluated arithmetically (identical integer results)
+  const int x_cb = cb - 128, x_cr = cr - 128;
+  const int cr_r = (91881 * x_cr + 32768) >> 16;
+  const int cb_b = (116130 * x_cb + 32768) >> 16;
+  const int g_add = (-46802 * x_cr + (-22554 * x_cb + 32768)) >> 16;
+  *r = clamp255(y + cr_r);
+  *g = clamp255(y + g_add);
+  *b = clamp255(y + cb_b);
+}
+
+__global__ void __launch_bounds__(256) k_color(int n, const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.y;
+  if (img >= n) return;
+  const ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
+  const int w = d->src_w, h = d->src_y1 - d->src_y0;
+  const int64_t total = (int64_t)w * h;
+  const uint8_t* planes = scratch + d->off_planes;
+  uint8_t* rgb = scratch + d->off_rgb;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int yy = (int)(i / w), xx = (int)(i - (int64_t)yy * w);
+    const int x = d->src_x0 + xx, y = d->src_y0 + yy;
+    uint32_t R, G, B;
+    const int Y = up_sample(planes + d->comp[0].plane_off, d->comp[0], x, y);
+    if (d->ncomp == 1) {
+      R = G = B = (uint32_t)Y;
+    } else {
+      const int cb = up_sample(planes + d->comp[1].plane_off, d->comp[1], x, y);
+      const int cr = up_sample(planes + d->comp[2].plane_off, d->comp[2], x, y);
+      ycc_to_rgb(Y, cb, cr, &R, &G, &B);
+    }
+    uint8_t* o = rgb + i * 3;
+    o[0] = (uint8_t)R;
+    o[1] = (uint8_t)G;
+    o[2] = (uint8_t)B;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_coeffs: Pillow precompute_coeffs + normalize_coeffs_8bpc for both passes (doubles).
+// ------------------------------------------------------------------------------------------
+__device__ double filt_eval(int filter, double x) {
+  switch (filter) {
+    case SDSJ_FILTER_BOX:
+      return (x > -0.5 && x <= 0.5) ? 1.0 : 0.0;
+    case SDSJ_FILTER_BILINEAR:
+      if (x < 0.0) x = -x;
+      return x < 1.0 ? 1.0 - x : 0.0;
+    case SDSJ_FILTER_HAMMING:
+      if (x < 0.0) x = -x;
+      if (x == 0.0) return 1.0;
+      if (x >= 1.0) return 0.0;
+      x = x * M_PI;
+      return sin(x) / x * (0.54 + 0.46 * cos(x));
+    case SDSJ_FILTER_BICUBIC: {
+      const double a = -0.5;
+      if (x < 0.0) x = -x;
+      if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+      if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+      return 0.0;
+    }
+    default: {
+      if (!(-3.0 <= x && x < 3.0)) return 0.0;
+      double s1 = x == 0.0 ? 1.0 : sin(x * M_PI) / (x * M_PI);
+      double x3 = x / 3;
+      double s2 = x3 == 0.0 ? 1.0 : sin(x3 * M_PI) / (x3 * M_PI);
+      return s1 * s2;
+    }
+  }
+}
+
+__device__ void coeffs_one(int in_size, int out_size, int filter, int ksize, int xx, int32_t* bounds, int32_t* kk) {
+  const double scale = (double)in_size / out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = filter_support(filter) * filterscale;
+  const double center = 0.0 + (xx + 0.5) * scale;
+  double ww = 0.0;
+  const double ss = 1.0 / filterscale;
+  int xmin = (int)(center - support + 0.5);
+  if (xmin < 0) xmin = 0;
+  int xmax = (int)(center + support + 0.5);
+  if (xmax > in_size) xmax = in_size;
+  xmax -= xmin;
+  double w[64];
+  int32_t* k = kk + (int64_t)xx * ksize;
+  // two passes: the weights are recomputed rather than stored when ksize > 64
+  for (int x = 0; x < xmax; x++) {
+    double v = filt_eval(filter, (x + xmin - center + 0.5) * ss);
+    if (x < 64) w[x] = v;
+    ww += v;
+  }
+  for (int x = 0; x < xmax; x++) {
+    double v = x < 64 ? w[x] : filt_eval(filter, (x + xmin - center + 0.5) * ss);
+    if (ww != 0.0) v /= ww;
+    double s = v * (double)(1 << 22);
+    k[x] = v < 0 ? (int32_t)(-0.5 + s) : (int32_t)(0.5 + s);
+  }
+  for (int x = xmax; x < ksize; x++) k[x] = 0;
+  bounds[2 * xx] = xmin;
+  bounds[2 * xx + 1] = xmax;
+}
+
+__global__ void __launch_bounds__(256) k_coeffs(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+                                                uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.y;
+  if (img >= n) return;
+  const ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || d->geo != kGeoResize) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d->need_h && i < op.out_w) {
+    int32_t* b = reinterpret_cast<int32_t*>(scratch + d->off_kh);
+    coeffs_one(d->cw, op.out_w, op.filter, d->ksh, i, b, b + 2 * op.out_w);
+  }
+  if (d->need_v && i < op.out_h) {
+    int32_t* b = reinterpret_cast<int32_t*>(scratch + d->off_kv);
+    coeffs_one(d->ch, op.out_h, op.filter, d->ksv, i, b, b + 2 * op.out_h);
+  }
+}
+
+__device__ __forceinline__ uint32_t clip8(int32_t v) {
+  v >>= 22;
+  return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_hpass: rows [yf, yl) of the crop, out_w columns; taps clamp to the crop window.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_hpass(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+                                               uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.y;
+  if (img >= n) return;
+  const ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || !d->need_h) return;
+  const int rows = d->yl - d->yf, ow = op.out_w;
+  const int64_t total = (int64_t)rows * ow;
+  const int32_t* bounds = reinterpret_cast<const int32_t*>(scratch + d->off_kh);
+  const int32_t* kk = bounds + 2 * ow;
+  const uint8_t* rgb = scratch + d->off_rgb;
+  uint8_t* tmp = scratch + d->off_tmp;
+  const int sw = d->src_w, ks = d->ksh;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int yy = (int)(i / ow), xx = (int)(i - (int64_t)yy * ow);
+    const int xmin = bounds[2 * xx], xmax = bounds[2 * xx + 1];
+    const int32_t* k = kk + (int64_t)xx * ks;
+    const uint8_t* row = rgb + ((int64_t)yy * sw + xmin) * 3;
+    int32_t s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+    for (int x = 0; x < xmax; x++) {
+      const int32_t c = k[x];
+      s0 += row[3 * x] * c;
+      s1 += row[3 * x + 1] * c;
+      s2 += row[3 * x + 2] * c;
+    }
+    uint8_t* o = tmp + i * 3;
+    o[0] = (uint8_t)clip8(s0);
+    o[1] = (uint8_t)clip8(s1);
+    o[2] = (uint8_t)clip8(s2);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_vpass: vertical pass (or copy) + hflip + CHW/HWC layout + uint8 / float32 LUT output.
+// Failed samples get zeros.  Also publishes the per-sample status.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_vpass(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+                                               const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
+                                               void* __restrict__ out, int32_t* __restrict__ status,
+                                               const float* __restrict__ lut) {
+  const int img = blockIdx.y;
+  if (img >= n) return;
+  const ImgDesc* d = &descs[img];
+  const int oh = op.out_h, ow = op.out_w;
+  const int64_t plane = (int64_t)oh * ow;
+  const int64_t total = plane;
+  const bool ok = d->status == SDSJ_OK;
+  if (blockIdx.x == 0 && threadIdx.x == 0) status[img] = d->status;
+  const bool zeros = !ok || d->geo == kGeoZeros;
+  const bool fl = flip ? flip[img] != 0 : false;
+  const bool f32 = op.out_dtype == SDSJ_DTYPE_F32;
+  const bool hwc = op.layout == SDSJ_LAYOUT_HWC;
+  uint8_t* o8 = reinterpret_cast<uint8_t*>(out) + (f32 ? 0 : img * plane * 3);
+  float* of = reinterpret_cast<float*>(out) + (f32 ? img * plane * 3 : 0);
+  // source: H-pass output (need_h) or the materialised RGB rows (crop columns)
+  const uint8_t* src = zeros ? nullptr : (d->need_h ? scratch + d->off_tmp : scratch + d->off_rgb);
+  const int sw = d->need_h ? ow : d->src_w;
+  const int32_t* bounds = d->need_v ? reinterpret_cast<const int32_t*>(scratch + d->off_kv) : nullptr;
+  const int32_t* kk = bounds ? bounds + 2 * oh : nullptr;
+  const int ks = d->ksv, yf = d->yf;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int yy = (int)(i / ow), xx = (int)(i - (int64_t)yy * ow);
+    uint32_t v0 = 0, v1 = 0, v2 = 0;
+    if (!zeros) {
+      if (d->need_v) {
+        const int ymin = bounds[2 * yy] - yf, ymax = bounds[2 * yy + 1];
+        const int32_t* k = kk + (int64_t)yy * ks;
+        int32_t s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+        for (int y = 0; y < ymax; y++) {
+          const uint8_t* p = src + ((int64_t)(y + ymin) * sw + xx) * 3;
+          const int32_t c = k[y];
+          s0 += p[0] * c;
+          s1 += p[1] * c;
+          s2 += p[2] * c;
+        }
+        v0 = clip8(s0);
+        v1 = clip8(s1);
+        v2 = clip8(s2);
+      } else {
+        const uint8_t* p = src + ((int64_t)yy * sw + xx) * 3;
+        v0 = p[0];
+        v1 = p[1];
+        v2 = p[2];
+      }
+    }
+    const int ox = fl ? ow - 1 - xx : xx;
+    const int64_t pix = (int64_t)yy * ow + ox;
+    if (f32) {
+      float* b = of;
+      if (hwc) {
+        b[pix * 3] = lut[v0];
+        b[pix * 3 + 1] = lut[v1];
+        b[pix * 3 + 2] = lut[v2];
+      } else {
+        b[pix] = lut[v0];
+        b[plane + pix] = lut[v1];
+        b[2 * plane + pix] = lut[v2];
+      }
+    } else {
+      uint8_t* b = o8;
+      if (hwc) {
+        b[pix * 3] = (uint8_t)v0;
+        b[pix * 3 + 1] = (uint8_t)v1;
+        b[pix * 3 + 2] = (uint8_t)v2;
+      } else {
+        b[pix] = (uint8_t)v0;
+        b[plane + pix] = (uint8_t)v1;
+        b[2 * plane + pix] = (uint8_t)v2;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Host-side launchers (called by the engine; all asynchronous on `stream`).
+// ------------------------------------------------------------------------------------------
+hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, const int32_t* lengths, const sdsj_op& op,
+                        ImgDesc* descs, ImgTables* tables, hipStream_t s) {
+  hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, offsets, lengths, op, descs, tables);
+  return hipGetLastError();
+}
+hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, hipStream_t s) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, n, descs, capacity, total);
+  return hipGetLastError();
+}
+hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_unstuff, dim3(n), dim3(kUnstuffThreads), 0, s, n, blob, offsets, descs, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_entropy(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
+  hipLaunchKernelGGL(k_entropy, dim3(n), dim3(kDecodeThreads), 0, s, n, descs, tables, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
+  hipLaunchKernelGGL(k_idct, dim3(64, n), dim3(kIdctThreads), 0, s, n, descs, tables, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, hipStream_t s) {
+  hipLaunchKernelGGL(k_color, dim3(64, n), dim3(256), 0, s, n, descs, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s) {
+  int mx = op.out_w > op.out_h ? op.out_w : op.out_h;
+  hipLaunchKernelGGL(k_coeffs, dim3((mx + 255) / 256, n), dim3(256), 0, s, n, descs, op, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_hpass(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s) {
+  hipLaunchKernelGGL(k_hpass, dim3(32, n), dim3(256), 0, s, n, descs, op, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_vpass(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
+                        void* out, int32_t* status, const float* lut, hipStream_t s) {
+  hipLaunchKernelGGL(k_vpass, dim3(32, n), dim3(256), 0, s, n, descs, op, scratch, flip, out, status, lut);
+  return hipGetLastError();
+}
+
+}  // namespace sdsj
+
+namespace sdsj {
+struct HostReader {
+  const uint8_t* p;
+  int operator()(int64_t i) const { return p[i]; }
+};
+
+int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status) {
+  ImgDesc d;
+  static thread_local ImgTables t;
+  HostReader rd{jpg};
+  int st = parse_headers(rd, n, &d, &t);
+  if (st == SDSJ_OK) st = setup_geometry(&d, &t);
+  int64_t need = 0;
+  if (st == SDSJ_OK) need = plan_image(&d, op);
+  *status = st;
+  return need;
+}
+}  // namespace sdsj

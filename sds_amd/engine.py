@@ -1,0 +1,187 @@
+"""Python handle over the native engine (include/sdsj.h): batched JPEG decode + crop/resize on MI355X.
+
+One engine per (process, device), created lazily on first use -- never in a parent process
+before a DataLoader fork (the reference runs transforms inside forked workers,
+sds/dataset.py:422-428 / README.md:283).  Outputs are torch tensors allocated by torch's caching
+allocator on the current HIP stream; the engine only owns its scratch.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import SdsjCfg, SdsjOp
+
+
+class ImageDecodeError(OSError):
+    """A sample the MI355X path could not decode (PIL raises OSError for such inputs)."""
+
+    def __init__(self, status: int, index: int = 0, msg: str = ""):
+        name = _lib.STATUS_NAMES.get(status, str(status))
+        super().__init__(msg or f"sample {index}: JPEG decode failed with status {name}")
+        self.status = status
+        self.index = index
+
+
+class UnsupportedImageError(ImageDecodeError):
+    """A valid image the MI355X path does not decode (progressive/arithmetic/12-bit JPEG, CMYK, PNG...)."""
+
+
+def raise_for_status(status: int, index: int = 0) -> None:
+    if status == _lib.OK:
+        return
+    if status == _lib.UNSUPPORTED:
+        raise UnsupportedImageError(status, index)
+    raise ImageDecodeError(status, index)
+
+
+def _device_index(device) -> int:
+    if device is None:
+        return torch.cuda.current_device()
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"the MI355X path needs a cuda (HIP) device, got {d}")
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
+class JpegEngine:
+    """Owns one native ``sdsj_engine`` bound to one HIP device."""
+
+    def __init__(self, device=None, max_batch: int = 4096, scratch_bytes: int = 0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("sds_amd needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.lib = _lib.load()
+        self.device = _device_index(device)
+        self.max_batch = int(max_batch)
+        cfg = SdsjCfg(_lib.SDSJ_ABI_VERSION, self.max_batch, int(scratch_bytes))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            st = self.lib.sdsj_engine_create(self.device, ctypes.byref(cfg), ctypes.byref(h))
+        if st != _lib.OK:
+            raise RuntimeError(f"sdsj_engine_create failed: {_lib.STATUS_NAMES.get(st, st)}")
+        self._h = h
+        self._pid = os.getpid()
+
+    # -- lifetime --------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value and self._pid == os.getpid():
+            self.lib.sdsj_engine_destroy(self._h)
+        self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != _lib.OK:
+            err = self.lib.sdsj_last_error(self._h)
+            raise RuntimeError(f"{what} failed ({_lib.STATUS_NAMES.get(rc, rc)}): {err.decode() if err else ''}")
+
+    # -- helpers ---------------------------------------------------------------------------
+    @staticmethod
+    def make_op(resolution, crop_before_resize=True, filter="bilinear", normalize=False, layout="chw") -> SdsjOp:
+        out_h, out_w = (int(v) for v in resolution)
+        if filter not in _lib.FILTERS:
+            raise NotImplementedError(f"interpolation mode {filter!r} is not implemented on the MI355X path")
+        lay = {"chw": _lib.LAYOUT_CHW, "hwc": _lib.LAYOUT_HWC}[layout.lower()]
+        return SdsjOp(out_h, out_w, int(bool(crop_before_resize)), _lib.FILTERS[filter],
+                      _lib.DTYPE_F32 if normalize else _lib.DTYPE_U8, lay)
+
+    def _alloc_out(self, n: int, op: SdsjOp) -> torch.Tensor:
+        shape = (n, 3, op.out_h, op.out_w) if op.layout == _lib.LAYOUT_CHW else (n, op.out_h, op.out_w, 3)
+        dtype = torch.float32 if op.out_dtype == _lib.DTYPE_F32 else torch.uint8
+        return torch.empty(shape, dtype=dtype, device=f"cuda:{self.device}")
+
+    # -- host-bytes batch ------------------------------------------------------------------
+    def decode_resize(self, jpgs: Sequence[bytes], resolution, *, crop_before_resize: bool = True,
+                      filter: str = "bilinear", normalize: bool = False, flip: Optional[Sequence[bool]] = None,
+                      layout: str = "chw", out: Optional[torch.Tensor] = None) -> tuple[torch.Tensor, np.ndarray]:
+        """Decodes host JPEG bytes into a [n, 3, H, W] (or [n, H, W, 3]) device tensor.
+
+        Returns (tensor, per-sample status array).  Failed samples are zero-filled; use
+        ``raise_for_status`` to turn a status into the reference's OSError semantics.
+        """
+        op = self.make_op(resolution, crop_before_resize, filter, normalize, layout)
+        n = len(jpgs)
+        if out is None:
+            out = self._alloc_out(n, op)
+        status = (ctypes.c_int32 * max(n, 1))()
+        if n == 0:
+            return out, np.zeros(0, np.int32)
+        ptrs = (ctypes.c_char_p * n)(*jpgs)
+        lens = (ctypes.c_size_t * n)(*[len(b) for b in jpgs])
+        flip_arr = None
+        if flip is not None:
+            flip_arr = (ctypes.c_uint8 * n)(*[1 if f else 0 for f in flip])
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = self.lib.sdsj_decode_resize_batch(self._h, n, ptrs, lens, ctypes.byref(op),
+                                                   ctypes.cast(flip_arr, ctypes.c_void_p) if flip_arr else None,
+                                                   ctypes.c_void_p(out.data_ptr()), status, ctypes.c_void_p(stream))
+        self._check(rc, "sdsj_decode_resize_batch")
+        return out, np.frombuffer(status, dtype=np.int32, count=n).copy()
+
+    # -- device-resident batch -------------------------------------------------------------
+    def decode_resize_device(self, blob: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor, resolution, *,
+                             crop_before_resize: bool = True, filter: str = "bilinear", normalize: bool = False,
+                             flip: Optional[torch.Tensor] = None, layout: str = "chw",
+                             out: Optional[torch.Tensor] = None,
+                             status: Optional[torch.Tensor] = None) -> tuple[torch.Tensor, torch.Tensor]:
+        """Decodes JPEGs already resident in device memory (uint8 ``blob``; int64 ``offsets`` and
+        int32 ``lengths`` per sample, both on the device).  Fully asynchronous on the current stream."""
+        op = self.make_op(resolution, crop_before_resize, filter, normalize, layout)
+        n = int(offsets.numel())
+        for t, dt in ((blob, torch.uint8), (offsets, torch.int64), (lengths, torch.int32)):
+            if t.device.type != "cuda" or t.dtype != dt or not t.is_contiguous():
+                raise ValueError("blob/offsets/lengths must be contiguous cuda tensors of uint8/int64/int32")
+        if out is None:
+            out = self._alloc_out(n, op)
+        if status is None:
+            status = torch.empty(n, dtype=torch.int32, device=f"cuda:{self.device}")
+        if flip is not None and (flip.dtype != torch.uint8 or flip.device.type != "cuda"):
+            raise ValueError("flip must be a cuda uint8 tensor")
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = self.lib.sdsj_decode_resize_batch_device(
+                self._h, n, ctypes.c_void_p(blob.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
+                ctypes.c_void_p(lengths.data_ptr()), ctypes.byref(op),
+                ctypes.c_void_p(flip.data_ptr()) if flip is not None else None, ctypes.c_void_p(out.data_ptr()),
+                ctypes.c_void_p(status.data_ptr()), ctypes.c_void_p(stream))
+        self._check(rc, "sdsj_decode_resize_batch_device")
+        return out, status
+
+    # -- diagnostics -----------------------------------------------------------------------
+    def set_timing(self, enable: bool) -> None:
+        self.lib.sdsj_engine_set_timing(self._h, int(bool(enable)))
+
+    def stage_times(self) -> dict[str, float]:
+        ms = (ctypes.c_float * 16)()
+        n = ctypes.c_int()
+        self._check(self.lib.sdsj_engine_stage_times(self._h, ms, 16, ctypes.byref(n)), "sdsj_engine_stage_times")
+        return {self.lib.sdsj_stage_name(k).decode(): float(ms[k]) for k in range(n.value)}
+
+
+_engines: dict[tuple[int, int], JpegEngine] = {}
+_engines_lock = threading.Lock()
+
+
+def get_engine(device=None) -> JpegEngine:
+    """The per-(process, device) engine, created on first use (fork-safe: keyed by pid)."""
+    idx = _device_index(device)
+    key = (os.getpid(), idx)
+    eng = _engines.get(key)
+    if eng is None:
+        with _engines_lock:
+            eng = _engines.get(key)
+            if eng is None:
+                eng = JpegEngine(idx)
+                _engines[key] = eng
+    return eng

@@ -1,0 +1,68 @@
+"""Host-side helpers of the image path (the parts of sds/transforms/functional.py that decide
+*what* to compute; the arithmetic itself runs in the HIP kernels)."""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+
+_RESIZE_KWARGS = {"crop_before_resize", "allow_vertical", "random_resize", "interpolation_mode"}
+
+
+def filter_name(mode) -> str:
+    """torchvision InterpolationMode (enum or its string value) -> engine filter name.
+
+    The reference resizes PIL images, so TVF.resize delegates to PIL.Image.resize with the same
+    filter; every Pillow separable filter is implemented.  NEAREST uses a different Pillow code
+    path and is not implemented."""
+    name = getattr(mode, "value", mode)
+    name = str(name).lower()
+    if name not in _lib.FILTERS:
+        raise NotImplementedError(f"interpolation_mode={mode!r} is not implemented on the MI355X path")
+    return name
+
+
+def check_resize_kwargs(kw: dict) -> None:
+    unknown = set(kw) - _RESIZE_KWARGS
+    if unknown:
+        raise TypeError(f"unexpected resize kwargs {sorted(unknown)} (lean_resize_frames, functional.py:42-50)")
+    filter_name(kw.get("interpolation_mode", "bilinear"))
+
+
+def image_size(data: bytes) -> tuple[int, int]:
+    """(width, height) from the JPEG header (host parse, sdsj_probe)."""
+    st, info = _lib.probe(data)
+    if info.width <= 0 or info.height <= 0:
+        from .engine import raise_for_status
+        raise_for_status(st if st != _lib.OK else _lib.CORRUPT)
+    return int(info.width), int(info.height)
+
+
+def target_resolution(w: int, h: int, resolution, allow_vertical: bool = False,
+                      random_resize: Optional[dict] = None) -> tuple[int, int]:
+    """functional.py:62-76: random downsampling choice (np global RNG) and vertical flip of the
+    target; returns (h_trg, w_trg)."""
+    is_originally_vertical = h > w
+    if random_resize is not None:
+        assert sum(random_resize.values()) == 1.0, f"Probabilities should sum to 1.0: {random_resize}"
+        random_resize = {k: v for k, v in random_resize.items() if k[0] <= w and k[1] <= h}
+        if len(random_resize) > 0:
+            resolutions, probs = zip(*random_resize.items())
+            resolution = resolutions[np.random.choice(len(resolutions), p=np.array(probs) / sum(probs))]
+    h_trg, w_trg = (max(resolution), min(resolution)) if is_originally_vertical and allow_vertical else resolution
+    return int(h_trg), int(w_trg)
+
+
+def crop_box(w: int, h: int, out_h: int, out_w: int) -> tuple[int, int, int, int]:
+    """functional.py:118-140 crop_to_aspect_ratio box (left, top, right, bottom)."""
+    cur = w / h
+    tgt = out_w / out_h
+    if cur > tgt:
+        nw = int(h * tgt)
+        left = (w - nw) // 2
+        return left, 0, left + nw, h
+    nh = int(w / tgt)
+    top = (h - nh) // 2
+    return 0, top, w, top + nh

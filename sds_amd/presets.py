@@ -1,0 +1,249 @@
+"""Drop-in image transform pipeline for sds.dataset.StreamingDataset, decoding on MI355X.
+
+Mirrors the reference's transform-callable API (sds/structs.py:68-69: ``Callable[[dict], dict]``)
+and its pipeline factory ``create_standard_image_pipeline`` (sds/transforms/presets.py:716-744):
+same signature (plus a keyword-only ``device``), same sample-dict routing (key set, order and
+values), but the decode/crop/resize/to-tensor/normalise steps run as one fused GPU transform that
+leaves a device tensor in ``sample[output_field]``.
+
+Transforms are plain picklable classes (presets.py:1-5): the native engine is created lazily in
+the process that first calls them (a DataLoader worker after fork), never pickled.
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import functional as F
+from .engine import get_engine, raise_for_status
+
+SampleData = dict  # sds/structs.py:68
+SampleTransform = Callable[[SampleData], Any]  # sds/structs.py:69
+
+
+# ------------------------------------------------------------------------------------------
+# Field validation / routing helpers (presets.py:393-415, :906-917), restated.
+# ------------------------------------------------------------------------------------------
+def is_dummy_field(d: dict, field: str, return_reason: bool = False):
+    """presets.py:393-415: absent, None, empty str/list/dict, float NaN or a tensor with NaN."""
+    is_dummy, reason = False, ""
+    if field not in d:
+        is_dummy, reason = True, f"Field '{field}' is absent."
+    elif d[field] is None:
+        is_dummy, reason = True, f"Field '{field}' is None."
+    elif isinstance(d[field], str) and d[field] == "":
+        is_dummy, reason = True, f"Field '{field}' is an empty string."
+    elif isinstance(d[field], (list, dict)) and len(d[field]) == 0:
+        is_dummy, reason = True, f"Field '{field}' is an empty {type(d[field]).__name__}."
+    elif isinstance(d[field], float) and np.isnan(d[field]):
+        is_dummy, reason = True, f"Field '{field}' is float and NaN."
+    elif isinstance(d[field], torch.Tensor) and torch.isnan(d[field]).any():
+        is_dummy, reason = True, f"Field '{field}' is a torch.Tensor and contains NaN values."
+    return (is_dummy, reason) if return_reason else is_dummy
+
+
+def _validate_fields(sample: SampleData, present, absent: Sequence[str], check_dummy_values: bool = False) -> None:
+    """presets.py:906-917."""
+    for field in present:
+        assert field in sample, f"Field '{field}' not found in sample with keys {list(sample.keys())}."
+        if check_dummy_values:
+            is_dummy, reason = is_dummy_field(sample, field, return_reason=True)
+            assert not is_dummy, f"Field '{field}' is dummy: {reason} Sample keys: {list(sample.keys())}."
+        if isinstance(present, dict) and present[field] is not None:
+            assert isinstance(sample[field], present[field]), \
+                f"Field '{field}' should be of type {present[field]}, but got {type(sample[field])}."
+    for field in absent:
+        assert field not in sample, f"Field '{field}' should not be present in sample with keys {list(sample.keys())}."
+
+
+class BaseTransform:
+    """presets.py:26-34."""
+
+    def __init__(self, input_field: str, output_field: Optional[str] = None, **transform_kwargs):
+        self.input_field = input_field
+        self.output_field = output_field if output_field is not None else input_field
+        self.transform_kwargs = transform_kwargs
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        raise NotImplementedError
+
+
+class LoadFromDiskTransform:
+    """presets.py:613-626: replaces each path field by the file's bytes, in place."""
+
+    def __init__(self, fields_to_load: Sequence[str], mode: str = "rb"):
+        assert len(fields_to_load) > 0, "At least one field must be specified to load from disk."
+        self.fields_to_load = fields_to_load
+        self.mode = mode
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        for field in self.fields_to_load:
+            assert field in sample, f"Column {field} not found in sample with keys {list(sample.keys())}."
+            with open(sample[field], self.mode) as f:
+                sample[field] = f.read()
+        return sample
+
+
+class GpuDecodeResizeImageTransform(BaseTransform):
+    """Fused replacement of DecodeImage -> ResizeImage -> ConvertImageToByteTensor [-> NormalizeFrames]
+    (presets.py:39-58, :68-74, :154-162) running on the GPU.
+
+    ``sample[output_field]`` becomes a device tensor [3, H, W] with the reference's exact values and
+    strides (HWC storage viewed as CHW, functional.py:104-108): uint8, or float32 ``x/127.5-1`` when
+    ``normalize``.  ``resize_kwargs`` are those of lean_resize_frames (functional.py:42-50):
+    crop_before_resize, allow_vertical, random_resize (np global RNG, same calls), interpolation_mode.
+    ``hflip_prob`` (extension, default 0) fuses README.md:99-108's HorizontalFlipTransform: the coin is
+    ``torch.rand(1) < hflip_prob`` from the global torch RNG, as that transform draws it.
+    """
+
+    def __init__(self, input_field: str, output_field: Optional[str] = None, resolution=(256, 256),
+                 normalize: bool = False, device=None, hflip_prob: float = 0.0, **resize_kwargs):
+        super().__init__(input_field, output_field)
+        self.resolution = tuple(int(v) for v in resolution)
+        assert len(self.resolution) == 2, f"Wrong resolution: {resolution}"
+        self.normalize = bool(normalize)
+        self.device = device
+        self.hflip_prob = float(hflip_prob)
+        self.resize_kwargs = dict(resize_kwargs)
+        F.check_resize_kwargs(self.resize_kwargs)
+
+    def __getstate__(self):
+        return dict(self.__dict__)  # no native handle is ever stored on the transform
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        _validate_fields(sample, present=[self.input_field], absent=[])
+        data = sample[self.input_field]
+        if not isinstance(data, (bytes, bytearray, memoryview)):
+            raise TypeError(f"Field '{self.input_field}' must hold encoded image bytes, got {type(data)}")
+        data = bytes(data)
+        kw = self.resize_kwargs
+        resolution = self.resolution
+        if kw.get("allow_vertical") or kw.get("random_resize") is not None:
+            w, h = F.image_size(data)
+            resolution = F.target_resolution(w, h, self.resolution, kw.get("allow_vertical", False),
+                                             kw.get("random_resize"))
+        flip = None
+        if self.hflip_prob > 0.0:
+            flip = [bool(torch.rand(1) < self.hflip_prob)]
+        eng = get_engine(self.device)
+        out, status = eng.decode_resize([data], resolution, crop_before_resize=kw.get("crop_before_resize", True),
+                                        filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),
+                                        normalize=self.normalize, flip=flip, layout="hwc")
+        raise_for_status(int(status[0]))
+        sample[self.output_field] = out[0].permute(2, 0, 1)  # [3, h, w] view of HWC storage
+        return sample
+
+
+class ReshapeImageAsVideoTransform(BaseTransform):
+    """presets.py:60-66 -> functional.py:88-92."""
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        _validate_fields(sample, present=[self.input_field], absent=[self.output_field])
+        image = sample[self.input_field]
+        assert len(image.shape) == 3, f"Wrong shape: {image.shape}."
+        sample[self.output_field] = image.unsqueeze(0)
+        return sample
+
+
+class NormalizeFramesTransform(BaseTransform):
+    """presets.py:154-162 (device-agnostic; runs on the GPU tensor)."""
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        _validate_fields(sample, present={self.input_field: torch.Tensor}, absent=[])
+        assert sample[self.input_field].dtype == torch.uint8, \
+            f"Expected input field '{self.input_field}' to be of type torch.uint8, but got {sample[self.input_field].dtype}."
+        sample[self.output_field] = sample[self.input_field].float() / 127.5 - 1.0
+        return sample
+
+
+class FieldsFilteringTransform:
+    """presets.py:628-644."""
+
+    def __init__(self, fields_to_keep: Optional[Sequence[str]] = None, fields_to_remove: Optional[Sequence[str]] = None):
+        assert fields_to_keep is not None or fields_to_remove is not None, \
+            "At least one of fields_to_keep or fields_to_remove must be provided."
+        self.fields_to_keep = fields_to_keep
+        self.fields_to_remove = fields_to_remove
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        if self.fields_to_remove is not None:
+            for field in self.fields_to_remove:
+                sample.pop(field, None)
+        if self.fields_to_keep is not None:
+            for field in list(sample.keys()):
+                if field not in self.fields_to_keep:
+                    sample.pop(field, None)
+        return sample
+
+
+class AugmentNewFieldsTransform:
+    """presets.py:646-656."""
+
+    def __init__(self, new_fields: dict):
+        self.new_fields = new_fields
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        for field, value in self.new_fields.items():
+            assert field not in sample, f"Field '{field}' already exists in sample with keys {list(sample.keys())}."
+            sample[field] = value
+        return sample
+
+
+class EnsureFieldsTransform:
+    """presets.py:670-686: presence/type/dummy checks; ``drop_others`` keeps whitelisted keys in order."""
+
+    def __init__(self, fields_whitelist, check_dummy_values: bool = False, drop_others: bool = False):
+        self.fields_whitelist = fields_whitelist
+        self.check_dummy_values = check_dummy_values
+        self.drop_others = drop_others
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        _validate_fields(sample, present=self.fields_whitelist, absent=[], check_dummy_values=self.check_dummy_values)
+        if self.drop_others:
+            for field in list(sample.keys()):
+                if field not in self.fields_whitelist:
+                    del sample[field]
+        return sample
+
+
+class HorizontalFlipTransform:
+    """README.md:99-108 / examples/iter_img2img.py:29-41 (user code there), device-agnostic."""
+
+    def __init__(self, image_field: str = "image"):
+        self.image_field = image_field
+
+    def __call__(self, sample: dict) -> dict:
+        assert self.image_field in sample, f"Image field is missing in the sample: {sample.keys()}"
+        img = sample[self.image_field]
+        assert isinstance(img, torch.Tensor) and img.ndim == 3 and img.shape[0] in (1, 3)
+        sample[self.image_field] = torch.flip(img, dims=[2]) if torch.rand(1) < 0.5 else img
+        return sample
+
+
+def create_standard_image_pipeline(
+    image_field: str,
+    resolution: tuple[int, int],
+    return_image_as_single_frame_video: bool = False,
+    normalize: bool = False,
+    resize_kwargs: dict = {},  # noqa: B006  (same default as the reference signature)
+    output_field: str = "image",
+    video_output_field: str = "video",
+    *,
+    device=None,
+    hflip_prob: float = 0.0,
+) -> Sequence[SampleTransform]:
+    """presets.py:716-744 with the decode/resize/to-tensor/normalise chain fused on the GPU."""
+    transforms: list = [
+        LoadFromDiskTransform([image_field]),
+        GpuDecodeResizeImageTransform(input_field=image_field, output_field=output_field, resolution=resolution,
+                                      normalize=normalize, device=device, hflip_prob=hflip_prob, **resize_kwargs),
+    ]
+    if return_image_as_single_frame_video:
+        transforms.extend([
+            ReshapeImageAsVideoTransform(input_field=output_field, output_field=video_output_field),
+            FieldsFilteringTransform(fields_to_remove=[output_field]),
+            AugmentNewFieldsTransform(new_fields=dict(framerate=960.0)),
+        ])
+    return transforms

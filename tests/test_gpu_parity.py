@@ -1,0 +1,161 @@
+"""GPU parity of the MI355X path against the reference's golden vectors and the C oracle.
+
+Every comparison is bit-exact (the decode, resize and routing steps are integer; the normalise
+step is a 256-entry float32 table equal to the reference's ``x.float()/127.5 - 1``, so it is
+bit-exact too: tolerance 0).  All calls go through the C-ABI (libsdsj.so via sds_amd).
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402  (checker only)
+from tests import goldens as G  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def engine():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sds_amd.engine import JpegEngine
+    return JpegEngine(max_batch=512)
+
+
+def _status(engine, jpg):
+    _, st = engine.decode_resize([jpg], (8, 8))
+    return int(st[0])
+
+
+G1 = list(G.g1())
+
+
+@pytest.mark.parametrize("case,jpg,arrs", G1, ids=[c["name"] for c, _, _ in G1])
+def test_g1_golden(engine, case, jpg, arrs):
+    from sds_amd import _lib
+    name = case["name"]
+    if case["decode"] != "ok":
+        assert _status(engine, jpg) == _lib.CORRUPT
+        return
+    if name.startswith("progressive"):
+        assert _status(engine, jpg) == _lib.UNSUPPORTED
+        return
+    w, h = case["size"]
+    # full-resolution decode = same-size shortcut (functional.py:78-80)
+    full, st = engine.decode_resize([jpg], (h, w), layout="hwc")
+    assert st[0] == 0
+    np.testing.assert_array_equal(full[0].cpu().numpy(), arrs["rgb"])
+    for key, out in case["outputs"].items():
+        res = tuple(int(v) for v in key.split("x"))
+        got, st = engine.decode_resize([jpg], res)
+        assert st[0] == 0
+        np.testing.assert_array_equal(got[0].cpu().numpy(), arrs[f"out_{key}"])
+        gn, st = engine.decode_resize([jpg], res, normalize=True)
+        assert G.sha(gn[0].cpu().numpy()) == out["norm_sha256"]
+
+
+def test_g1_as_one_batch(engine):
+    """All decodable G1 cases in one launch at 48x64 (mixed sizes/samplings/restarts in a batch)."""
+    cases = [(c, j, a) for c, j, a in G1 if c["decode"] == "ok" and not c["name"].startswith("progressive")]
+    got, st = engine.decode_resize([j for _, j, _ in cases], (48, 64))
+    assert (st == 0).all()
+    for k, (c, j, a) in enumerate(cases):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), a["out_48x64"], err_msg=c["name"])
+
+
+def test_g2_synthetic_vga_batch(engine):
+    meta, jpgs = G.g2_jpegs()
+    got, st = engine.decode_resize(jpgs, (256, 256))
+    assert (st == 0).all()
+    gf, st = engine.decode_resize(jpgs, (256, 256), normalize=True)
+    full0 = np.load(os.path.join(G.GOLDEN, "g2_full0.npy"))
+    np.testing.assert_array_equal(got[0].cpu().numpy(), full0)
+    for k, im in enumerate(meta["images"]):
+        assert G.sha(got[k].cpu().numpy()) == im["u8_256_sha256"]
+        assert G.sha(gf[k].cpu().numpy()) == im["f32_256_sha256"]
+
+
+def test_g3_mixed_flip_normalize(engine):
+    meta, jpgs = G.g3_jpegs()
+    flips = [im["flip"] for im in meta["images"]]
+    got, st = engine.decode_resize(jpgs, (512, 512), flip=flips)
+    assert (st == 0).all()
+    gf, _ = engine.decode_resize(jpgs, (512, 512), flip=flips, normalize=True)
+    for k, im in enumerate(meta["images"]):
+        assert G.sha(got[k].cpu().numpy()) == im["u8_512_sha256"], k
+        assert G.sha(gf[k].cpu().numpy()) == im["f32_512_sha256"], k
+
+
+def test_device_resident_api_matches_host_api(engine):
+    _, jpgs = G.g2_jpegs()
+    host, _ = engine.decode_resize(jpgs, (256, 256))
+    lens = [len(j) for j in jpgs]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    blob = torch.from_numpy(np.frombuffer(b"".join(jpgs), np.uint8).copy()).cuda()
+    out, st = engine.decode_resize_device(blob, torch.from_numpy(offs).cuda(),
+                                          torch.tensor(lens, dtype=torch.int32).cuda(), (256, 256))
+    assert (st.cpu() == 0).all()
+    assert torch.equal(out, host)
+
+
+def test_hwc_layout_and_flip(engine):
+    _, jpgs = G.g2_jpegs()
+    chw, _ = engine.decode_resize(jpgs[:2], (96, 128))
+    hwc, _ = engine.decode_resize(jpgs[:2], (96, 128), layout="hwc", flip=[True, False])
+    assert torch.equal(hwc[0].permute(2, 0, 1), torch.flip(chw[0], dims=[2]))
+    assert torch.equal(hwc[1].permute(2, 0, 1), chw[1])
+
+
+def _random_jpegs(seed: int, n: int):
+    from tests.golden.synth import encode_jpeg, synth_rgb
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        w, h = int(rng.integers(1, 300)), int(rng.integers(1, 300))
+        rgb = rng.integers(0, 256, (h, w, 3), dtype=np.uint8) if i % 2 else synth_rgb(rng, w, h)
+        kw = dict(quality=int(rng.integers(5, 101)))
+        if i % 5 == 0:
+            from PIL import Image
+            rgb = np.array(Image.fromarray(rgb).convert("L"))
+        else:
+            kw["subsampling"] = int(rng.integers(0, 3))
+        r = rng.random()
+        if r < 0.2:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 6))
+        elif r < 0.35:
+            kw["restart_marker_rows"] = int(rng.integers(1, 3))
+        if rng.random() < 0.25:
+            kw["optimize"] = True
+        out.append(encode_jpeg(rgb, **kw))
+    return out
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_random_batch_vs_oracle(engine, seed):
+    jpgs = _random_jpegs(seed, 64)
+    rng = np.random.default_rng(seed + 100)
+    res = (int(rng.integers(1, 200)), int(rng.integers(1, 200)))
+    got, st = engine.decode_resize(jpgs, res)
+    assert (st == 0).all()
+    for k, j in enumerate(jpgs):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res), err_msg=f"image {k}")
+
+
+@pytest.mark.parametrize("filt", ["box", "bicubic", "hamming", "lanczos"])
+def test_other_pillow_filters(engine, filt):
+    _, jpgs = G.g2_jpegs()
+    got, st = engine.decode_resize(jpgs[:2], (200, 150), filter=filt)
+    for k in range(2):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(jpgs[k], (200, 150), filter=filt))
+
+
+def test_4k_vs_oracle(engine):
+    from tests.golden.synth import encode_jpeg, synth_rgb
+    rng = np.random.default_rng(5)
+    jpg = encode_jpeg(synth_rgb(rng, 3840, 2160), 90)
+    got, st = engine.decode_resize([jpg], (512, 512), flip=[True])
+    assert st[0] == 0
+    np.testing.assert_array_equal(got[0].cpu().numpy(), O.pipeline(jpg, (512, 512), flip=True))
