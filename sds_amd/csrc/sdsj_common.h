@@ -97,6 +97,10 @@ struct ImgDesc {
   int32_t nsub;         // actual subsequences (set by the entropy kernel)
   int32_t useg_found;   // segments found by the unstuff kernel
   int64_t ulen;         // unstuffed entropy bytes
+  // entropy-kernel statistics (diagnostics): sync rounds, symbols decoded per phase
+  int32_t sync_rounds;
+  int32_t pad0;
+  int64_t sym_spec, sym_sync, sym_write;
 };
 
 // Entropy decoder state at a subsequence boundary (Weissenberger & Schmidt style self-sync).

@@ -396,6 +396,8 @@ struct LdsEntropy {
   int32_t changed;
   int32_t nsub;
   int32_t bad;
+  int32_t rounds;
+  unsigned long long sym[3];
 };
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
@@ -429,7 +431,7 @@ __device__ __forceinline__ int huff_extend(uint32_t x, int s) {
 // Decodes symbols from `entry` until the next symbol would start at or after `end_bit`.
 // WRITE: scatter coefficients of blocks [g, g_end) to `coef`.
 template <bool WRITE>
-__device__ void decode_subseq(const LdsEntropy& L, const uint32_t* words, uint32_t entry_p, int blk, int z,
+__device__ int decode_subseq(const LdsEntropy& L, const uint32_t* words, uint32_t entry_p, int blk, int z,
                               uint32_t end_bit, int bpm, int* nblk_out, int* dc_out, uint32_t* exit_p, int* exit_blk,
                               int* exit_z, int64_t g, int64_t g_end, const int* dc_pred_in, int16_t* coef, int* bad,
                               uint32_t* done_p) {
@@ -446,7 +448,9 @@ __device__ void decode_subseq(const LdsEntropy& L, const uint32_t* words, uint32
   }
   int comp = L.blk_c[blk];
   int tdc = L.blk_dc[blk], tac = L.blk_ac[blk];
+  int nsym = 0;
   while (br.pos() < end_bit) {
+    nsym++;
     br.refill();
     const uint32_t peek = (uint32_t)(br.buf >> 48);
     const int tab = z == 0 ? tdc : tac;
@@ -529,6 +533,7 @@ __device__ void decode_subseq(const LdsEntropy& L, const uint32_t* words, uint32
   *exit_p = br.pos();
   *exit_blk = blk;
   *exit_z = z;
+  return nsym;
 }
 
 __global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __restrict__ descs,
@@ -564,6 +569,8 @@ __global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __re
   if (t == 0) {
     L.bad = 0;
     L.nsub = 0;
+    L.rounds = 0;
+    L.sym[0] = L.sym[1] = L.sym[2] = 0;
   }
   __syncthreads();
 
@@ -611,14 +618,16 @@ __global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __re
   __syncthreads();
   const int nsub = L.nsub;
   int bad = 0;
+  int spec_bad = 0;  // invalid codes met while decoding from unverified states are expected
+  unsigned long long nsym_spec = 0, nsym_sync = 0, nsym_write = 0;
 
   // --- round 0: speculative decode from each subsequence start ---
   for (int j = t; j < nsub; j += kDecodeThreads) {
     SubState& S = sub[j];
     int nb, dc[3], eb, ez;
     uint32_t ep, dp;
-    decode_subseq<false>(L, words, S.start_bit, 0, 0, S.end_bit, bpm, &nb, dc, &ep, &eb, &ez, 0, 0, nullptr,
-                         nullptr, &bad, &dp);
+    nsym_spec += decode_subseq<false>(L, words, S.start_bit, 0, 0, S.end_bit, bpm, &nb, dc, &ep, &eb, &ez, 0, 0,
+                                      nullptr, nullptr, &spec_bad, &dp);
     S.entry_p = S.start_bit;
     S.entry_bz = 0;
     S.exit_p = ep;
@@ -650,8 +659,8 @@ __global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __re
       if (ep == S.entry_p && ebz == S.entry_bz) continue;
       int nb, dc[3], eb, ez;
       uint32_t xp, dp;
-      decode_subseq<false>(L, words, ep, ebz >> 8, ebz & 0xFF, S.end_bit, bpm, &nb, dc, &xp, &eb, &ez, 0, 0,
-                           nullptr, nullptr, &bad, &dp);
+      nsym_sync += decode_subseq<false>(L, words, ep, ebz >> 8, ebz & 0xFF, S.end_bit, bpm, &nb, dc, &xp, &eb,
+                                        &ez, 0, 0, nullptr, nullptr, &spec_bad, &dp);
       S.exit_p2 = xp;
       S.exit_bz2 = (uint16_t)((eb << 8) | ez);
       S.nblk2 = nb;
@@ -683,6 +692,7 @@ __global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __re
       S.dc[2] = S.dc2[2];
     }
     __syncthreads();
+    if (t == 0) L.rounds++;
     if (!L.changed) break;
     __syncthreads();
   }
@@ -761,8 +771,8 @@ __global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __re
     int nb, dc[3], eb, ez;
     uint32_t xp, dp = 0;
     const int pred[3] = {S.dc2[0], S.dc2[1], S.dc2[2]};
-    decode_subseq<true>(L, words, S.entry_p, S.entry_bz >> 8, S.entry_bz & 0xFF, S.end_bit, bpm, &nb, dc, &xp, &eb,
-                        &ez, g, gend, pred, coef, &bad, &dp);
+    nsym_write += decode_subseq<true>(L, words, S.entry_p, S.entry_bz >> 8, S.entry_bz & 0xFF, S.end_bit, bpm, &nb,
+                                      dc, &xp, &eb, &ez, g, gend, pred, coef, &bad, &dp);
     // completeness: the last subsequence of each segment must reach the segment's block count
     // using real (not padding) bits
     const bool last_of_seg = (j + 1 == nsub) || sub[j + 1].first;
@@ -773,9 +783,16 @@ __global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __re
     }
   }
   if (bad) atomicOr(&L.bad, 1);
+  atomicAdd(&L.sym[0], nsym_spec);
+  atomicAdd(&L.sym[1], nsym_sync);
+  atomicAdd(&L.sym[2], nsym_write);
   __syncthreads();
   if (t == 0) {
     d->nsub = nsub;
+    d->sync_rounds = L.rounds;
+    d->sym_spec = (int64_t)L.sym[0];
+    d->sym_sync = (int64_t)L.sym[1];
+    d->sym_write = (int64_t)L.sym[2];
     if (L.bad) d->status = SDSJ_CORRUPT;
   }
 }

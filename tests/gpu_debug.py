@@ -31,7 +31,8 @@ class ImgDescC(ctypes.Structure):
                                    "src_y0", "src_y1", "src_x0", "src_w", "sub_bits", "nsub_cap")] + \
                [(n, i64) for n in ("off_ustream", "ustream_cap", "off_seg", "off_sub", "off_coef", "off_planes",
                                    "off_rgb", "off_tmp", "off_kh", "off_kv", "need")] + \
-               [("nsub", i32), ("useg_found", i32), ("ulen", i64)]
+               [("nsub", i32), ("useg_found", i32), ("ulen", i64), ("sync_rounds", i32), ("pad0", i32),
+                ("sym_spec", i64), ("sym_sync", i64), ("sym_write", i64)]
 
 
 def _memcpy_d2h(ptr: int, nbytes: int) -> np.ndarray:

@@ -1,0 +1,25 @@
+"""Prints entropy-kernel statistics (sync rounds, symbols per phase) for a batch of synthetic VGA JPEGs."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from sds_amd.engine import JpegEngine  # noqa: E402
+from tests.golden.synth import synth_jpegs  # noqa: E402
+from tests.gpu_debug import snapshot  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+jpgs = synth_jpegs(n, seed=99)
+eng = JpegEngine(max_batch=n)
+out, st = eng.decode_resize(jpgs, (256, 256))
+descs, _ = snapshot(eng, n)
+r = np.array([d.sync_rounds for d in descs])
+sp = np.array([d.sym_spec for d in descs])
+sy = np.array([d.sym_sync for d in descs])
+wr = np.array([d.sym_write for d in descs])
+ns = np.array([d.nsub for d in descs])
+print(f"images={n} status_ok={(st == 0).all()} nsub mean={ns.mean():.1f} bits/sub={descs[0].sub_bits}")
+print(f"sync rounds: mean={r.mean():.2f} max={r.max()} hist={np.bincount(r).tolist()}")
+print(f"symbols/image: spec={sp.mean():.0f} sync={sy.mean():.0f} write={wr.mean():.0f} "
+      f"-> {(sp + sy + wr).mean() / wr.mean():.2f}x the write pass")
