@@ -121,7 +121,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
-    from sds_amd.distributed import compute_index_slice
+    from sds_amd.distributed import compute_index_slice, max_over_ranks
     from sds_amd.engine import JpegEngine
 
     workers = max(1, min(16, host_cores()) // max(1, world))
@@ -193,11 +193,7 @@ def main():
     barrier()
     stages = eng.stage_times()  # summed over the timed steps (HIP events on the launch stream)
     eng.set_timing(False)
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(t1 - t0, device=dev)
     imgs = B * args.steps * world
     value = imgs / elapsed
     if args.profile_steps and rank == 0:

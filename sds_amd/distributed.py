@@ -21,3 +21,14 @@ def env_rank() -> tuple[int, int, int]:
     """(rank, world_size, local_rank) from the torch.distributed.run environment."""
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
             int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Maximum of a per-rank scalar (the bench's timed region), via all_reduce(MAX)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
