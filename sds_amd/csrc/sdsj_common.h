@@ -8,7 +8,7 @@
 #pragma once
 #include <stdint.h>
 
-#include "../../include/sdsj.h"
+#include "sdsj.h"
 
 #if defined(__HIPCC__)
 #define SDSJ_HD __host__ __device__
@@ -20,10 +20,11 @@ namespace sdsj {
 
 constexpr int kMaxComp = 3;
 constexpr int kMaxBlocksPerMcu = 10;  // D_MAX_BLOCKS_IN_MCU
-constexpr int kLutBits = 9;           // first-level Huffman lookup width
+constexpr int kLutBits = 11;          // Huffman lookup width built by k_parse (99.7% of code lengths)
+constexpr int kRec = 64;              // block-boundary records kept per subsequence by k_entsync
 constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
-constexpr int kUPad = 64;             // zero bytes after each unstuffed stream
+constexpr int kUPad = 128;            // zero bytes after each unstuffed stream (bit-reader prefetch)
 
 // Raw DHT content (bits[1..16], huffval) -- jdmarker.c get_dht.
 struct HuffSpec {
@@ -38,7 +39,7 @@ struct HuffSpec {
 struct HuffDerived {
   int32_t maxcode[18];    // maxcode[l] for l = 1..16, maxcode[17] sentinel
   int32_t valoffset[18];
-  uint16_t lut[1 << kLutBits];  // (len << 8) | symbol, len = 0 -> slow path
+  uint16_t lut[1 << kLutBits];  // len | size << 4 | run << 8 (len = 0 -> slow path)
   uint8_t vals[256];
 };
 
@@ -88,6 +89,7 @@ struct ImgDesc {
   int64_t off_ustream, ustream_cap;
   int64_t off_seg;      // int32 [nseg + 2]: segment start bytes, then the stream length
   int64_t off_sub;      // SubState [nsub_cap]
+  int64_t off_rec;      // SyncRec [nsub_cap][kRec]
   int64_t off_coef;     // int16 [total_blocks * 64]
   int64_t off_planes;
   int64_t off_rgb;      // uint8 RGB rows [src_y0, src_y1) x [src_x0, src_x0 + src_w)
@@ -101,25 +103,32 @@ struct ImgDesc {
   int32_t sync_rounds;
   int32_t pad0;
   int64_t sym_spec, sym_sync, sym_write;
+  // lane utilisation / phase timing diagnostics (s_memtime ticks, wave-loop iterations x 64)
+  int64_t t_spec, t_sync, t_scan, t_write;
+  int64_t it_spec, it_sync, it_write;
 };
 
-// Entropy decoder state at a subsequence boundary (Weissenberger & Schmidt style self-sync).
+// Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).
+// State at a symbol boundary = (bit position p, MCU block index blk, zig-zag index z); bz packs
+// (blk << 8) | z.  "spec" = the speculative decode from the subsequence's first bit, "cur" = the
+// decode from the current entry estimate; after k_entsync, entry is verified and nblk_ex / dc_ex
+// hold the exclusive (segmented) prefix of blocks and DC differences before the entry.
 struct SubState {
-  uint32_t entry_p;   // bit position of the first symbol decoded (entry state)
-  uint32_t exit_p;    // bit position after the last symbol that starts inside the subsequence
-  uint32_t exit_p2;   // double buffer for the sync rounds
-  uint16_t entry_bz;  // (blk << 8) | z
-  uint16_t exit_bz;
-  uint16_t exit_bz2;
-  uint16_t seg;       // segment id (low 16 bits; diagnostics only)
-  uint32_t start_bit; // first bit of the subsequence
-  uint32_t end_bit;   // one past its last bit
-  int32_t nblk;       // blocks completed while decoding it from the entry state
-  int32_t dc[kMaxComp];
-  int32_t nblk2;
-  int32_t dc2[kMaxComp];
-  int32_t first;      // 1 if it starts a segment (entry state known exactly)
-  int32_t pad;
+  uint32_t start_bit, end_bit;
+  uint32_t entry_p, cur_exit_p, spec_exit_p, new_exit_p, new_entry_p, res_p;
+  uint16_t entry_bz, cur_exit_bz, spec_exit_bz, new_exit_bz, new_entry_bz, res_bz;
+  int32_t cur_nblk, spec_nblk, new_nblk, nrec, res_nblk, res_ri;
+  int32_t cur_dc[kMaxComp], spec_dc[kMaxComp], new_dc[kMaxComp], res_dc[kMaxComp], res_q[kMaxComp];
+  int32_t nblk_ex, dc_ex[kMaxComp];
+  int32_t first, seg;
+};
+
+// One block boundary met by the speculative decode (for early sync detection).
+struct SyncRec {
+  uint32_t p;       // bit position after the block's last symbol
+  int16_t dc;       // DC difference decoded for that block
+  uint8_t blk;      // MCU block index of the completed block
+  uint8_t pad;
 };
 
 SDSJ_HD inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
@@ -138,19 +147,18 @@ inline int natural_order(int k) {
   return t[k];
 }
 
-// Parses markers up to the first SOS (jdmarker.c subset).  `rd(i)` returns byte i.
+// Parses markers up to the first SOS (jdmarker.c subset).  `rd(i)` returns byte i; `t` must be
+// non-null (no null checks: on the device it points into LDS).
 template <class Reader>
 SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t) {
   d->status = SDSJ_OK;
   d->width = d->height = d->ncomp = 0;
   d->restart_interval = 0;
   d->saw_jfif = d->saw_adobe = d->adobe_transform = 0;
-  if (t) {
-    for (int q = 0; q < 4; q++) {
-      t->qt_defined[q] = 0;
-      t->dc_spec[q].defined = 0;
-      t->ac_spec[q].defined = 0;
-    }
+  for (int q = 0; q < 4; q++) {
+    t->qt_defined[q] = 0;
+    t->dc_spec[q].defined = 0;
+    t->ac_spec[q].defined = 0;
   }
   if (n < 4 || rd(0) != 0xFF || rd(1) != 0xD8) return SDSJ_CORRUPT;
   int64_t i = 2;
@@ -204,18 +212,16 @@ SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t)
           int tc = rd(s + k) >> 4, th = rd(s + k) & 15;
           if (tc > 1 || th > 3) return SDSJ_CORRUPT;
           int cnt = 0;
-          HuffSpec* h = t ? (tc ? &t->ac_spec[th] : &t->dc_spec[th]) : nullptr;
+          HuffSpec* h = tc ? &t->ac_spec[th] : &t->dc_spec[th];
           for (int l = 1; l <= 16; l++) {
             int b = rd(s + k + l);
             cnt += b;
-            if (h) h->bits[l] = (uint8_t)b;
+            h->bits[l] = (uint8_t)b;
           }
           if (cnt > 256 || k + 17 + cnt > sl) return SDSJ_CORRUPT;
-          if (h) {
-            h->bits[0] = 0;
-            for (int q = 0; q < 256; q++) h->vals[q] = q < cnt ? (uint8_t)rd(s + k + 17 + q) : 0;
-            h->defined = 1;
-          }
+          h->bits[0] = 0;
+          for (int q = 0; q < 256; q++) h->vals[q] = q < cnt ? (uint8_t)rd(s + k + 17 + q) : 0;
+          h->defined = 1;
           k += 17 + cnt;
         }
         break;
@@ -227,13 +233,11 @@ SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t)
           if (tq > 3 || pq > 1) return SDSJ_CORRUPT;
           int need = 1 + 64 * (pq ? 2 : 1);
           if (k + need > sl) return SDSJ_CORRUPT;
-          if (t) {
-            for (int q = 0; q < 64; q++) {
-              int v = pq ? ((rd(s + k + 1 + 2 * q) << 8) | rd(s + k + 2 + 2 * q)) : rd(s + k + 1 + q);
-              t->qt[tq][natural_order(q)] = (uint16_t)v;
-            }
-            t->qt_defined[tq] = 1;
+          for (int q = 0; q < 64; q++) {
+            int v = pq ? ((rd(s + k + 1 + 2 * q) << 8) | rd(s + k + 2 + 2 * q)) : rd(s + k + 1 + q);
+            t->qt[tq][natural_order(q)] = (uint16_t)v;
           }
+          t->qt_defined[tq] = 1;
           k += need;
         }
         break;
@@ -302,10 +306,8 @@ SDSJ_HD inline int setup_geometry(ImgDesc* d, const ImgTables* t) {
     if (cp.rh > 2 || cp.rv > 2) return SDSJ_UNSUPPORTED;
     cp.dw = ceil_div(d->width * cp.h, d->hmax);
     cp.dh = ceil_div(d->height * cp.v, d->vmax);
-    if (t) {
-      if (!t->qt_defined[cp.tq]) return SDSJ_CORRUPT;
-      if (!t->dc_spec[cp.td].defined || !t->ac_spec[cp.ta].defined) return SDSJ_CORRUPT;
-    }
+    if (!t->qt_defined[cp.tq]) return SDSJ_CORRUPT;
+    if (!t->dc_spec[cp.td].defined || !t->ac_spec[cp.ta].defined) return SDSJ_CORRUPT;
   }
   if (d->ncomp == 1) {
     CompDesc& cp = d->comp[0];
@@ -342,6 +344,7 @@ SDSJ_HD inline int setup_geometry(ImgDesc* d, const ImgTables* t) {
     plane += align_up((int64_t)cp.pitch * cp.bh * 8, 256);
   }
   d->total_blocks = (int64_t)d->mcux * d->mcuy * d->bpm;
+  if (d->total_blocks >= (int64_t)1 << 24) return SDSJ_UNSUPPORTED;  // > ~700 MP (block indices are 24-bit)
   int64_t mcus = (int64_t)d->mcux * d->mcuy;
   d->nseg = d->restart_interval ? (int32_t)((mcus + d->restart_interval - 1) / d->restart_interval) : 1;
   return SDSJ_OK;

@@ -19,8 +19,8 @@
 using namespace sdsj;
 
 namespace {
-constexpr int kStages = 9;
-const char* kStageNames[kStages] = {"parse", "plan", "unstuff", "entropy", "idct", "color", "coeffs", "hpass", "vpass"};
+constexpr int kStages = 10;
+const char* kStageNames[kStages] = {"parse", "plan", "unstuff", "entsync", "entwrite", "idct", "color", "coeffs", "hpass", "vpass"};
 }  // namespace
 
 struct sdsj_engine {
@@ -146,18 +146,20 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
   mark(2);
   SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, e->descs, e->scratch, s));
   mark(3);
-  SDSJ_HIP(e, launch_entropy(n, e->descs, e->tables, e->scratch, s));
+  SDSJ_HIP(e, launch_entsync(n, e->descs, e->tables, e->scratch, s));
   mark(4);
-  SDSJ_HIP(e, launch_idct(n, e->descs, e->tables, e->scratch, s));
+  SDSJ_HIP(e, launch_entwrite(n, e->descs, e->tables, e->scratch, s));
   mark(5);
-  SDSJ_HIP(e, launch_color(n, e->descs, e->scratch, s));
+  SDSJ_HIP(e, launch_idct(n, e->descs, e->tables, e->scratch, s));
   mark(6);
-  SDSJ_HIP(e, launch_coeffs(n, e->descs, op, e->scratch, s));
+  SDSJ_HIP(e, launch_color(n, e->descs, e->scratch, s));
   mark(7);
-  SDSJ_HIP(e, launch_hpass(n, e->descs, op, e->scratch, s));
+  SDSJ_HIP(e, launch_coeffs(n, e->descs, op, e->scratch, s));
   mark(8);
-  SDSJ_HIP(e, launch_vpass(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_lut, s));
+  SDSJ_HIP(e, launch_hpass(n, e->descs, op, e->scratch, s));
   mark(9);
+  SDSJ_HIP(e, launch_vpass(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_lut, s));
+  mark(10);
   return SDSJ_OK;
 }
 

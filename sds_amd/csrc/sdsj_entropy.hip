@@ -1,0 +1,757 @@
+// sdsj_entropy.hip -- parallel Huffman decoding of baseline JPEG scans on gfx950.
+//
+// Restates libjpeg-turbo jdhuff.c decode_mcu (the decoder Pillow runs for
+// sds/transforms/functional.py:100) with one image per 256-thread workgroup and the entropy
+// segment split into subsequences decoded in parallel (self-synchronisation, after Weissenberger &
+// Schmidt, "Massively Parallel Huffman Decoding on GPUs"):
+//
+//   k_entsync   1. speculative pass: subsequence j decodes from its first bit assuming (block 0,
+//                  DC) and records its block boundaries (SyncRec);
+//               2. sync: every j whose entry state differs from the exit state of j-1 re-decodes
+//                  from that state and stops at the first boundary where it meets a record of its
+//                  speculative pass (the paths have merged, the rest of that result is exact).  The
+//                  re-decodes run as work stages with a doubling symbol budget: unfinished tasks
+//                  save their state and are packed into the fewest waves for the next stage, so the
+//                  few long re-decodes do not hold every wave of the workgroup.  Rounds repeat
+//                  until every entry equals its predecessor's exit (Jacobi fixed point);
+//               3. segmented exclusive scan of (blocks completed, DC differences) -> every
+//                  subsequence's first block index and DC predictors (prediction resets at RSTn).
+//   k_entwrite  4. verified decode: each lane assembles its current 8x8 block in LDS (natural order,
+//                  jpeg_natural_order with its 16 guard entries); the wave flushes completed blocks
+//                  cooperatively as 128-byte stores.  A block belongs to the subsequence in which
+//                  its DC symbol starts (the owner decodes past its end to finish it).
+//
+// Symbol decoding: 2^LB-entry lookup of (code length, size, run) -- LB = 11 for images using at
+// most 4 Huffman tables, LB = 10 otherwise (two kernel variants, each skips the other's images)
+// -- and the canonical maxcode search of jpeg_huff_decode for longer codes.  The MCU position
+// (block -> table slots, component) comes from per-image packed registers, so the per-symbol path
+// is branch-free apart from the rare long-code search and the refill.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sdsj_common.h"
+#include "sdsj_kernels.h"
+
+namespace sdsj {
+
+constexpr int kEntThreads = kDecodeThreads;
+constexpr int kLutEntries = 1 << 13;  // LDS lookup capacity: 4 tables x 2^11 or 8 x 2^10
+constexpr int kStageStride = 64;      // int16 per lane staging block (one 128-byte block)
+constexpr int kBudget0 = 64;          // first sync stage's symbol budget
+constexpr int kMaxTasks = 1024;
+constexpr int kMaxSlots = 2 * kMaxComp;  // a DC and an AC table per component at most
+
+// ------------------------------------------------------------------------------------------
+// Per-image decode tables in LDS.
+// ------------------------------------------------------------------------------------------
+struct EntTables {
+  uint16_t lut[kLutEntries];
+  int32_t maxcode[kMaxSlots][18];
+  int32_t valoff[kMaxSlots][18];
+  uint8_t vals[kMaxSlots][256];
+  uint8_t nat[80];
+  int32_t slot_src[kMaxSlots];  // (kind << 2) | id of the table in each slot (kind 0 = DC, 1 = AC)
+  int32_t nslots;
+  uint32_t pk_dc[2], pk_ac[2], pk_c;  // per MCU block: DC slot, AC slot (4 bits each), component (2)
+};
+
+// Is this image decoded by the LB variant?  (LB = 11 when its tables fit 4 slots, else LB = 10.)
+template <int LB>
+__device__ __forceinline__ bool variant_owns(int ns) {
+  return LB == 11 ? (ns << 11) <= kLutEntries : (ns << 11) > kLutEntries && (ns << 10) <= kLutEntries;
+}
+
+template <int LB>
+__device__ int load_tables(EntTables& T, const ImgDesc* d, const ImgTables* tb) {
+  const int t = threadIdx.x;
+  if (t == 0) {
+    int ns = 0;
+    auto slot_of = [&](int key) {
+      for (int q = 0; q < ns; q++)
+        if (T.slot_src[q] == key) return q;
+      T.slot_src[ns] = key;
+      return ns++;
+    };
+    int dcs[kMaxComp], acs[kMaxComp];
+    for (int c = 0; c < d->ncomp; c++) {
+      dcs[c] = slot_of(d->comp[c].td);
+      acs[c] = slot_of(4 | d->comp[c].ta);
+    }
+    T.nslots = ns;
+    uint64_t pdc = 0, pac = 0;
+    uint32_t pc = 0;
+    for (int b = 0; b < d->bpm; b++) {
+      const int c = d->blk_comp[b];
+      pdc |= (uint64_t)dcs[c] << (4 * b);
+      pac |= (uint64_t)acs[c] << (4 * b);
+      pc |= (uint32_t)c << (2 * b);
+    }
+    T.pk_dc[0] = (uint32_t)pdc;
+    T.pk_dc[1] = (uint32_t)(pdc >> 32);
+    T.pk_ac[0] = (uint32_t)pac;
+    T.pk_ac[1] = (uint32_t)(pac >> 32);
+    T.pk_c = pc;
+  }
+  if (t < 80) T.nat[t] = (uint8_t)natural_order(t);
+  __syncthreads();
+  const int ns = T.nslots;
+  if (!variant_owns<LB>(ns)) return ns;
+  constexpr int shift = kLutBits - LB;  // scratch tables are 2^kLutBits wide
+  for (int i = t; i < (ns << LB); i += blockDim.x) {
+    const int q = i >> LB, k = i & ((1 << LB) - 1);
+    const int key = T.slot_src[q];
+    const HuffDerived& h = (key & 4) ? tb->ac[key & 3] : tb->dc[key & 3];
+    const uint16_t e = h.lut[k << shift];
+    T.lut[i] = (e & 15) > LB ? (uint16_t)0 : e;  // codes longer than LB take the slow path
+  }
+  for (int i = t; i < ns * 18; i += blockDim.x) {
+    const int q = i / 18, k = i % 18;
+    const int key = T.slot_src[q];
+    const HuffDerived& h = (key & 4) ? tb->ac[key & 3] : tb->dc[key & 3];
+    T.maxcode[q][k] = h.maxcode[k];
+    T.valoff[q][k] = h.valoffset[k];
+  }
+  for (int i = t; i < ns * 256; i += blockDim.x) {
+    const int q = i >> 8, k = i & 255;
+    const int key = T.slot_src[q];
+    T.vals[q][k] = (key & 4) ? tb->ac[key & 3].vals[k] : tb->dc[key & 3].vals[k];
+  }
+  __syncthreads();
+  return ns;
+}
+
+// ------------------------------------------------------------------------------------------
+// Bit reader: 64-bit MSB-first window; one 32-bit word prefetched ahead (its load is issued at
+// the previous refill, ~4 symbols earlier).
+// ------------------------------------------------------------------------------------------
+struct Bits {
+  const uint32_t* src;
+  uint64_t buf;
+  int nb;
+  uint32_t nw;   // next word (big-endian, as loaded)
+  uint32_t wi;   // index of the word after nw
+  uint32_t pos;  // absolute bit position of the next unconsumed bit
+};
+
+__device__ __forceinline__ void bits_init(Bits& b, const uint32_t* src, uint32_t p) {
+  b.src = src;
+  const uint32_t w = p >> 5;
+  const uint32_t hi = __builtin_bswap32(src[w]), lo = __builtin_bswap32(src[w + 1]);
+  const int sh = p & 31;
+  b.buf = (((uint64_t)hi << 32) | lo) << sh;
+  b.nb = 64 - sh;
+  b.nw = src[w + 2];
+  b.wi = w + 3;
+  b.pos = p;
+}
+
+__device__ __forceinline__ void bits_refill(Bits& b) {
+  if (b.nb <= 32) {
+    b.buf |= (uint64_t)__builtin_bswap32(b.nw) << (32 - b.nb);
+    b.nb += 32;
+    b.nw = b.src[b.wi++];
+  }
+}
+
+// MCU position -> table slots and component, from packed per-image registers.
+struct BlkCtx {
+  uint64_t pdc, pac;
+  uint32_t pc;
+  int bpm;
+};
+
+__device__ __forceinline__ int ctx_dc(const BlkCtx& k, int blk) { return (int)(k.pdc >> (4 * blk)) & 15; }
+__device__ __forceinline__ int ctx_ac(const BlkCtx& k, int blk) { return (int)(k.pac >> (4 * blk)) & 15; }
+__device__ __forceinline__ int ctx_c(const BlkCtx& k, int blk) { return (int)(k.pc >> (2 * blk)) & 3; }
+
+__device__ __forceinline__ BlkCtx make_ctx(const EntTables& T, int bpm) {
+  BlkCtx k;
+  k.pdc = ((uint64_t)T.pk_dc[1] << 32) | T.pk_dc[0];
+  k.pac = ((uint64_t)T.pk_ac[1] << 32) | T.pk_ac[0];
+  k.pc = T.pk_c;
+  k.bpm = bpm;
+  return k;
+}
+
+// One symbol (jdhuff.c HUFF_DECODE + get_bits + HUFF_EXTEND): DC -> category s, r = 0;
+// AC -> (r, s).  val = the extended value (0 when s = 0).
+template <int LB>
+__device__ __forceinline__ void decode_sym(const EntTables& T, Bits& b, int slot, bool isdc, int& s, int& r, int& val,
+                                           int& bad) {
+  bits_refill(b);
+  const uint32_t hi = (uint32_t)(b.buf >> 32);
+  const uint32_t e = T.lut[(slot << LB) + (hi >> (32 - LB))];
+  int l = e & 15;
+  s = (e >> 4) & 15;
+  r = (e >> 8) & 15;
+  if (l == 0) {
+    // jpeg_huff_decode: canonical search (longer codes, or a DC category > 15)
+    const uint32_t peek = hi >> 16;
+    int ll = 1;
+    while (ll <= 16 && (int32_t)(peek >> (16 - ll)) > T.maxcode[slot][ll]) ll++;
+    if (ll > 16) {
+      bad = 1;  // JWRN_HUFF_BAD_CODE
+      l = 16;
+      s = 0;
+      r = 0;
+    } else {
+      const int sym = T.vals[slot][((int32_t)(peek >> (16 - ll)) + T.valoff[slot][ll]) & 0xFF];
+      l = ll;
+      s = isdc ? sym : (sym & 15);
+      r = isdc ? 0 : (sym >> 4);
+      if (s > 16) {
+        bad = 1;
+        s = 16;
+      }
+    }
+  }
+  const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - s) & 31);
+  val = s == 0 ? 0 : (x < (1u << (s - 1)) ? (int)x - (1 << s) + 1 : (int)x);
+  const int tot = l + s;
+  b.buf <<= tot;
+  b.nb -= tot;
+  b.pos += tot;
+}
+
+// decode_mcu's k loop: DC -> k = 1; AC value -> k += r + 1; ZRL -> k += 16; EOB -> done.
+// Returns true when the block is complete (z wraps to 0).
+__device__ __forceinline__ bool next_z(int& z, int s, int r) {
+  const int zn = z == 0 ? 1 : (s ? z + r + 1 : (r == 15 ? z + 16 : 64));
+  z = zn >= 64 ? 0 : zn;
+  return zn >= 64;
+}
+
+__device__ __forceinline__ void add_dc(int c, int v, int& d0, int& d1, int& d2) {
+  d0 += c == 0 ? v : 0;
+  d1 += c == 1 ? v : 0;
+  d2 += c == 2 ? v : 0;
+}
+
+__device__ inline int block_excl_scan(int v, int* tmp, int* total) {
+  const int t = threadIdx.x;
+  tmp[t] = v;
+  __syncthreads();
+  for (int off = 1; off < kEntThreads; off <<= 1) {
+    int a = t >= off ? tmp[t - off] : 0;
+    __syncthreads();
+    tmp[t] += a;
+    __syncthreads();
+  }
+  const int incl = tmp[t];
+  *total = tmp[kEntThreads - 1];
+  __syncthreads();
+  return incl - v;
+}
+
+// ------------------------------------------------------------------------------------------
+// k_entsync
+// ------------------------------------------------------------------------------------------
+struct LdsSync {
+  EntTables T;
+  int32_t scan[5][kEntThreads];
+  int32_t flag[kEntThreads];
+  int32_t task[2][kMaxTasks];
+  int32_t nsub, rounds, stages;
+  unsigned long long sym[2];
+  unsigned long long t0, t1, t2;
+  unsigned long long it[2];
+  int32_t wmax[kEntThreads / 64];
+};
+
+// Speculative decode of subsequence S from its first bit (state: block 0, DC); records boundaries.
+template <int LB>
+__device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec) {
+  const uint32_t start = S.start_bit, end = S.end_bit;
+  Bits b;
+  bits_init(b, src, start);
+  int blk = 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
+  int d0 = 0, d1 = 0, d2 = 0;
+  int c = ctx_c(K, 0), sdc = ctx_dc(K, 0), sac = ctx_ac(K, 0);
+  while (b.pos < end) {
+    int s, r, val;
+    const bool isdc = z == 0;
+    decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+    nsym++;
+    dcd = isdc ? val : dcd;
+    add_dc(c, isdc ? val : 0, d0, d1, d2);
+    if (next_z(z, s, r)) {
+      if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
+      nrec++;
+      blk = blk + 1 == K.bpm ? 0 : blk + 1;
+      c = ctx_c(K, blk);
+      sdc = ctx_dc(K, blk);
+      sac = ctx_ac(K, blk);
+      nblk++;
+    }
+  }
+  S.entry_p = start;
+  S.entry_bz = 0;
+  S.spec_exit_p = S.cur_exit_p = b.pos;
+  S.spec_exit_bz = S.cur_exit_bz = (uint16_t)((blk << 8) | z);
+  S.spec_nblk = S.cur_nblk = nblk;
+  S.spec_dc[0] = S.cur_dc[0] = d0;
+  S.spec_dc[1] = S.cur_dc[1] = d1;
+  S.spec_dc[2] = S.cur_dc[2] = d2;
+  S.nrec = nrec < kRec ? nrec : kRec;
+  return nsym;
+}
+
+// Resumable re-decode of S (state in S.res_*), at most `budget` symbols.  Returns true when the
+// task is finished (merged with a record, or reached the subsequence end); new_exit_* / new_nblk /
+// new_dc then hold the result.  Otherwise the state is saved for the next stage.
+template <int LB>
+__device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, const SyncRec* rec,
+                          int budget, int* nsym_out) {
+  const uint32_t end = S.end_bit;
+  const int nrec = S.nrec;
+  Bits b;
+  bits_init(b, src, S.res_p);
+  int blk = S.res_bz >> 8, z = S.res_bz & 0xFF;
+  int nblk = S.res_nblk, ri = S.res_ri;
+  int d0 = S.res_dc[0], d1 = S.res_dc[1], d2 = S.res_dc[2];
+  int q0 = S.res_q[0], q1 = S.res_q[1], q2 = S.res_q[2];  // speculative DC prefix up to record ri
+  int bad = 0, nsym = 0;
+  int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
+  SyncRec R = ri < nrec ? rec[ri] : SyncRec{0xFFFFFFFFu, 0, 0, 0};
+  while (b.pos < end && nsym < budget) {
+    int s, r, val;
+    const bool isdc = z == 0;
+    decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+    nsym++;
+    add_dc(c, isdc ? val : 0, d0, d1, d2);
+    if (next_z(z, s, r)) {
+      const int done_blk = blk;
+      blk = blk + 1 == K.bpm ? 0 : blk + 1;
+      c = ctx_c(K, blk);
+      sdc = ctx_dc(K, blk);
+      sac = ctx_ac(K, blk);
+      nblk++;
+      while (R.p <= b.pos) {
+        add_dc(ctx_c(K, R.blk), R.dc, q0, q1, q2);
+        ri++;
+        if (R.p == b.pos && R.blk == done_blk) {
+          // merged with the speculative path: its remainder is exact
+          S.new_exit_p = S.spec_exit_p;
+          S.new_exit_bz = S.spec_exit_bz;
+          S.new_nblk = nblk + S.spec_nblk - ri;
+          S.new_dc[0] = d0 + S.spec_dc[0] - q0;
+          S.new_dc[1] = d1 + S.spec_dc[1] - q1;
+          S.new_dc[2] = d2 + S.spec_dc[2] - q2;
+          *nsym_out = nsym;
+          return true;
+        }
+        R = ri < nrec ? rec[ri] : SyncRec{0xFFFFFFFFu, 0, 0, 0};
+      }
+    }
+  }
+  *nsym_out = nsym;
+  if (b.pos >= end) {
+    S.new_exit_p = b.pos;
+    S.new_exit_bz = (uint16_t)((blk << 8) | z);
+    S.new_nblk = nblk;
+    S.new_dc[0] = d0;
+    S.new_dc[1] = d1;
+    S.new_dc[2] = d2;
+    return true;
+  }
+  S.res_p = b.pos;
+  S.res_bz = (uint16_t)((blk << 8) | z);
+  S.res_nblk = nblk;
+  S.res_ri = ri;
+  S.res_dc[0] = d0;
+  S.res_dc[1] = d1;
+  S.res_dc[2] = d2;
+  S.res_q[0] = q0;
+  S.res_q[1] = q1;
+  S.res_q[2] = q2;
+  return false;
+}
+
+template <int LB>
+__global__ void __launch_bounds__(kEntThreads) k_entsync(int n, ImgDesc* __restrict__ descs,
+                                                         const ImgTables* __restrict__ tables,
+                                                         uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.x;
+  if (img >= n) return;
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK) return;
+  __shared__ LdsSync L;
+  const int t = threadIdx.x;
+  const int ns = load_tables<LB>(L.T, d, &tables[img]);
+  if (!variant_owns<LB>(ns)) return;
+  if (t == 0) {
+    L.rounds = 0;
+    L.stages = 0;
+    L.sym[0] = L.sym[1] = 0;
+    L.it[0] = L.it[1] = 0;
+  }
+  const BlkCtx K = make_ctx(L.T, d->bpm);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
+  const int32_t* seg = reinterpret_cast<const int32_t*>(scratch + d->off_seg);
+  SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
+  SyncRec* recs = reinterpret_cast<SyncRec*>(scratch + d->off_rec);
+  const int nseg = d->nseg;
+  const uint32_t SB = (uint32_t)d->sub_bits;
+
+  // --- subsequence layout: segment s (bytes [seg[s], seg[s+1])) -> max(1, ceil(bits / SB)) ---
+  {
+    int carry = 0;
+    for (int base = 0; base < nseg; base += kEntThreads) {
+      const int s = base + t;
+      int cnt = 0;
+      uint32_t b0 = 0, b1 = 0;
+      if (s < nseg) {
+        b0 = (uint32_t)seg[s] * 8u;
+        b1 = (uint32_t)seg[s + 1] * 8u;
+        if (b1 < b0) b1 = b0;
+        cnt = b1 > b0 ? (int)((b1 - b0 + SB - 1) / SB) : 1;
+      }
+      int total;
+      const int off = carry + block_excl_scan(cnt, L.scan[0], &total);
+      if (s < nseg) {
+        for (int k = 0; k < cnt; k++) {
+          const int j = off + k;
+          if (j >= d->nsub_cap) break;
+          SubState& S = sub[j];
+          S.start_bit = b0 + (uint32_t)k * SB;
+          const uint32_t e = S.start_bit + SB;
+          S.end_bit = e < b1 ? e : b1;
+          S.first = k == 0;
+          S.seg = s;
+        }
+      }
+      carry += total;
+    }
+    if (t == 0) L.nsub = carry < d->nsub_cap ? carry : d->nsub_cap;
+  }
+  __syncthreads();
+  const int nsub = L.nsub;
+  unsigned long long nsym_spec = 0, nsym_sync = 0;
+
+  // --- 1. speculative pass ---
+  if (t == 0) L.t0 = __builtin_amdgcn_s_memtime();
+  if ((t & 63) == 0) L.wmax[t >> 6] = 0;
+  __syncthreads();
+  for (int j = t; j < nsub; j += kEntThreads) {
+    const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec);
+    nsym_spec += k;
+    atomicMax(&L.wmax[t >> 6], k);
+  }
+  __syncthreads();
+  if (t == 0) {
+    L.t1 = __builtin_amdgcn_s_memtime();
+    for (int w = 0; w < kEntThreads / 64; w++) L.it[0] += 64ull * L.wmax[w];
+  }
+
+  // --- 2. sync rounds until every entry equals its predecessor's exit ---
+  for (;;) {
+    // tasks of this round: j with entry != exit(j-1); new entry = exit(j-1) (previous values)
+    int ntask = 0;
+    for (int base = 0; base < nsub; base += kEntThreads) {
+      const int j = base + t;
+      bool need = false;
+      uint32_t ep = 0;
+      uint16_t ebz = 0;
+      if (j < nsub && !sub[j].first) {
+        ep = sub[j - 1].cur_exit_p;
+        ebz = sub[j - 1].cur_exit_bz;
+        need = ep != sub[j].entry_p || ebz != sub[j].entry_bz;
+      }
+      int tot;
+      const int off = block_excl_scan(need ? 1 : 0, L.scan[0], &tot);
+      if (need && ntask + off < kMaxTasks) {
+        L.task[0][ntask + off] = j;
+        SubState& S = sub[j];
+        S.new_entry_p = ep;
+        S.new_entry_bz = ebz;
+        S.res_p = ep;
+        S.res_bz = ebz;
+        S.res_nblk = 0;
+        S.res_ri = 0;
+        S.res_dc[0] = S.res_dc[1] = S.res_dc[2] = 0;
+        S.res_q[0] = S.res_q[1] = S.res_q[2] = 0;
+      }
+      ntask += tot;
+    }
+    if (ntask > kMaxTasks) ntask = kMaxTasks;  // the rest are picked up by the next round
+    __syncthreads();
+    if (ntask == 0) break;
+    if (t == 0) L.rounds++;
+    // work stages with doubling budgets; unfinished tasks are compacted to the front
+    int cur = 0, nt = ntask, budget = kBudget0;
+    while (nt > 0) {
+      if ((t & 63) == 0) L.wmax[t >> 6] = 0;
+      __syncthreads();
+      bool pending = false;
+      int my_task = -1;
+      if (t < nt) {
+        my_task = L.task[cur][t];
+        int k = 0;
+        pending = !sync_step<LB>(L.T, K, src, sub[my_task], recs + (int64_t)my_task * kRec, budget, &k);
+        nsym_sync += k;
+        atomicMax(&L.wmax[t >> 6], k);
+      }
+      for (int i = t + kEntThreads; i < nt; i += kEntThreads) {  // beyond one task per thread: no budget
+        int k = 0;
+        const int j = L.task[cur][i];
+        sync_step<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, 1 << 30, &k);
+        nsym_sync += k;
+      }
+      int tot;
+      const int off = block_excl_scan(pending ? 1 : 0, L.scan[0], &tot);
+      if (pending) L.task[cur ^ 1][off] = my_task;
+      if (t == 0) {
+        L.stages++;
+        for (int w = 0; w < kEntThreads / 64; w++) L.it[1] += 64ull * L.wmax[w];
+      }
+      __syncthreads();
+      cur ^= 1;
+      nt = tot;
+      budget *= 2;
+    }
+    // commit every task of the round (entries first: they were read from cur_exit of j-1)
+    for (int i = t; i < ntask; i += kEntThreads) {
+      SubState& S = sub[L.task[0][i]];
+      S.entry_p = S.new_entry_p;
+      S.entry_bz = S.new_entry_bz;
+    }
+    __syncthreads();
+    for (int i = t; i < ntask; i += kEntThreads) {
+      SubState& S = sub[L.task[0][i]];
+      S.cur_exit_p = S.new_exit_p;
+      S.cur_exit_bz = S.new_exit_bz;
+      S.cur_nblk = S.new_nblk;
+      S.cur_dc[0] = S.new_dc[0];
+      S.cur_dc[1] = S.new_dc[1];
+      S.cur_dc[2] = S.new_dc[2];
+    }
+    __syncthreads();
+  }
+
+  // --- 3. segmented exclusive scan of (blocks, dc0, dc1, dc2) ---
+  if (t == 0) L.t2 = __builtin_amdgcn_s_memtime();
+  {
+    int carry[4] = {0, 0, 0, 0};
+    for (int base = 0; base < nsub; base += kEntThreads) {
+      const int j = base + t;
+      int v[4] = {0, 0, 0, 0};
+      int f = 1;
+      if (j < nsub) {
+        const SubState& S = sub[j];
+        v[0] = S.cur_nblk;
+        v[1] = S.cur_dc[0];
+        v[2] = S.cur_dc[1];
+        v[3] = S.cur_dc[2];
+        f = S.first;
+      }
+      for (int q = 0; q < 4; q++) L.scan[q][t] = v[q];
+      L.flag[t] = f;
+      __syncthreads();
+      for (int off = 1; off < kEntThreads; off <<= 1) {
+        int a[4] = {0, 0, 0, 0}, af = 0;
+        const bool take = t >= off;
+        if (take) {
+          for (int q = 0; q < 4; q++) a[q] = L.scan[q][t - off];
+          af = L.flag[t - off];
+        }
+        __syncthreads();
+        if (take && !L.flag[t])
+          for (int q = 0; q < 4; q++) L.scan[q][t] += a[q];
+        if (take) L.flag[t] |= af;
+        __syncthreads();
+      }
+      if (j < nsub) {
+        SubState& S = sub[j];
+        const int hit = L.flag[t];
+        int ex[4];
+        for (int q = 0; q < 4; q++) ex[q] = S.first ? 0 : L.scan[q][t] - v[q] + (hit ? 0 : carry[q]);
+        S.nblk_ex = ex[0];
+        S.dc_ex[0] = ex[1];
+        S.dc_ex[1] = ex[2];
+        S.dc_ex[2] = ex[3];
+      }
+      __syncthreads();
+      const int any = L.flag[kEntThreads - 1];
+      for (int q = 0; q < 4; q++) carry[q] = L.scan[q][kEntThreads - 1] + (any ? 0 : carry[q]);
+      __syncthreads();
+    }
+  }
+  atomicAdd(&L.sym[0], nsym_spec);
+  atomicAdd(&L.sym[1], nsym_sync);
+  __syncthreads();
+  if (t == 0) {
+    d->nsub = nsub;
+    d->sync_rounds = L.rounds;
+    d->pad0 = L.stages;
+    d->sym_spec = (int64_t)L.sym[0];
+    d->sym_sync = (int64_t)L.sym[1];
+    d->t_spec = (int64_t)(L.t1 - L.t0);
+    d->t_sync = (int64_t)(L.t2 - L.t1);
+    d->t_scan = (int64_t)(__builtin_amdgcn_s_memtime() - L.t2);
+    d->it_spec = (int64_t)L.it[0];
+    d->it_sync = (int64_t)L.it[1];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_entwrite
+// ------------------------------------------------------------------------------------------
+struct LdsWrite {
+  unsigned long long t0, it;
+  EntTables T;
+  alignas(16) int16_t stage[(kEntThreads + 1) * kStageStride];  // + one shared sink block
+  uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
+  int32_t bad;
+  unsigned long long sym;
+};
+
+template <int LB>
+__global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __restrict__ descs,
+                                                          const ImgTables* __restrict__ tables,
+                                                          uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.x;
+  if (img >= n) return;
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK) return;
+  __shared__ LdsWrite L;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int ns = load_tables<LB>(L.T, d, &tables[img]);
+  if (!variant_owns<LB>(ns)) return;
+  {
+    uint4* z4 = reinterpret_cast<uint4*>(L.stage);
+    for (int i = t; i < (kEntThreads + 1) * kStageStride * 2 / 16; i += kEntThreads) z4[i] = make_uint4(0, 0, 0, 0);
+  }
+  if (t == 0) {
+    L.bad = 0;
+    L.sym = 0;
+    L.it = 0;
+    L.t0 = __builtin_amdgcn_s_memtime();
+  }
+  __syncthreads();
+  const EntTables& T = L.T;
+  const BlkCtx K = make_ctx(T, d->bpm);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
+  const int32_t* seg = reinterpret_cast<const int32_t*>(scratch + d->off_seg);
+  const SubState* sub = reinterpret_cast<const SubState*>(scratch + d->off_sub);
+  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
+  const int nsub = d->nsub, nseg = d->nseg;
+  const int64_t blocks_per_seg = d->restart_interval ? (int64_t)d->restart_interval * K.bpm : d->total_blocks;
+  const int my_base = t * kStageStride, sink_base = kEntThreads * kStageStride;
+  int bad = 0;
+  unsigned long long nsym = 0, witers = 0;
+
+  for (int jb = 0; jb < nsub; jb += kEntThreads) {  // uniform trip count for the whole workgroup
+    const int j = jb + t;
+    const bool active = j < nsub;
+    Bits b;
+    int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, sdc = 0, sac = 0;
+    int64_t g = 0, gend = 0;
+    uint32_t end_bit = 0, done_p = 0, seg_end_bit = 0;
+    bool writing = false, last_of_seg = false, run = false;
+    if (active) {
+      const SubState& S = sub[j];
+      const int s = S.seg;
+      const int64_t g0 = (int64_t)s * blocks_per_seg;
+      gend = g0 + blocks_per_seg;
+      if (gend > d->total_blocks) gend = d->total_blocks;
+      g = g0 + S.nblk_ex;
+      p0 = S.dc_ex[0];
+      p1 = S.dc_ex[1];
+      p2 = S.dc_ex[2];
+      blk = S.entry_bz >> 8;
+      z = S.entry_bz & 0xFF;
+      c = ctx_c(K, blk);
+      sdc = ctx_dc(K, blk);
+      sac = ctx_ac(K, blk);
+      writing = z == 0;
+      end_bit = S.end_bit;
+      seg_end_bit = (uint32_t)seg[s + 1 <= nseg ? s + 1 : nseg] * 8u;
+      last_of_seg = (j + 1 == nsub) || sub[j + 1].first;
+      bits_init(b, src, S.entry_p);
+      run = g < gend && (b.pos < end_bit || z != 0);
+    }
+    while (__builtin_amdgcn_ballot_w64(run) != 0) {
+      witers++;
+      bool ready = false;
+      uint32_t gdone = 0;
+      if (run) {
+        int s, r, val, sb = 0;
+        const bool isdc = z == 0;
+        decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
+        nsym++;
+        bad |= sb;
+        // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
+        const int add = isdc ? val : 0;
+        p0 += c == 0 ? add : 0;
+        p1 += c == 1 ? add : 0;
+        p2 += c == 2 ? add : 0;
+        const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
+        const int wpos = isdc ? 0 : (int)T.nat[z + r];
+        L.stage[((writing && (isdc || s)) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pv : val);
+        if (next_z(z, s, r)) {
+          ready = writing;
+          gdone = (uint32_t)g;
+          blk = blk + 1 == K.bpm ? 0 : blk + 1;
+          c = ctx_c(K, blk);
+          sdc = ctx_dc(K, blk);
+          sac = ctx_ac(K, blk);
+          g++;
+          writing = true;
+          if (g == gend) done_p = b.pos;
+        }
+        run = g < gend && (b.pos < end_bit || z != 0);
+      }
+      // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
+      const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
+      if (m) {
+        const int cnt = __popcll(m);
+        if (ready) {
+          const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+          L.flist[wv][idx] = ((uint32_t)t << 24) | gdone;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        for (int b0 = 0; b0 < cnt; b0 += 8) {
+          const int bi = b0 + (lane >> 3);
+          if (bi < cnt) {
+            const uint32_t f = L.flist[wv][bi];
+            uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
+            const uint4 v = *sp;
+            reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64)[lane & 7] = v;
+            *sp = make_uint4(0, 0, 0, 0);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (active && last_of_seg) {
+      if (g < gend) bad = 1;                    // segment ended before its last block
+      else if (done_p > seg_end_bit) bad = 1;   // last block needed bits past the segment
+    }
+  }
+  if (bad) atomicOr(&L.bad, 1);
+  atomicAdd(&L.sym, nsym);
+  if (lane == 0) atomicAdd(&L.it, 64ull * witers);
+  __syncthreads();
+  if (t == 0) {
+    d->sym_write = (int64_t)L.sym;
+    d->it_write = (int64_t)L.it;
+    d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - L.t0);
+    if (L.bad) d->status = SDSJ_CORRUPT;
+  }
+}
+
+hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
+  hipLaunchKernelGGL(k_entsync<11>, dim3(n), dim3(kEntThreads), 0, s, n, descs, tables, scratch);
+  hipLaunchKernelGGL(k_entsync<10>, dim3(n), dim3(kEntThreads), 0, s, n, descs, tables, scratch);
+  return hipGetLastError();
+}
+
+hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
+  hipLaunchKernelGGL(k_entwrite<11>, dim3(n), dim3(kEntThreads), 0, s, n, descs, tables, scratch);
+  hipLaunchKernelGGL(k_entwrite<10>, dim3(n), dim3(kEntThreads), 0, s, n, descs, tables, scratch);
+  return hipGetLastError();
+}
+
+}  // namespace sdsj

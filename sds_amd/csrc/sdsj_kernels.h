@@ -10,7 +10,8 @@ hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, cons
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, hipStream_t s);
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
-hipError_t launch_entropy(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
+hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
+hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
 hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, hipStream_t s);
 hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s);

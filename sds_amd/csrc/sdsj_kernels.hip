@@ -4,7 +4,8 @@
 //   k_parse    markers, tables, geometry          jdmarker.c / jdhuff.c tables / functional.py:118-140
 //   k_plan     per-batch scratch offsets          (no reference counterpart)
 //   k_unstuff  byte unstuffing + RSTn split        jdhuff.c jpeg_fill_bit_buffer / process_restart
-//   k_entropy  self-synchronising Huffman decode  jdhuff.c decode_mcu (parallel restatement)
+//   k_entsync  speculative decode + self-sync     jdhuff.c decode_mcu (parallel restatement), in
+//   k_entwrite verified decode -> coefficients    sdsj_entropy.hip
 //   k_idct     dequant + ISLOW IDCT                jidctint.c jpeg_idct_islow
 //   k_color    fancy upsampling + YCbCr->RGB      jdsample.c / jdmainct.c / jdcolor.c
 //   k_coeffs   resampling tables (doubles)        Pillow Resample.c precompute_coeffs
@@ -103,6 +104,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
   d->ustream_cap = d->entropy_len + kUPad;
   d->off_seg = take((int64_t)(d->nseg + 2) * 4);
   d->off_sub = take((int64_t)d->nsub_cap * sizeof(SubState));
+  d->off_rec = take((int64_t)d->nsub_cap * kRec * sizeof(SyncRec));
   d->off_coef = take(d->total_blocks * 128);
   int64_t planes = 0;
   for (int c = 0; c < d->ncomp; c++) planes += align_up((int64_t)d->comp[c].pitch * d->comp[c].bh * 8, 256);
@@ -190,7 +192,11 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
         if (l <= kLutBits) {
           int base = huffcode[k] << (kLutBits - l);
           int cnt = 1 << (kLutBits - l);
-          uint16_t e = (uint16_t)((l << 8) | hs.vals[k]);
+          const int sym = hs.vals[k];
+          const int sz = tix < 4 ? sym : (sym & 15);  // DC: category; AC: size
+          const int run = tix < 4 ? 0 : (sym >> 4);
+          // (len | size << 4 | run << 8); DC categories > 15 take the slow path (flagged there)
+          uint16_t e = sz > 15 ? (uint16_t)0 : (uint16_t)(l | (sz << 4) | (run << 8));
           for (int r = 0; r < cnt; r++) hd.lut[base + r] = e;
         }
       }
@@ -240,6 +246,7 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         d.off_ustream += start;
         d.off_seg += start;
         d.off_sub += start;
+        d.off_rec += start;
         d.off_coef += start;
         d.off_planes += start;
         d.off_rgb += start;
@@ -258,7 +265,6 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
 // ------------------------------------------------------------------------------------------
 // k_unstuff: one 256-thread workgroup per image.  Removes FF00 stuffing and fill bytes, splits at
 // RSTn markers and stops at the first other marker (jdhuff.c jpeg_fill_bit_buffer semantics).
-// Also zero-fills the image's coefficient area for k_entropy.
 // ------------------------------------------------------------------------------------------
 constexpr int kUnstuffThreads = 256;
 constexpr int kUnstuffBytes = 16;
@@ -296,12 +302,6 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
   int32_t* seg = reinterpret_cast<int32_t*>(scratch + d->off_seg);
   const int nseg = d->nseg;
 
-  // zero the coefficient area (16 B per store)
-  {
-    uint4* cz = reinterpret_cast<uint4*>(scratch + d->off_coef);
-    const int64_t nz = d->total_blocks * 128 / 16;
-    for (int64_t i = t; i < nz; i += kUnstuffThreads) cz[i] = make_uint4(0, 0, 0, 0);
-  }
   if (t == 0) seg[0] = 0;
 
   int64_t out_pos = 0;
@@ -373,427 +373,6 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
     d->ulen = out_pos;
     d->useg_found = 1 + rst_count;
     if (1 + rst_count < nseg) d->status = SDSJ_CORRUPT;  // missing restart markers
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// k_entropy: one 256-thread workgroup per image.  Self-synchronising parallel Huffman decoding:
-//   round 0   every subsequence decodes speculatively from its first bit (state: block 0, DC);
-//   rounds r  subsequence j re-decodes from the exit state of j-1 until all exits agree (Jacobi);
-//   scan      segmented exclusive scan of (blocks completed, DC sums) -> entry block / predictors;
-//   write     every subsequence decodes from its verified entry and scatters coefficients.
-// The decode of one symbol follows jdhuff.c decode_mcu exactly (HUFF_EXTEND, ZRL, EOB, k+r
-// overflow into jpeg_natural_order's guard entries, DC prediction per component).
-// ------------------------------------------------------------------------------------------
-struct LdsEntropy {
-  uint16_t lut[8][1 << kLutBits];
-  int32_t maxcode[8][18];
-  int32_t valoff[8][18];
-  uint8_t vals[8][256];
-  uint8_t blk_dc[kMaxBlocksPerMcu], blk_ac[kMaxBlocksPerMcu], blk_c[kMaxBlocksPerMcu];
-  int32_t scan[5][256];
-  int32_t flag[256];
-  int32_t changed;
-  int32_t nsub;
-  int32_t bad;
-  int32_t rounds;
-  unsigned long long sym[3];
-};
-
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
-struct BitReader {
-  const uint32_t* w;
-  uint64_t buf;
-  int nb;
-  uint32_t next;
-  __device__ __forceinline__ void init(uint32_t p) {
-    uint32_t wi = p >> 5;
-    int sh = p & 31;
-    uint64_t a = bswap32(w[wi]), b = bswap32(w[wi + 1]);
-    buf = ((a << 32) | b) << sh;
-    nb = 64 - sh;
-    next = wi + 2;
-  }
-  __device__ __forceinline__ void refill() {
-    if (nb <= 32) {
-      buf |= (uint64_t)bswap32(w[next++]) << (32 - nb);
-      nb += 32;
-    }
-  }
-  __device__ __forceinline__ uint32_t pos() const { return next * 32u - (uint32_t)nb; }
-};
-
-__device__ __forceinline__ int huff_extend(uint32_t x, int s) {
-  return (x < (1u << (s - 1))) ? (int)x + (int)((~0u << s) + 1u) : (int)x;
-}
-
-// Decodes symbols from `entry` until the next symbol would start at or after `end_bit`.
-// WRITE: scatter coefficients of blocks [g, g_end) to `coef`.
-template <bool WRITE>
-__device__ int decode_subseq(const LdsEntropy& L, const uint32_t* words, uint32_t entry_p, int blk, int z,
-                              uint32_t end_bit, int bpm, int* nblk_out, int* dc_out, uint32_t* exit_p, int* exit_blk,
-                              int* exit_z, int64_t g, int64_t g_end, const int* dc_pred_in, int16_t* coef, int* bad,
-                              uint32_t* done_p) {
-  BitReader br;
-  br.w = words;
-  br.init(entry_p);
-  int nblk = 0;
-  int dc0 = 0, dc1 = 0, dc2 = 0;
-  int pred0 = 0, pred1 = 0, pred2 = 0;
-  if (WRITE) {
-    pred0 = dc_pred_in[0];
-    pred1 = dc_pred_in[1];
-    pred2 = dc_pred_in[2];
-  }
-  int comp = L.blk_c[blk];
-  int tdc = L.blk_dc[blk], tac = L.blk_ac[blk];
-  int nsym = 0;
-  while (br.pos() < end_bit) {
-    nsym++;
-    br.refill();
-    const uint32_t peek = (uint32_t)(br.buf >> 48);
-    const int tab = z == 0 ? tdc : tac;
-    const uint16_t e = L.lut[tab][peek >> (16 - kLutBits)];
-    int len = e >> 8;
-    int sym = e & 0xFF;
-    if (len == 0) {
-      int l = kLutBits + 1;
-      while (l <= 16 && (int32_t)(peek >> (16 - l)) > L.maxcode[tab][l]) l++;
-      if (l > 16) {
-        // bad code (JWRN_HUFF_BAD_CODE): only a verified decode of a real block counts
-        if (WRITE && g < g_end) *bad = 1;
-        len = 16;
-        sym = 0;
-      } else {
-        len = l;
-        sym = L.vals[tab][((int32_t)(peek >> (16 - l)) + L.valoff[tab][l]) & 0xFF];
-      }
-    }
-    br.buf <<= len;
-    br.nb -= len;
-    int s, r;
-    if (z == 0) {
-      s = sym;
-      r = 0;
-      if (s > 16) {
-        if (WRITE && g < g_end) *bad = 1;
-        s = 16;
-      }
-    } else {
-      s = sym & 15;
-      r = sym >> 4;
-    }
-    int val = 0;
-    if (s) {
-      uint32_t x = (uint32_t)(br.buf >> (64 - s));
-      br.buf <<= s;
-      br.nb -= s;
-      val = huff_extend(x, s);
-    }
-    if (z == 0) {
-      if (WRITE) {
-        int p;
-        if (comp == 0) p = (pred0 += val);
-        else if (comp == 1) p = (pred1 += val);
-        else p = (pred2 += val);
-        if (g < g_end) coef[g * 64] = (int16_t)p;
-      } else {
-        if (comp == 0) dc0 += val;
-        else if (comp == 1) dc1 += val;
-        else dc2 += val;
-      }
-      z = 1;
-    } else if (s) {
-      z += r;
-      if (WRITE && g < g_end) coef[g * 64 + natural_order(z)] = (int16_t)val;
-      z += 1;
-    } else if (r == 15) {
-      z += 16;
-    } else {
-      z = 64;
-    }
-    if (z >= 64) {
-      z = 0;
-      blk = blk + 1 == bpm ? 0 : blk + 1;
-      comp = L.blk_c[blk];
-      tdc = L.blk_dc[blk];
-      tac = L.blk_ac[blk];
-      nblk++;
-      if (WRITE) {
-        g++;
-        if (g == g_end) *done_p = br.pos();
-      }
-    }
-  }
-  *nblk_out = nblk;
-  dc_out[0] = dc0;
-  dc_out[1] = dc1;
-  dc_out[2] = dc2;
-  *exit_p = br.pos();
-  *exit_blk = blk;
-  *exit_z = z;
-  return nsym;
-}
-
-__global__ void __launch_bounds__(kDecodeThreads) k_entropy(int n, ImgDesc* __restrict__ descs,
-                                                            const ImgTables* __restrict__ tables,
-                                                            uint8_t* __restrict__ scratch) {
-  const int img = blockIdx.x;
-  if (img >= n) return;
-  ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK) return;
-  __shared__ LdsEntropy L;
-  const int t = threadIdx.x;
-  const ImgTables* tb = &tables[img];
-  for (int i = t; i < 8 * (1 << kLutBits); i += kDecodeThreads) {
-    int tix = i >> kLutBits, k = i & ((1 << kLutBits) - 1);
-    L.lut[tix][k] = tix < 4 ? tb->dc[tix].lut[k] : tb->ac[tix - 4].lut[k];
-  }
-  for (int i = t; i < 8 * 18; i += kDecodeThreads) {
-    int tix = i / 18, k = i % 18;
-    L.maxcode[tix][k] = tix < 4 ? tb->dc[tix].maxcode[k] : tb->ac[tix - 4].maxcode[k];
-    L.valoff[tix][k] = tix < 4 ? tb->dc[tix].valoffset[k] : tb->ac[tix - 4].valoffset[k];
-  }
-  for (int i = t; i < 8 * 256; i += kDecodeThreads) {
-    int tix = i >> 8, k = i & 255;
-    L.vals[tix][k] = tix < 4 ? tb->dc[tix].vals[k] : tb->ac[tix - 4].vals[k];
-  }
-  const int bpm = d->bpm;
-  if (t < bpm) {
-    int c = d->blk_comp[t];
-    L.blk_c[t] = (uint8_t)c;
-    L.blk_dc[t] = (uint8_t)d->comp[c].td;
-    L.blk_ac[t] = (uint8_t)(4 + d->comp[c].ta);
-  }
-  if (t == 0) {
-    L.bad = 0;
-    L.nsub = 0;
-    L.rounds = 0;
-    L.sym[0] = L.sym[1] = L.sym[2] = 0;
-  }
-  __syncthreads();
-
-  const uint32_t* words = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
-  const int32_t* seg = reinterpret_cast<const int32_t*>(scratch + d->off_seg);
-  SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
-  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
-  const int nseg = d->nseg;
-  const uint32_t SB = (uint32_t)d->sub_bits;
-  const int64_t blocks_per_seg = d->restart_interval ? (int64_t)d->restart_interval * bpm : d->total_blocks;
-
-  // --- subsequence layout: segment s covers bytes [seg[s], seg[s+1]) of the unstuffed stream ---
-  // nsub_s = max(1, ceil(bits_s / SB)); exclusive scan over segments (tiles of 256)
-  {
-    int carry = 0;
-    for (int base = 0; base < nseg; base += kDecodeThreads) {
-      int s = base + t;
-      int cnt = 0;
-      uint32_t b0 = 0, b1 = 0;
-      if (s < nseg) {
-        b0 = (uint32_t)seg[s] * 8u;
-        b1 = (uint32_t)seg[s + 1] * 8u;
-        if (s + 1 < nseg && b1 < b0) b1 = b0;
-        cnt = b1 > b0 ? (int)((b1 - b0 + SB - 1) / SB) : 1;
-      }
-      int total;
-      int off = carry + block_excl_scan_256(cnt, L.scan[0], &total);
-      if (s < nseg) {
-        for (int k = 0; k < cnt; k++) {
-          int j = off + k;
-          if (j >= d->nsub_cap) break;
-          SubState& S = sub[j];
-          S.start_bit = b0 + (uint32_t)k * SB;
-          uint32_t e = S.start_bit + SB;
-          S.end_bit = e < b1 ? e : b1;
-          if (S.end_bit < S.start_bit) S.end_bit = S.start_bit;
-          S.first = k == 0;
-          S.seg = (uint16_t)s;
-        }
-      }
-      carry += total;
-    }
-    if (t == 0) L.nsub = carry < d->nsub_cap ? carry : d->nsub_cap;
-  }
-  __syncthreads();
-  const int nsub = L.nsub;
-  int bad = 0;
-  int spec_bad = 0;  // invalid codes met while decoding from unverified states are expected
-  unsigned long long nsym_spec = 0, nsym_sync = 0, nsym_write = 0;
-
-  // --- round 0: speculative decode from each subsequence start ---
-  for (int j = t; j < nsub; j += kDecodeThreads) {
-    SubState& S = sub[j];
-    int nb, dc[3], eb, ez;
-    uint32_t ep, dp;
-    nsym_spec += decode_subseq<false>(L, words, S.start_bit, 0, 0, S.end_bit, bpm, &nb, dc, &ep, &eb, &ez, 0, 0,
-                                      nullptr, nullptr, &spec_bad, &dp);
-    S.entry_p = S.start_bit;
-    S.entry_bz = 0;
-    S.exit_p = ep;
-    S.exit_bz = (uint16_t)((eb << 8) | ez);
-    S.nblk = nb;
-    S.dc[0] = dc[0];
-    S.dc[1] = dc[1];
-    S.dc[2] = dc[2];
-  }
-  __syncthreads();
-
-  // --- sync rounds (Jacobi): entry(j) <- exit(j-1) ---
-  for (int round = 0; round < 1 << 20; round++) {
-    if (t == 0) L.changed = 0;
-    __syncthreads();
-    // read phase: compute new values into the *2 fields
-    for (int j = t; j < nsub; j += kDecodeThreads) {
-      SubState& S = sub[j];
-      S.exit_p2 = S.exit_p;
-      S.exit_bz2 = S.exit_bz;
-      S.nblk2 = S.nblk;
-      S.dc2[0] = S.dc[0];
-      S.dc2[1] = S.dc[1];
-      S.dc2[2] = S.dc[2];
-      if (S.first) continue;
-      const SubState& P = sub[j - 1];
-      uint32_t ep = P.exit_p;
-      uint16_t ebz = P.exit_bz;
-      if (ep == S.entry_p && ebz == S.entry_bz) continue;
-      int nb, dc[3], eb, ez;
-      uint32_t xp, dp;
-      nsym_sync += decode_subseq<false>(L, words, ep, ebz >> 8, ebz & 0xFF, S.end_bit, bpm, &nb, dc, &xp, &eb,
-                                        &ez, 0, 0, nullptr, nullptr, &spec_bad, &dp);
-      S.exit_p2 = xp;
-      S.exit_bz2 = (uint16_t)((eb << 8) | ez);
-      S.nblk2 = nb;
-      S.dc2[0] = dc[0];
-      S.dc2[1] = dc[1];
-      S.dc2[2] = dc[2];
-    }
-    __syncthreads();
-    // commit phase
-    for (int j = t; j < nsub; j += kDecodeThreads) {
-      SubState& S = sub[j];
-      if (!S.first) {
-        const SubState& P = sub[j - 1];
-        // entry becomes the predecessor's exit as read in this round (P.exit_p not yet committed:
-        // P's committed values are exit_p; the read phase used exit_p too)
-        S.entry_p = P.exit_p;
-        S.entry_bz = P.exit_bz;
-      }
-    }
-    __syncthreads();
-    for (int j = t; j < nsub; j += kDecodeThreads) {
-      SubState& S = sub[j];
-      if (S.exit_p2 != S.exit_p || S.exit_bz2 != S.exit_bz) L.changed = 1;
-      S.exit_p = S.exit_p2;
-      S.exit_bz = S.exit_bz2;
-      S.nblk = S.nblk2;
-      S.dc[0] = S.dc2[0];
-      S.dc[1] = S.dc2[1];
-      S.dc[2] = S.dc2[2];
-    }
-    __syncthreads();
-    if (t == 0) L.rounds++;
-    if (!L.changed) break;
-    __syncthreads();
-  }
-
-  // --- segmented exclusive scan of (nblk, dc0, dc1, dc2) in subsequence order ---
-  // Stored into S.nblk2 (entry block index) and S.dc2 (entry DC predictors).
-  {
-    int carry[4] = {0, 0, 0, 0};
-    int carry_seg = -1;
-    for (int base = 0; base < nsub; base += kDecodeThreads) {
-      int j = base + t;
-      int v[4] = {0, 0, 0, 0};
-      int f = 1;
-      if (j < nsub) {
-        const SubState& S = sub[j];
-        v[0] = S.nblk;
-        v[1] = S.dc[0];
-        v[2] = S.dc[1];
-        v[3] = S.dc[2];
-        f = S.first;
-      }
-      // inclusive segmented scan (Hillis-Steele on (flag, value))
-      for (int q = 0; q < 4; q++) L.scan[q][t] = v[q];
-      L.flag[t] = f;
-      __syncthreads();
-      for (int off = 1; off < kDecodeThreads; off <<= 1) {
-        int a[4], af = 0;
-        bool take = t >= off;
-        if (take) {
-          for (int q = 0; q < 4; q++) a[q] = L.scan[q][t - off];
-          af = L.flag[t - off];
-        }
-        __syncthreads();
-        if (take && !L.flag[t]) {
-          for (int q = 0; q < 4; q++) L.scan[q][t] += a[q];
-        }
-        if (take) L.flag[t] |= af;
-        __syncthreads();
-      }
-      // exclusive value = inclusive - own; add the carry from previous tiles if no segment start
-      // occurred at or before this element inside the tile
-      if (j < nsub) {
-        SubState& S = sub[j];
-        int hit_start = L.flag[t];
-        int ex[4];
-        for (int q = 0; q < 4; q++) ex[q] = L.scan[q][t] - v[q] + (hit_start ? 0 : carry[q]);
-        if (S.first) {
-          for (int q = 0; q < 4; q++) ex[q] = 0;
-        }
-        int sidx = S.seg;
-        (void)sidx;
-        S.nblk2 = ex[0];
-        S.dc2[0] = ex[1];
-        S.dc2[1] = ex[2];
-        S.dc2[2] = ex[3];
-      }
-      __syncthreads();
-      // carry for the next tile: inclusive value of the last element
-      int last = kDecodeThreads - 1;
-      int any_start = L.flag[last];
-      for (int q = 0; q < 4; q++) carry[q] = L.scan[q][last] + (any_start ? 0 : carry[q]);
-      (void)carry_seg;
-      __syncthreads();
-    }
-  }
-  __syncthreads();
-
-  // --- write pass ---
-  for (int j = t; j < nsub; j += kDecodeThreads) {
-    const SubState& S = sub[j];
-    const int s = S.seg;
-    const int64_t gseg0 = (int64_t)s * blocks_per_seg;
-    int64_t gend = gseg0 + blocks_per_seg;
-    if (gend > d->total_blocks) gend = d->total_blocks;
-    const int64_t g = gseg0 + S.nblk2;
-    int nb, dc[3], eb, ez;
-    uint32_t xp, dp = 0;
-    const int pred[3] = {S.dc2[0], S.dc2[1], S.dc2[2]};
-    nsym_write += decode_subseq<true>(L, words, S.entry_p, S.entry_bz >> 8, S.entry_bz & 0xFF, S.end_bit, bpm, &nb,
-                                      dc, &xp, &eb, &ez, g, gend, pred, coef, &bad, &dp);
-    // completeness: the last subsequence of each segment must reach the segment's block count
-    // using real (not padding) bits
-    const bool last_of_seg = (j + 1 == nsub) || sub[j + 1].first;
-    if (last_of_seg) {
-      if (g + nb < gend) bad = 1;
-      const uint32_t seg_end_bit = (uint32_t)seg[s + 1 <= nseg ? s + 1 : nseg] * 8u;
-      if (dp > seg_end_bit) bad = 1;
-    }
-  }
-  if (bad) atomicOr(&L.bad, 1);
-  atomicAdd(&L.sym[0], nsym_spec);
-  atomicAdd(&L.sym[1], nsym_sync);
-  atomicAdd(&L.sym[2], nsym_write);
-  __syncthreads();
-  if (t == 0) {
-    d->nsub = nsub;
-    d->sync_rounds = L.rounds;
-    d->sym_spec = (int64_t)L.sym[0];
-    d->sym_sync = (int64_t)L.sym[1];
-    d->sym_write = (int64_t)L.sym[2];
-    if (L.bad) d->status = SDSJ_CORRUPT;
   }
 }
 
@@ -1238,10 +817,6 @@ hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, 
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s) {
   hipLaunchKernelGGL(k_unstuff, dim3(n), dim3(kUnstuffThreads), 0, s, n, blob, offsets, descs, scratch);
-  return hipGetLastError();
-}
-hipError_t launch_entropy(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
-  hipLaunchKernelGGL(k_entropy, dim3(n), dim3(kDecodeThreads), 0, s, n, descs, tables, scratch);
   return hipGetLastError();
 }
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {

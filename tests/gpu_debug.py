@@ -29,10 +29,12 @@ class ImgDescC(ctypes.Structure):
                 ("blk_comp", i32 * 10), ("blk_dx", i32 * 10), ("blk_dy", i32 * 10), ("comp", CompDescC * 3)] + \
                [(n, i32) for n in ("geo", "cx0", "cy0", "cw", "ch", "need_h", "need_v", "ksh", "ksv", "yf", "yl",
                                    "src_y0", "src_y1", "src_x0", "src_w", "sub_bits", "nsub_cap")] + \
-               [(n, i64) for n in ("off_ustream", "ustream_cap", "off_seg", "off_sub", "off_coef", "off_planes",
+               [(n, i64) for n in ("off_ustream", "ustream_cap", "off_seg", "off_sub", "off_rec", "off_coef", "off_planes",
                                    "off_rgb", "off_tmp", "off_kh", "off_kv", "need")] + \
                [("nsub", i32), ("useg_found", i32), ("ulen", i64), ("sync_rounds", i32), ("pad0", i32),
-                ("sym_spec", i64), ("sym_sync", i64), ("sym_write", i64)]
+                ("sym_spec", i64), ("sym_sync", i64), ("sym_write", i64),
+                ("t_spec", i64), ("t_sync", i64), ("t_scan", i64), ("t_write", i64), ("it_spec", i64), ("it_sync", i64),
+                ("it_write", i64)]
 
 
 def _memcpy_d2h(ptr: int, nbytes: int) -> np.ndarray:
