@@ -16,7 +16,8 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsdsj.so")
+# SDSJ_LIBRARY: an alternative in-tree build (kernel experiments under tools/); default = the product
+LIB_PATH = os.environ.get("SDSJ_LIBRARY") or os.path.join(_HERE, "lib", "libsdsj.so")
 
 SDSJ_ABI_VERSION = 1
 OK, EINVAL, UNSUPPORTED, CORRUPT, ENOMEM, EHIP, ECAPACITY = 0, -1, -2, -3, -4, -5, -6

@@ -25,6 +25,9 @@ constexpr int kRec = 64;              // block-boundary records kept per subsequ
 constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
 constexpr int kUPad = 128;            // zero bytes after each unstuffed stream (bit-reader prefetch)
+constexpr int kMaxSpan = 960;         // source columns per fused-resample tile (LDS row width)
+constexpr int kRingDW = 3072;         // fused-resample ring (dwords): ring_rows x (3072 / ring_rows) columns
+constexpr int kRingMaxRows = 16;      // vertical windows longer than this use the unfused path
 
 // Raw DHT content (bits[1..16], huffval) -- jdmarker.c get_dht.
 struct HuffSpec {
@@ -106,6 +109,12 @@ struct ImgDesc {
   // lane utilisation / phase timing diagnostics (s_memtime ticks, wave-loop iterations x 64)
   int64_t t_spec, t_sync, t_scan, t_write;
   int64_t it_spec, it_sync, it_write;
+  // fused resample (sdsj_resample.hip): 1 when every tile of tile_w output columns needs at most
+  // kMaxSpan source columns; 0 -> the unfused colour / h-pass / v-pass kernels
+  int32_t fused, tile_w, ring_rows;
+  int32_t pad1;
+  // k_resample phase ticks (s_memtime, summed over the image's workgroups; experiment builds only)
+  int64_t t_rs[4];
 };
 
 // Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).

@@ -19,8 +19,9 @@
 using namespace sdsj;
 
 namespace {
-constexpr int kStages = 10;
-const char* kStageNames[kStages] = {"parse", "plan", "unstuff", "entsync", "entwrite", "idct", "color", "coeffs", "hpass", "vpass"};
+constexpr int kStages = 11;
+const char* kStageNames[kStages] = {"parse", "plan",  "unstuff", "entsync", "entwrite", "idct",
+                                    "color", "coeffs", "hpass",   "vpass",   "resample"};
 }  // namespace
 
 struct sdsj_engine {
@@ -160,6 +161,8 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
   mark(9);
   SDSJ_HIP(e, launch_vpass(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_lut, s));
   mark(10);
+  SDSJ_HIP(e, launch_resample(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_lut, s));
+  mark(11);
   return SDSJ_OK;
 }
 

@@ -121,16 +121,22 @@ __device__ int load_tables(EntTables& T, const ImgDesc* d, const ImgTables* tb) 
 }
 
 // ------------------------------------------------------------------------------------------
-// Bit reader: 64-bit MSB-first window; one 32-bit word prefetched ahead (its load is issued at
-// the previous refill, ~4 symbols earlier).
+// Bit reader: 64-bit MSB-first window fed from a queue of kQ byte-swapped words held in
+// registers.  The queue is refilled for every lane of a wave at once (bits_fill) when any lane
+// has run dry; the byte swap consumes the loads there, so the decode loop itself carries no
+// global loads.  (CDNA counts loads and stores on one vmcnt: a load waited on inside the loop
+// would also wait for every coefficient/record store issued since.)
 // ------------------------------------------------------------------------------------------
+constexpr int kQ = 8;
+
 struct Bits {
   const uint32_t* src;
   uint64_t buf;
   int nb;
-  uint32_t nw;   // next word (big-endian, as loaded)
-  uint32_t wi;   // index of the word after nw
+  int nq;        // valid words in q
+  uint32_t wi;   // word index of q[0]
   uint32_t pos;  // absolute bit position of the next unconsumed bit
+  uint32_t q[kQ];
 };
 
 __device__ __forceinline__ void bits_init(Bits& b, const uint32_t* src, uint32_t p) {
@@ -140,16 +146,31 @@ __device__ __forceinline__ void bits_init(Bits& b, const uint32_t* src, uint32_t
   const int sh = p & 31;
   b.buf = (((uint64_t)hi << 32) | lo) << sh;
   b.nb = 64 - sh;
-  b.nw = src[w + 2];
-  b.wi = w + 3;
+  b.nq = 0;
+  b.wi = w + 2;
   b.pos = p;
+#pragma unroll
+  for (int k = 0; k < kQ; k++) b.q[k] = 0;
 }
 
-__device__ __forceinline__ void bits_refill(Bits& b) {
+// Wave-synchronous refill: re-reads kQ words from wi (the ustream carries kUPad bytes of slack).
+__device__ __forceinline__ void bits_fill(Bits& b) {
+#pragma unroll
+  for (int k = 0; k < kQ; k++) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+  b.nq = kQ;
+}
+
+// Can the next symbol (at most 32 bits) be decoded without a refill?
+__device__ __forceinline__ bool bits_can(const Bits& b) { return b.nb > 32 || b.nq > 0; }
+
+__device__ __forceinline__ void bits_pull(Bits& b) {
   if (b.nb <= 32) {
-    b.buf |= (uint64_t)__builtin_bswap32(b.nw) << (32 - b.nb);
+    b.buf |= (uint64_t)b.q[0] << (32 - b.nb);
     b.nb += 32;
-    b.nw = b.src[b.wi++];
+#pragma unroll
+    for (int k = 0; k + 1 < kQ; k++) b.q[k] = b.q[k + 1];
+    b.nq--;
+    b.wi++;
   }
 }
 
@@ -178,17 +199,19 @@ __device__ __forceinline__ BlkCtx make_ctx(const EntTables& T, int bpm) {
 template <int LB>
 __device__ __forceinline__ void decode_sym(const EntTables& T, Bits& b, int slot, bool isdc, int& s, int& r, int& val,
                                            int& bad) {
-  bits_refill(b);
+  bits_pull(b);
   const uint32_t hi = (uint32_t)(b.buf >> 32);
   const uint32_t e = T.lut[(slot << LB) + (hi >> (32 - LB))];
   int l = e & 15;
   s = (e >> 4) & 15;
   r = (e >> 8) & 15;
   if (l == 0) {
-    // jpeg_huff_decode: canonical search (longer codes, or a DC category > 15)
+    // jpeg_huff_decode: canonical search (longer codes, or a DC category > 15) -- the first
+    // length whose code is <= maxcode; all 16 compares issue together
     const uint32_t peek = hi >> 16;
-    int ll = 1;
-    while (ll <= 16 && (int32_t)(peek >> (16 - ll)) > T.maxcode[slot][ll]) ll++;
+    int ll = 17;
+#pragma unroll
+    for (int k = 16; k >= 1; k--) ll = (int32_t)(peek >> (16 - k)) <= T.maxcode[slot][k] ? k : ll;
     if (ll > 16) {
       bad = 1;  // JWRN_HUFF_BAD_CODE
       l = 16;
@@ -267,21 +290,30 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
   int blk = 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
   int d0 = 0, d1 = 0, d2 = 0;
   int c = ctx_c(K, 0), sdc = ctx_dc(K, 0), sac = ctx_ac(K, 0);
-  while (b.pos < end) {
-    int s, r, val;
-    const bool isdc = z == 0;
-    decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
-    nsym++;
-    dcd = isdc ? val : dcd;
-    add_dc(c, isdc ? val : 0, d0, d1, d2);
-    if (next_z(z, s, r)) {
-      if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
-      nrec++;
-      blk = blk + 1 == K.bpm ? 0 : blk + 1;
-      c = ctx_c(K, blk);
-      sdc = ctx_dc(K, blk);
-      sac = ctx_ac(K, blk);
-      nblk++;
+  bool run = b.pos < end;
+  while (__builtin_amdgcn_ballot_w64(run)) {
+    if (run) bits_fill(b);
+    for (;;) {
+      // leave to refill as soon as any running lane is dry
+      if (__builtin_amdgcn_ballot_w64(run && !bits_can(b)) || !__builtin_amdgcn_ballot_w64(run)) break;
+      if (run) {
+        int s, r, val;
+        const bool isdc = z == 0;
+        decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+        nsym++;
+        dcd = isdc ? val : dcd;
+        add_dc(c, isdc ? val : 0, d0, d1, d2);
+        if (next_z(z, s, r)) {
+          if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
+          nrec++;
+          blk = blk + 1 == K.bpm ? 0 : blk + 1;
+          c = ctx_c(K, blk);
+          sdc = ctx_dc(K, blk);
+          sac = ctx_ac(K, blk);
+          nblk++;
+        }
+        run = b.pos < end;
+      }
     }
   }
   S.entry_p = start;
@@ -294,6 +326,20 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
   S.spec_dc[2] = S.cur_dc[2] = d2;
   S.nrec = nrec < kRec ? nrec : kRec;
   return nsym;
+}
+
+// Records of the speculative pass, kRQ at a time in registers (filled with the bit queue).
+constexpr int kRQ = 6;
+
+__device__ __forceinline__ void rec_fill(const SyncRec* rec, int ri, int nrec, uint32_t* rp, uint32_t* rx) {
+  const uint2* r2 = reinterpret_cast<const uint2*>(rec);
+#pragma unroll
+  for (int k = 0; k < kRQ; k++) {
+    const int i = ri + k;
+    const uint2 v = r2[i < kRec ? i : kRec - 1];
+    rp[k] = i < nrec ? v.x : 0xFFFFFFFFu;  // past the last record: never reached
+    rx[k] = i < nrec ? v.y : 0u;           // dc (low 16 bits) | blk << 16
+  }
 }
 
 // Resumable re-decode of S (state in S.res_*), at most `budget` symbols.  Returns true when the
@@ -312,39 +358,74 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
   int q0 = S.res_q[0], q1 = S.res_q[1], q2 = S.res_q[2];  // speculative DC prefix up to record ri
   int bad = 0, nsym = 0;
   int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
-  SyncRec R = ri < nrec ? rec[ri] : SyncRec{0xFFFFFFFFu, 0, 0, 0};
-  while (b.pos < end && nsym < budget) {
-    int s, r, val;
-    const bool isdc = z == 0;
-    decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
-    nsym++;
-    add_dc(c, isdc ? val : 0, d0, d1, d2);
-    if (next_z(z, s, r)) {
-      const int done_blk = blk;
-      blk = blk + 1 == K.bpm ? 0 : blk + 1;
-      c = ctx_c(K, blk);
-      sdc = ctx_dc(K, blk);
-      sac = ctx_ac(K, blk);
-      nblk++;
-      while (R.p <= b.pos) {
-        add_dc(ctx_c(K, R.blk), R.dc, q0, q1, q2);
-        ri++;
-        if (R.p == b.pos && R.blk == done_blk) {
-          // merged with the speculative path: its remainder is exact
-          S.new_exit_p = S.spec_exit_p;
-          S.new_exit_bz = S.spec_exit_bz;
-          S.new_nblk = nblk + S.spec_nblk - ri;
-          S.new_dc[0] = d0 + S.spec_dc[0] - q0;
-          S.new_dc[1] = d1 + S.spec_dc[1] - q1;
-          S.new_dc[2] = d2 + S.spec_dc[2] - q2;
-          *nsym_out = nsym;
-          return true;
+  uint32_t rp[kRQ], rx[kRQ];
+  int nr = 0, done_blk = 0;
+  uint32_t P = 0;
+  bool adv = false, merged = false;  // adv: records up to boundary P still to be passed
+  bool run = b.pos < end && budget > 0;
+  while (__builtin_amdgcn_ballot_w64(run)) {
+    if (run) {
+      bits_fill(b);
+      rec_fill(rec, ri, nrec, rp, rx);
+      nr = kRQ;
+    }
+    for (;;) {
+      const bool dry = run && (adv ? nr == 0 : !bits_can(b));
+      if (__builtin_amdgcn_ballot_w64(dry) || !__builtin_amdgcn_ballot_w64(run)) break;
+      if (run) {
+        if (!adv) {
+          int s, r, val;
+          const bool isdc = z == 0;
+          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+          nsym++;
+          add_dc(c, isdc ? val : 0, d0, d1, d2);
+          if (next_z(z, s, r)) {
+            done_blk = blk;
+            blk = blk + 1 == K.bpm ? 0 : blk + 1;
+            c = ctx_c(K, blk);
+            sdc = ctx_dc(K, blk);
+            sac = ctx_ac(K, blk);
+            nblk++;
+            adv = true;
+            P = b.pos;
+          }
         }
-        R = ri < nrec ? rec[ri] : SyncRec{0xFFFFFFFFu, 0, 0, 0};
+        // pass the records at or before P; a record at P of the same MCU block = merged paths
+        while (adv && nr > 0) {
+          const uint32_t Rp = rp[0], Rx = rx[0];
+          if (Rp > P) {
+            adv = false;
+            break;
+          }
+          const int rb = (int)(Rx >> 16) & 0xFF;
+          add_dc(ctx_c(K, rb), (int)(int16_t)(Rx & 0xFFFF), q0, q1, q2);
+          ri++;
+#pragma unroll
+          for (int k = 0; k + 1 < kRQ; k++) {
+            rp[k] = rp[k + 1];
+            rx[k] = rx[k + 1];
+          }
+          nr--;
+          if (Rp == P && rb == done_blk) {
+            merged = true;
+            adv = false;
+          }
+        }
+        run = !merged && (adv || (b.pos < end && nsym < budget));
       }
     }
   }
   *nsym_out = nsym;
+  if (merged) {
+    // the remainder of the speculative result is exact
+    S.new_exit_p = S.spec_exit_p;
+    S.new_exit_bz = S.spec_exit_bz;
+    S.new_nblk = nblk + S.spec_nblk - ri;
+    S.new_dc[0] = d0 + S.spec_dc[0] - q0;
+    S.new_dc[1] = d1 + S.spec_dc[1] - q1;
+    S.new_dc[2] = d2 + S.spec_dc[2] - q2;
+    return true;
+  }
   if (b.pos >= end) {
     S.new_exit_p = b.pos;
     S.new_exit_bz = (uint16_t)((blk << 8) | z);
@@ -670,59 +751,63 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
       bits_init(b, src, S.entry_p);
       run = g < gend && (b.pos < end_bit || z != 0);
     }
-    while (__builtin_amdgcn_ballot_w64(run) != 0) {
-      witers++;
-      bool ready = false;
-      uint32_t gdone = 0;
-      if (run) {
-        int s, r, val, sb = 0;
-        const bool isdc = z == 0;
-        decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
-        nsym++;
-        bad |= sb;
-        // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
-        const int add = isdc ? val : 0;
-        p0 += c == 0 ? add : 0;
-        p1 += c == 1 ? add : 0;
-        p2 += c == 2 ? add : 0;
-        const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
-        const int wpos = isdc ? 0 : (int)T.nat[z + r];
-        L.stage[((writing && (isdc || s)) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pv : val);
-        if (next_z(z, s, r)) {
-          ready = writing;
-          gdone = (uint32_t)g;
-          blk = blk + 1 == K.bpm ? 0 : blk + 1;
-          c = ctx_c(K, blk);
-          sdc = ctx_dc(K, blk);
-          sac = ctx_ac(K, blk);
-          g++;
-          writing = true;
-          if (g == gend) done_p = b.pos;
-        }
-        run = g < gend && (b.pos < end_bit || z != 0);
-      }
-      // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
-      const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
-      if (m) {
-        const int cnt = __popcll(m);
-        if (ready) {
-          const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-          L.flist[wv][idx] = ((uint32_t)t << 24) | gdone;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        for (int b0 = 0; b0 < cnt; b0 += 8) {
-          const int bi = b0 + (lane >> 3);
-          if (bi < cnt) {
-            const uint32_t f = L.flist[wv][bi];
-            uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
-            const uint4 v = *sp;
-            reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64)[lane & 7] = v;
-            *sp = make_uint4(0, 0, 0, 0);
+    while (__builtin_amdgcn_ballot_w64(run)) {
+      if (run) bits_fill(b);
+      for (;;) {
+        if (__builtin_amdgcn_ballot_w64(run && !bits_can(b)) || !__builtin_amdgcn_ballot_w64(run)) break;
+        witers++;
+        bool ready = false;
+        uint32_t gdone = 0;
+        if (run) {
+          int s, r, val, sb = 0;
+          const bool isdc = z == 0;
+          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
+          nsym++;
+          bad |= sb;
+          // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
+          const int add = isdc ? val : 0;
+          p0 += c == 0 ? add : 0;
+          p1 += c == 1 ? add : 0;
+          p2 += c == 2 ? add : 0;
+          const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
+          const int wpos = isdc ? 0 : (int)T.nat[z + r];
+          L.stage[((writing && (isdc || s)) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pv : val);
+          if (next_z(z, s, r)) {
+            ready = writing;
+            gdone = (uint32_t)g;
+            blk = blk + 1 == K.bpm ? 0 : blk + 1;
+            c = ctx_c(K, blk);
+            sdc = ctx_dc(K, blk);
+            sac = ctx_ac(K, blk);
+            g++;
+            writing = true;
+            if (g == gend) done_p = b.pos;
           }
+          run = g < gend && (b.pos < end_bit || z != 0);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
+        // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
+        const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
+        if (m) {
+          const int cnt = __popcll(m);
+          if (ready) {
+            const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            L.flist[wv][idx] = ((uint32_t)t << 24) | gdone;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          for (int b0 = 0; b0 < cnt; b0 += 8) {
+            const int bi = b0 + (lane >> 3);
+            if (bi < cnt) {
+              const uint32_t f = L.flist[wv][bi];
+              uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
+              const uint4 v = *sp;
+              reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64)[lane & 7] = v;
+              *sp = make_uint4(0, 0, 0, 0);
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+        }
       }
     }
     if (active && last_of_seg) {

@@ -12,6 +12,8 @@
 //   k_hpass    horizontal pass, uint8 out         Pillow ImagingResampleHorizontal_8bpc
 //   k_vpass    vertical pass + hflip + layout/LUT Pillow ImagingResampleVertical_8bpc,
 //                                                 functional.py:102-110, presets.py:154-162
+//   (k_color / k_hpass / k_vpass only run for images with fused = 0; the others, and every
+//    failed sample, go through k_resample in sdsj_resample.hip)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -90,6 +92,27 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
   d->src_y1 = d->cy0 + d->yl;
   d->src_x0 = d->cx0;
   d->src_w = d->geo == kGeoZeros ? 0 : d->cw;
+  // fused resample tiles: halve the tile width until a tile's source columns fit kMaxSpan
+  // (bound: (tw - 1) * scale + 2 * support + 2 columns, Pillow precompute_coeffs windows)
+  d->fused = 0;
+  d->tile_w = 0;
+  d->ring_rows = 1;
+  while (d->ring_rows < d->ksv) d->ring_rows *= 2;  // vertical window rows kept per column
+  if (d->geo != kGeoZeros && d->ring_rows <= kRingMaxRows) {
+    const double scale = d->need_h ? (double)d->cw / op.out_w : 1.0;
+    const double supp = d->need_h ? sup * (scale < 1.0 ? 1.0 : scale) : 0.0;
+    int tw = op.out_w < 256 ? op.out_w : 256;
+    if (tw > kRingDW / d->ring_rows) tw = kRingDW / d->ring_rows;
+    for (;;) {
+      if ((double)tw * scale + 2.0 * supp + 4.0 <= (double)kMaxSpan) {
+        d->fused = 1;
+        d->tile_w = tw;
+        break;
+      }
+      if (tw == 1) break;
+      tw = (tw + 1) / 2;
+    }
+  }
   d->sub_bits = (int32_t)align_up((d->entropy_len * 8 + kDecodeThreads - 1) / kDecodeThreads, 32);
   if (d->sub_bits < kMinSubBits) d->sub_bits = kMinSubBits;
   d->nsub_cap = (int32_t)((d->entropy_len * 8 + d->sub_bits - 1) / d->sub_bits) + d->nseg + 1;
@@ -109,8 +132,8 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
   int64_t planes = 0;
   for (int c = 0; c < d->ncomp; c++) planes += align_up((int64_t)d->comp[c].pitch * d->comp[c].bh * 8, 256);
   d->off_planes = take(planes);
-  d->off_rgb = take((int64_t)d->src_w * (d->src_y1 - d->src_y0) * 3);
-  d->off_tmp = take(d->need_h ? (int64_t)(d->yl - d->yf) * op.out_w * 3 : 0);
+  d->off_rgb = take(d->fused ? 0 : (int64_t)d->src_w * (d->src_y1 - d->src_y0) * 3);
+  d->off_tmp = take(!d->fused && d->need_h ? (int64_t)(d->yl - d->yf) * op.out_w * 3 : 0);
   d->off_kh = take(d->need_h ? ((int64_t)2 * op.out_w + (int64_t)op.out_w * d->ksh) * 4 : 0);
   d->off_kv = take(d->need_v ? ((int64_t)2 * op.out_h + (int64_t)op.out_h * d->ksv) * 4 : 0);
   d->need = o;
@@ -141,6 +164,7 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
     if (status == SDSJ_OK) status = setup_geometry(&sd, &st);
     if (status == SDSJ_OK) plan_image(&sd, op);
     sd.status = status;
+    for (int k = 0; k < 4; k++) sd.t_rs[k] = 0;
     s_status = status;
   }
   __syncthreads();
@@ -576,7 +600,7 @@ __global__ void __launch_bounds__(256) k_color(int n, const ImgDesc* __restrict_
   const int img = blockIdx.y;
   if (img >= n) return;
   const ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
+  if (d->status != SDSJ_OK || d->geo == kGeoZeros || d->fused) return;
   const int w = d->src_w, h = d->src_y1 - d->src_y0;
   const int64_t total = (int64_t)w * h;
   const uint8_t* planes = scratch + d->off_planes;
@@ -694,7 +718,7 @@ __global__ void __launch_bounds__(256) k_hpass(int n, const ImgDesc* __restrict_
   const int img = blockIdx.y;
   if (img >= n) return;
   const ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK || !d->need_h) return;
+  if (d->status != SDSJ_OK || !d->need_h || d->fused) return;
   const int rows = d->yl - d->yf, ow = op.out_w;
   const int64_t total = (int64_t)rows * ow;
   const int32_t* bounds = reinterpret_cast<const int32_t*>(scratch + d->off_kh);
@@ -735,9 +759,10 @@ __global__ void __launch_bounds__(256) k_vpass(int n, const ImgDesc* __restrict_
   const int oh = op.out_h, ow = op.out_w;
   const int64_t plane = (int64_t)oh * ow;
   const int64_t total = plane;
-  const bool ok = d->status == SDSJ_OK;
-  if (blockIdx.x == 0 && threadIdx.x == 0) status[img] = d->status;
-  const bool zeros = !ok || d->geo == kGeoZeros;
+  // failed / empty-crop / fused images are written (and their status published) by k_resample
+  if (d->status != SDSJ_OK || d->geo == kGeoZeros || d->fused) return;
+  (void)status;
+  const bool zeros = false;
   const bool fl = flip ? flip[img] != 0 : false;
   const bool f32 = op.out_dtype == SDSJ_DTYPE_F32;
   const bool hwc = op.layout == SDSJ_LAYOUT_HWC;

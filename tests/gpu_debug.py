@@ -34,7 +34,7 @@ class ImgDescC(ctypes.Structure):
                [("nsub", i32), ("useg_found", i32), ("ulen", i64), ("sync_rounds", i32), ("pad0", i32),
                 ("sym_spec", i64), ("sym_sync", i64), ("sym_write", i64),
                 ("t_spec", i64), ("t_sync", i64), ("t_scan", i64), ("t_write", i64), ("it_spec", i64), ("it_sync", i64),
-                ("it_write", i64)]
+                ("it_write", i64), ("fused", i32), ("tile_w", i32), ("ring_rows", i32), ("pad1", i32), ("t_rs", i64 * 4)]
 
 
 def _memcpy_d2h(ptr: int, nbytes: int) -> np.ndarray:
@@ -99,11 +99,14 @@ def stage_report(engine, jpg: bytes, resolution=(256, 256)) -> list[str]:
         bad = np.argwhere((got != ref).any(-1))
         lines.append(f"coef comp{c}: {len(bad)} / {ref.shape[0] * ref.shape[1]} blocks differ "
                      f"{bad[:4].tolist()}")
-    rgb_ref = O.decode(jpg)
-    h = d.src_y1 - d.src_y0
-    rgb = fetch(d.off_rgb, d.src_w * h * 3).reshape(h, d.src_w, 3)
-    ref_rows = rgb_ref[d.src_y0:d.src_y1, d.src_x0:d.src_x0 + d.src_w]
-    lines.append(f"rgb rows: {int((rgb != ref_rows).any(-1).sum())} px differ of {rgb.shape[0] * rgb.shape[1]}")
+    if not d.fused:  # the unfused path materialises the RGB rows
+        rgb_ref = O.decode(jpg)
+        h = d.src_y1 - d.src_y0
+        rgb = fetch(d.off_rgb, d.src_w * h * 3).reshape(h, d.src_w, 3)
+        ref_rows = rgb_ref[d.src_y0:d.src_y1, d.src_x0:d.src_x0 + d.src_w]
+        lines.append(f"rgb rows: {int((rgb != ref_rows).any(-1).sum())} px differ of {rgb.shape[0] * rgb.shape[1]}")
+    else:
+        lines.append(f"fused resample, tile_w={d.tile_w}")
     ref_out = O.pipeline(jpg, resolution)
     got_out = out[0].cpu().numpy()
     lines.append(f"final: {int((got_out != ref_out).sum())} values differ")
