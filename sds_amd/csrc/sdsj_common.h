@@ -112,7 +112,7 @@ struct ImgDesc {
   // fused resample (sdsj_resample.hip): 1 when every tile of tile_w output columns needs at most
   // kMaxSpan source columns; 0 -> the unfused colour / h-pass / v-pass kernels
   int32_t fused, tile_w, ring_rows;
-  int32_t pad1;
+  int32_t rs_fast;  // > 0: tap count of the specialised 4:2:0 kernel (k_rs420<rs_fast>), 0: generic k_resample
   // k_resample phase ticks (s_memtime, summed over the image's workgroups; experiment builds only)
   int64_t t_rs[4];
 };

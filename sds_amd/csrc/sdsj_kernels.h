@@ -20,6 +20,8 @@ hipError_t launch_vpass(int n, const ImgDesc* descs, const sdsj_op& op, const ui
                         void* out, int32_t* status, const float* lut, hipStream_t s);
 hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
                            void* out, int32_t* status, const float* lut, hipStream_t s);
+hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
+                              const uint8_t* flip, void* out, const float* lut, hipStream_t s);
 // host-side planning (same code as k_parse): returns the scratch bytes image `jpg` needs, or < 0
 int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status);
 }  // namespace sdsj

@@ -113,6 +113,14 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
       tw = (tw + 1) / 2;
     }
   }
+  // specialised fused kernel: 4:2:0 (h2v2 fancy chroma), horizontal and vertical passes, odd tap
+  // counts 3..11 (sdsj_resample420.hip); everything else takes the generic k_resample
+  d->rs_fast = 0;
+  if (d->fused && d->ncomp == 3 && d->need_h && d->need_v && d->ksh >= 3 && d->ksh <= 11 && (d->ksh & 1) &&
+      d->ring_rows <= kRingMaxRows && d->comp[0].rh == 1 && d->comp[0].rv == 1 && d->comp[1].rh == 2 &&
+      d->comp[1].rv == 2 && d->comp[2].rh == 2 && d->comp[2].rv == 2 && d->comp[1].dw > 2 &&
+      d->comp[2].dw == d->comp[1].dw && d->comp[2].dh == d->comp[1].dh)
+    d->rs_fast = d->ksh;
   d->sub_bits = (int32_t)align_up((d->entropy_len * 8 + kDecodeThreads - 1) / kDecodeThreads, 32);
   if (d->sub_bits < kMinSubBits) d->sub_bits = kMinSubBits;
   d->nsub_cap = (int32_t)((d->entropy_len * 8 + d->sub_bits - 1) / d->sub_bits) + d->nseg + 1;

@@ -21,6 +21,7 @@
 
 #include "sdsj_common.h"
 #include "sdsj_kernels.h"
+#include "sdsj_pixel.h"
 
 namespace sdsj {
 
@@ -36,8 +37,6 @@ constexpr int kStepRows = 4;                 // source rows per step (fewer when
 constexpr int kStageDW = 2944;               // staging pool (dwords): plane rows of one step
 constexpr int kRgbW = kMaxSpan + 32;         // LDS RGB row pitch (+ over-read of unused taps)
 
-constexpr int kMaxStrip = 64;                // output rows per workgroup (strip) at most
-constexpr int kVTaps = 16;                   // vertical taps staged in LDS (= the largest ring)
 
 struct LdsResample {
   uint32_t st[kStageDW];                     // plane rows of the step, row-contiguous (global_load_lds)
@@ -98,50 +97,9 @@ __device__ __forceinline__ int up_lds(const uint8_t* r0, const uint8_t* r1, int 
   return jx == dw - 1 ? a : (a * 3 + r0[jx + 1] + 2) >> 2;
 }
 
-__device__ __forceinline__ int rs_clip8(int32_t v) {
-  v >>= 22;
-  return v < 0 ? 0 : v > 255 ? 255 : v;
-}
-
-__device__ __forceinline__ int clamp255i(int v) { return v < 0 ? 0 : v > 255 ? 255 : v; }
-
-// jdcolor.c ycc_rgb_convert (its tables evaluated arithmetically); cb, cr already minus 128
-// (24-bit multiplies: |constant| < 2^17, |cb|, |cr| <= 128 -- exact, full rate)
-__device__ __forceinline__ void ycc_px(int y, int cb, int cr, int& r, int& g, int& b) {
-  r = clamp255i(y + ((__mul24(91881, cr) + 32768) >> 16));
-  g = clamp255i(y + ((__mul24(-46802, cr) + (__mul24(-22554, cb) + 32768)) >> 16));
-  b = clamp255i(y + ((__mul24(116130, cb) + 32768) >> 16));
-}
-
-// pixel (0..255) x Pillow coefficient (|k| < 2^23: normalised weights of magnitude < 2 in
-// 22-bit fixed point) -- exact in a 24-bit multiply (v_mad_i32_i24, full rate)
-__device__ __forceinline__ int32_t tap(int32_t px, int32_t k) { return __mul24(px, k); }
-
-enum { kLayGeneric = 0, kLay420 = 1, kLayFull = 2 };
-
-// Output addressing: element (channel c, pixel p) at base + p * ps + c * cs (elements).
-struct OutMap {
-  int64_t base, ps, cs;
-  bool f32;
-};
-
-__device__ __forceinline__ void put3(void* out, const OutMap& m, const float* lut, int64_t pix, int v0, int v1, int v2) {
-  const int64_t e = m.base + pix * m.ps;
-  if (m.f32) {
-    float* o = reinterpret_cast<float*>(out) + e;
-    o[0] = lut[v0];
-    o[m.cs] = lut[v1];
-    o[2 * m.cs] = lut[v2];
-  } else {
-    uint8_t* o = reinterpret_cast<uint8_t*>(out) + e;
-    o[0] = (uint8_t)v0;
-    o[m.cs] = (uint8_t)v1;
-    o[2 * m.cs] = (uint8_t)v2;
-  }
-}
-
 struct RsArgs {
   const ImgDesc* d;
+  CompDesc cg[kMaxComp];  // component geometry in registers (descriptor loads cannot be hoisted past stores)
   ImgDesc* dmut;  // diagnostics (SDSJ_RS_TIMING)
   const uint8_t* planes;
   const int32_t *bh, *kh, *bv, *kv;
@@ -161,10 +119,10 @@ __device__ __forceinline__ void convert_row(LdsResample& L, const RsArgs& A, int
 #pragma unroll
   for (int c = 0; c < kMaxComp; c++) {
     int i = y, f = y;
-    if (d->comp[c].rv == 2) {
+    if (A.cg[c].rv == 2) {
       i = y >> 1;
       f = (y & 1) ? i + 1 : i - 1;
-      f = f < 0 ? 0 : (f > d->comp[c].dh - 1 ? d->comp[c].dh - 1 : f);
+      f = f < 0 ? 0 : (f > A.cg[c].dh - 1 ? A.cg[c].dh - 1 : f);
     }
     rowi[c] = soff[c] + (i - ilo[c]) * nd[c];
     rowf[c] = soff[c] + (f - ilo[c]) * nd[c];
@@ -182,7 +140,7 @@ __device__ __forceinline__ void convert_row(LdsResample& L, const RsArgs& A, int
   if (A.layout == kLay420) {
     // h2v2_fancy_upsample on pixel pairs (2j, 2j + 1): both use column sum j, the even one blends
     // column j - 1 in, the odd one column j + 1 (edges repeat column j)
-    const int dw = d->comp[1].dw;
+    const int dw = A.cg[1].dw;
     const int j0 = ax0 >> 1, np = ((ax1 - 1) >> 1) - j0 + 1;
     for (int p = t; p < np; p += kRsThreads) {
       const int j = j0 + p, jm = j > 0 ? j - 1 : j, jp = j < dw - 1 ? j + 1 : j;
@@ -212,7 +170,7 @@ __device__ __forceinline__ void convert_row(LdsResample& L, const RsArgs& A, int
       oB[x] = (uint8_t)bb;
     }
   } else {
-    const CompDesc &c0 = d->comp[0], &c1 = d->comp[1], &c2 = d->comp[2];
+    const CompDesc &c0 = A.cg[0], &c1 = A.cg[1], &c2 = A.cg[2];
     for (int x = ax0 + t; x < ax1; x += kRsThreads) {
       const int Y = up_lds(a0, b0, c0.rh, c0.rv, c0.dw, x, y);
       int r = Y, g = Y, bb = Y;
@@ -242,13 +200,13 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
   int jal[kMaxComp] = {0, 0, 0}, nd[kMaxComp] = {0, 0, 0};
 #pragma unroll
   for (int c = 0; c < kMaxComp; c++)
-    if (c < A.ncomp) comp_cols(d->comp[c], ax0, ax1, &jal[c], &nd[c]);
+    if (c < A.ncomp) comp_cols(A.cg[c], ax0, ax1, &jal[c], &nd[c]);
   int rs = kStepRows;  // rows per step that fit the staging pool
   for (;;) {
     int need = 0;
 #pragma unroll
     for (int c = 0; c < kMaxComp; c++)
-      if (c < A.ncomp) need += (d->comp[c].rv == 2 ? rs / 2 + 2 : rs) * nd[c];
+      if (c < A.ncomp) need += (A.cg[c].rv == 2 ? rs / 2 + 2 : rs) * nd[c];
     if (need <= kStageDW || rs == 1) break;
     rs--;
   }
@@ -304,7 +262,7 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
       for (int c = 0; c < kMaxComp; c++) {
         soff[c] = o;
         if (c >= A.ncomp) continue;
-        const CompDesc& cd = d->comp[c];
+        const CompDesc& cd = A.cg[c];
         int ihi;
         comp_rows(cd, ya, yb, &ilo[c], &ihi);
         const int nch = (nd[c] + 63) >> 6;
@@ -410,7 +368,7 @@ __global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* _
         put3(out, A.om, lut, (int64_t)oy * A.ow + xx, 0, 0, 0);
     return;
   }
-  if (!d->fused) return;
+  if (!d->fused || d->rs_fast) return;  // unfused path / the specialised 4:2:0 kernel
   __shared__ LdsResample L;
   A.d = d;
   A.dmut = const_cast<ImgDesc*>(d);
@@ -431,7 +389,8 @@ __global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* _
   A.ntiles = (A.ow + A.tw - 1) / A.tw;
   A.rmask = d->ring_rows - 1;
   A.rstride = kRingDW / d->ring_rows;
-  const CompDesc &c0 = d->comp[0], &c1 = d->comp[1], &c2 = d->comp[2];
+  for (int c = 0; c < kMaxComp; c++) A.cg[c] = d->comp[c];
+  const CompDesc &c0 = A.cg[0], &c1 = A.cg[1], &c2 = A.cg[2];
   A.layout = kLayGeneric;
   if (c0.rh == 1 && c0.rv == 1) {
     if (A.ncomp == 1 || (c1.rh == 1 && c1.rv == 1 && c2.rh == 1 && c2.rv == 1)) A.layout = kLayFull;
@@ -460,7 +419,9 @@ hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const
   const int strips = (op.out_h + strip_h - 1) / strip_h;
   hipLaunchKernelGGL(k_resample, dim3(n, strips, tiles), dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip,
                      out, status, lut);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_resample420(n, descs, op, strip_h, scratch, flip, out, lut, s);
 }
 
 }  // namespace sdsj

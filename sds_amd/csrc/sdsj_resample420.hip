@@ -1,0 +1,279 @@
+// sdsj_resample420.hip -- the fused colour + resample kernel specialised for the dominant case:
+// 4:2:0 YCbCr (h2v2 fancy chroma upsampling), a horizontal and a vertical Pillow pass, KT taps
+// (odd, 3..11).  Same arithmetic and the same streaming structure as k_resample
+// (sdsj_resample.hip, whose header describes the phases and the reference lines), with the
+// per-image geometry fixed at compile time where it matters:
+//   * conversion is one flattened loop over (step row, pixel pair); each item loads 12 chroma
+//     bytes + 2 luma bytes from the staged rows and writes each channel's pair as one u16;
+//   * staging offsets of the step's rows come from a small LDS table, not from uniform registers
+//     (keeps the scalar file from spilling);
+//   * the horizontal taps are KT exactly, coefficients in registers.
+// plan_image sets ImgDesc::rs_fast = KT for the images this kernel takes; k_resample skips them.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sdsj_common.h"
+#include "sdsj_kernels.h"
+#include "sdsj_pixel.h"
+
+#ifndef SDSJ_RS_TIMING
+#define SDSJ_RS_TIMING 0
+#endif
+
+namespace sdsj {
+
+constexpr int kFThreads = 256;
+constexpr int kFRows = 4;                               // source rows per step
+constexpr int kFYDW = kMaxSpan / 4 + 2;                 // staged luma row (dwords)
+constexpr int kFCDW = kMaxSpan / 8 + 3;                 // staged chroma row (dwords)
+constexpr int kFStageDW = kFRows * kFYDW + 2 * kFRows * kFCDW;
+constexpr int kFRgbW = kMaxSpan + 32;                   // RGB row pitch (bytes, even)
+
+struct LdsF {
+  uint32_t st[kFStageDW];                 // step's plane rows: 4 luma rows, then 4 Cb, 4 Cr rows
+  uint8_t rgb[kFRows][3][kFRgbW];         // converted rows, planar, column x at x - xb (xb even)
+  uint32_t ring[kRingDW];                 // per column: horizontal results of the last R rows
+  int32_t vb[kMaxStrip][2];               // strip rows: vertical window (first row, row count)
+  int32_t vw[kMaxStrip][kVTaps];          // strip rows: vertical weights
+  int32_t rinfo[kFRows][8];               // step row q: byte offsets of its Y, Cb i/f, Cr i/f rows
+};
+
+template <int KT>
+__global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+                                                      int strip_h, const uint8_t* __restrict__ scratch,
+                                                      const uint8_t* __restrict__ flip, void* __restrict__ out,
+                                                      const float* __restrict__ lut) {
+  const int img = blockIdx.x;
+  if (img >= n) return;
+  const ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || d->rs_fast != KT) return;
+  const int oh = op.out_h, ow = op.out_w;
+  const int oy0 = blockIdx.y * strip_h;
+  if (oy0 >= oh) return;
+  const int oy1 = oy0 + strip_h < oh ? oy0 + strip_h : oh;
+  __shared__ LdsF L;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t plane = (int64_t)oh * ow;
+  OutMap om;
+  om.f32 = op.out_dtype == SDSJ_DTYPE_F32;
+  om.base = (int64_t)img * plane * 3;
+  om.ps = op.layout == SDSJ_LAYOUT_HWC ? 3 : 1;
+  om.cs = op.layout == SDSJ_LAYOUT_HWC ? 1 : plane;
+  const bool fl = flip ? flip[img] != 0 : false;
+  const int32_t* bh = reinterpret_cast<const int32_t*>(scratch + d->off_kh);
+  const int32_t* kh = bh + 2 * ow;
+  const int32_t* bv = reinterpret_cast<const int32_t*>(scratch + d->off_kv);
+  const int32_t* kv = bv + 2 * oh;
+  const int ksv = d->ksv, cx0 = d->cx0, cy0 = d->cy0, tw = d->tile_w;
+  const int rmask = d->ring_rows - 1, rstride = kRingDW / d->ring_rows;
+  const int dwc = d->comp[1].dw, dhc = d->comp[1].dh;
+  const uint8_t* pY = scratch + d->off_planes + d->comp[0].plane_off;
+  const uint8_t* pCb = scratch + d->off_planes + d->comp[1].plane_off;
+  const uint8_t* pCr = scratch + d->off_planes + d->comp[2].plane_off;
+  const int pitchY = d->comp[0].pitch, pitchC = d->comp[1].pitch;
+  const int ntiles = (ow + tw - 1) / tw;
+  const int r_lo = bv[2 * oy0], r_hi = bv[2 * (oy1 - 1)] + bv[2 * (oy1 - 1) + 1];
+  // the strip's vertical windows and weights
+  for (int i = t; i < (oy1 - oy0) * kVTaps; i += kFThreads) {
+    const int b = i / kVTaps, k = i % kVTaps, oy = oy0 + b;
+    if (k == 0) {
+      L.vb[b][0] = bv[2 * oy];
+      L.vb[b][1] = bv[2 * oy + 1];
+    }
+    L.vw[b][k] = k < ksv ? kv[(int64_t)oy * ksv + k] : 0;
+  }
+  const uint8_t* stb = reinterpret_cast<const uint8_t*>(L.st);
+
+  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+    const int ox0 = tile * tw, ox1 = ox0 + tw < ow ? ox0 + tw : ow;
+    const int s_lo = bh[2 * ox0], s_hi = bh[2 * (ox1 - 1)] + bh[2 * (ox1 - 1) + 1];
+    const int ax0 = cx0 + s_lo, ax1 = cx0 + s_hi;  // image columns of the tile
+    const int jb = (ax0 >> 1) & ~3;                // first chroma column of the first 4-pair group
+    const int xb = 2 * jb;                         // rgb row origin (8-aligned: dword writes)
+    const int ng = (((ax1 - 1) >> 1) - jb) / 4 + 1;  // 4-pair groups covering [ax0, ax1)
+    // staged columns: luma [xb, xb + 8 ng), chroma [jb - 4, jb + 4 ng + 4).  Bytes past a row end
+    // (or before the first one) come from neighbouring scratch and only feed pixels outside the tile.
+    const int jalY = xb, ndY = 2 * ng;
+    const int jalC = jb - 4, ndC = ng + 2;
+    const int xx = ox0 + t;
+    const bool active = xx < ox1;
+    int hm = 0, hc = 0;
+    if (active) {
+      hm = bh[2 * xx] - s_lo + (ax0 - xb);
+      hc = bh[2 * xx + 1];
+    }
+    int32_t cf[KT];
+#pragma unroll
+    for (int j = 0; j < KT; j++) cf[j] = active && j < hc ? kh[(int64_t)xx * KT + j] : 0;
+    const uint8_t* hp = &L.rgb[0][0][0] + hm;
+    uint32_t* ring = L.ring + t;
+    const int ox = fl ? ow - 1 - xx : xx;
+    int nb = oy0;
+
+    uint64_t tk[4] = {0, 0, 0, 0}, tm = SDSJ_RS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
+    auto mark = [&](int k) {
+      if (SDSJ_RS_TIMING) {
+        const uint64_t now = __builtin_amdgcn_s_memtime();
+        tk[k] += now - tm;
+        tm = now;
+      }
+    };
+    for (int ra = r_lo; ra < r_hi; ra += kFRows) {
+      const int nr = r_hi - ra < kFRows ? r_hi - ra : kFRows;
+      const int ya = cy0 + ra;
+      int ilo = (ya >> 1) - 1, ihi = ((ya + nr - 1) >> 1) + 1;
+      ilo = ilo < 0 ? 0 : ilo;
+      ihi = ihi > dhc - 1 ? dhc - 1 : ihi;
+      const int nrc = ihi - ilo + 1;
+      // A. stage: luma rows ya.., chroma rows ilo..ihi (one global_load_lds_dword per 64 dwords)
+      for (int row = wv; row < nr + 2 * nrc; row += 4) {
+        const uint8_t* g;
+        int nd, o;
+        if (row < nr) {
+          g = pY + (int64_t)(ya + row) * pitchY + jalY;
+          nd = ndY;
+          o = row * kFYDW;
+        } else if (row < nr + nrc) {
+          g = pCb + (int64_t)(ilo + row - nr) * pitchC + jalC;
+          nd = ndC;
+          o = kFRows * kFYDW + (row - nr) * kFCDW;
+        } else {
+          g = pCr + (int64_t)(ilo + row - nr - nrc) * pitchC + jalC;
+          nd = ndC;
+          o = kFRows * kFYDW + kFRows * kFCDW + (row - nr - nrc) * kFCDW;
+        }
+        for (int h = 0; h < nd; h += 64)
+          if (h + lane < nd)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 4 * (h + lane)),
+                                             (__attribute__((address_space(3))) void*)(L.st + o + h), 4, 0, 0);
+      }
+      if (t < nr) {
+        const int y = ya + t, i = y >> 1;
+        int f = (y & 1) ? i + 1 : i - 1;
+        f = f < 0 ? 0 : (f > dhc - 1 ? dhc - 1 : f);
+        L.rinfo[t][0] = 4 * (t * kFYDW) - jalY;
+        L.rinfo[t][1] = 4 * (kFRows * kFYDW + (i - ilo) * kFCDW) - jalC;
+        L.rinfo[t][2] = 4 * (kFRows * kFYDW + (f - ilo) * kFCDW) - jalC;
+        L.rinfo[t][3] = 4 * (kFRows * kFYDW + kFRows * kFCDW + (i - ilo) * kFCDW) - jalC;
+        L.rinfo[t][4] = 4 * (kFRows * kFYDW + kFRows * kFCDW + (f - ilo) * kFCDW) - jalC;
+      }
+      __syncthreads();  // DMA landed; previous step's H reads of rgb are done
+      mark(0);
+      // B. h2v2 fancy upsampling + ycc->rgb on 4 pixel pairs (8 pixels) per item: chroma columns
+      // jg - 4 .. jg + 7 and luma x .. x + 7 come in as aligned dwords (jg = jb + 4g)
+      for (int it = t; it < nr * ng; it += kFThreads) {
+        const int q = (it >= ng) + (it >= 2 * ng) + (it >= 3 * ng), gi = it - q * ng;
+        const int jg = jb + 4 * gi, x = 2 * jg;
+        const int oY = L.rinfo[q][0], oBi = L.rinfo[q][1], oBf = L.rinfo[q][2], oRi = L.rinfo[q][3],
+                  oRf = L.rinfo[q][4];
+        // column sums 3 * row_i + row_f for columns jg - 1 .. jg + 4 (edges repeat column 0 / dwc - 1)
+        int cb[6], cr[6];
+        {
+          const uint32_t* sw = L.st;
+          const uint32_t bi0 = sw[(oBi + jg - 4) >> 2], bi1 = sw[(oBi + jg) >> 2], bi2 = sw[(oBi + jg + 4) >> 2];
+          const uint32_t bf0 = sw[(oBf + jg - 4) >> 2], bf1 = sw[(oBf + jg) >> 2], bf2 = sw[(oBf + jg + 4) >> 2];
+          const uint32_t ri0 = sw[(oRi + jg - 4) >> 2], ri1 = sw[(oRi + jg) >> 2], ri2 = sw[(oRi + jg + 4) >> 2];
+          const uint32_t rf0 = sw[(oRf + jg - 4) >> 2], rf1 = sw[(oRf + jg) >> 2], rf2 = sw[(oRf + jg + 4) >> 2];
+          cb[0] = (int)(bi0 >> 24) * 3 + (int)(bf0 >> 24);
+          cr[0] = (int)(ri0 >> 24) * 3 + (int)(rf0 >> 24);
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            cb[1 + k] = (int)((bi1 >> (8 * k)) & 0xFF) * 3 + (int)((bf1 >> (8 * k)) & 0xFF);
+            cr[1 + k] = (int)((ri1 >> (8 * k)) & 0xFF) * 3 + (int)((rf1 >> (8 * k)) & 0xFF);
+          }
+          cb[5] = (int)(bi2 & 0xFF) * 3 + (int)(bf2 & 0xFF);
+          cr[5] = (int)(ri2 & 0xFF) * 3 + (int)(rf2 & 0xFF);
+          if (jg == 0) {
+            cb[0] = cb[1];
+            cr[0] = cr[1];
+          }
+#pragma unroll
+          for (int k = 0; k < 4; k++)  // right edge: column j + 1 past dwc - 1 repeats column j
+            if (jg + k + 1 > dwc - 1) {
+              cb[2 + k] = cb[1 + k];
+              cr[2 + k] = cr[1 + k];
+            }
+        }
+        const uint32_t y0 = L.st[(oY + x) >> 2], y1 = L.st[(oY + x + 4) >> 2];
+        uint32_t wr[2] = {0, 0}, wg[2] = {0, 0}, wb[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int c0 = cb[1 + k], d0 = cr[1 + k];
+          const uint32_t yw = k < 2 ? y0 : y1;
+          const int ye = (int)((yw >> (16 * (k & 1))) & 0xFF), yo = (int)((yw >> (16 * (k & 1) + 8)) & 0xFF);
+          int r0, g0, b0, r1, g1, b1;
+          ycc_px(ye, ((c0 * 3 + cb[k] + 8) >> 4) - 128, ((d0 * 3 + cr[k] + 8) >> 4) - 128, r0, g0, b0);
+          ycc_px(yo, ((c0 * 3 + cb[2 + k] + 7) >> 4) - 128, ((d0 * 3 + cr[2 + k] + 7) >> 4) - 128, r1, g1, b1);
+          const int sh = 16 * (k & 1);
+          wr[k >> 1] |= (uint32_t)(r0 | (r1 << 8)) << sh;
+          wg[k >> 1] |= (uint32_t)(g0 | (g1 << 8)) << sh;
+          wb[k >> 1] |= (uint32_t)(b0 | (b1 << 8)) << sh;
+        }
+        uint32_t* o = reinterpret_cast<uint32_t*>(&L.rgb[q][0][x - xb]);
+        o[0] = wr[0];
+        o[1] = wr[1];
+        o[kFRgbW / 4] = wg[0];
+        o[kFRgbW / 4 + 1] = wg[1];
+        o[kFRgbW / 2] = wb[0];
+        o[kFRgbW / 2 + 1] = wb[1];
+      }
+      __syncthreads();
+      mark(1);
+      if (active) {
+#pragma unroll
+        for (int q = 0; q < kFRows; q++) {
+          if (q >= nr) break;
+          // H. KT taps of step row q -> ring slot
+          int32_t s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
+          const uint8_t* pr = hp + q * 3 * kFRgbW;
+#pragma unroll
+          for (int j = 0; j < KT; j++) {
+            s0 += tap(pr[j], cf[j]);
+            s1 += tap(pr[kFRgbW + j], cf[j]);
+            s2 += tap(pr[2 * kFRgbW + j], cf[j]);
+          }
+          const int r = ra + q;
+          ring[(r & rmask) * rstride] =
+              (uint32_t)rs_clip8(s0) | ((uint32_t)rs_clip8(s1) << 8) | ((uint32_t)rs_clip8(s2) << 16);
+          // V. output rows whose window ends at row r
+          while (nb < oy1) {
+            const int vmin = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][0]);
+            const int vcnt = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][1]);
+            if (vmin + vcnt > r + 1) break;
+            int32_t v0 = 1 << 21, v1 = 1 << 21, v2 = 1 << 21;
+            const int32_t* wk = L.vw[nb - oy0];
+            for (int k = 0; k < vcnt; k++) {
+              const uint32_t h = ring[((vmin + k) & rmask) * rstride];
+              const int32_t w = wk[k];
+              v0 += tap((int32_t)(h & 0xFF), w);
+              v1 += tap((int32_t)((h >> 8) & 0xFF), w);
+              v2 += tap((int32_t)(h >> 16), w);
+            }
+            put3(out, om, lut, (int64_t)nb * ow + ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
+            nb++;
+          }
+        }
+      }
+      mark(2);
+    }
+    if (SDSJ_RS_TIMING && lane == 0)
+      for (int k = 0; k < 3; k++)
+        atomicAdd((unsigned long long*)&const_cast<ImgDesc*>(d)->t_rs[k], (unsigned long long)tk[k]);
+    __syncthreads();  // LDS reuse by the next tile
+  }
+}
+
+hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
+                              const uint8_t* flip, void* out, const float* lut, hipStream_t s) {
+  const int tiles = (op.out_w + kFThreads - 1) / kFThreads;
+  const int strips = (op.out_h + strip_h - 1) / strip_h;
+  const dim3 grid(n, strips, tiles);
+  hipLaunchKernelGGL(k_rs420<3>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
+  hipLaunchKernelGGL(k_rs420<5>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
+  hipLaunchKernelGGL(k_rs420<7>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
+  hipLaunchKernelGGL(k_rs420<9>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
+  hipLaunchKernelGGL(k_rs420<11>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
+  return hipGetLastError();
+}
+
+}  // namespace sdsj
