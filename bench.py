@@ -30,6 +30,31 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+PMC_JSON = os.path.join(REPO, "profiles", "pmc_latest.json")  # tools/pmc.sh + tools/pmc_summary.py output
+# engine stage -> kernels launched in it (rocprofv3 kernel names contain these)
+STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_unstuff"], "entsync": ["k_entsync"],
+                 "entwrite": ["k_entwrite"], "idct": ["k_idct"], "color": ["k_color"], "coeffs": ["k_coeffs"],
+                 "hpass": ["k_hpass"], "vpass": ["k_vpass"], "resample": ["k_resample", "k_rs420"]}
+
+
+def pmc_traffic(stage: str, batch: int):
+    """HBM bytes per launch of `stage` from the committed PMC summary (FETCH_SIZE + WRITE_SIZE, KB as
+    rocprofv3 reports them, summed over the stage's kernels), if it was collected at this batch size."""
+    try:
+        with open(PMC_JSON) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if pmc.get("batch") != batch:
+        return None
+    tot, hit = 0.0, False
+    for name, ctr in pmc.get("kernels", {}).items():
+        if any(k in name for k in STAGE_KERNELS.get(stage, [])) and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
+            tot += (ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024.0
+            hit = True
+    return {"bytes_per_launch": round(tot), "source": os.path.relpath(PMC_JSON, REPO),
+            "note": "FETCH_SIZE + WRITE_SIZE as reported (MI355X_MICROARCH.md: FETCH_SIZE counts 1/2 of 16-B/lane "
+                    "streaming reads; these kernels read <= 4 B/lane, uncalibrated)"} if hit else None
 
 
 def _make_pool_image(i: int) -> bytes:
@@ -206,6 +231,7 @@ def main():
     dom_ms = stages[dom] / args.steps  # mean duration of the dominant kernel per launch (1 launch / step)
     achieved = B * alg_bytes_per_img / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     pipeline_ms = sum(stages.values()) / args.steps
+    traffic = pmc_traffic(dom, B)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -232,7 +258,10 @@ def main():
                        "rows_per_gpu": nrows, "distinct_images": args.pool, "global_batch": B * world,
                        "mean_jpeg_bytes": round(mean_in, 1), "parallelism": f"index-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": (traffic or {}).get("bytes_per_launch"),
+                         "traffic_detail": traffic,
+                         "algorithmic_bytes_per_launch": round(B * alg_bytes_per_img),
                          "algorithmic_bytes_per_image": round(alg_bytes_per_img, 1),
                          "pipeline_achieved": round(B * alg_bytes_per_img / (pipeline_ms * 1e-3) / 1e9, 2)
                          if pipeline_ms > 0 else None},

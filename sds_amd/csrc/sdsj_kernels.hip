@@ -486,37 +486,48 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
   __shared__ int ws[kIdctBlocks * kWsStride];
-  __shared__ uint16_t qt[kMaxComp][64];
+  __shared__ int32_t qt[kMaxComp][64];
+  // per MCU block b: component, byte offset of its top-left pixel inside an MCU's footprint, and
+  // the per-MCU steps (x: h * 8 bytes, y: v * 8 rows of pitch) of its component (jdcoefct order)
+  __shared__ int32_t bcomp[kMaxBlocksPerMcu], boff[kMaxBlocksPerMcu];
+  __shared__ int32_t cstep_x[kMaxComp], cstep_y[kMaxComp], cpitch[kMaxComp];
+  __shared__ int64_t cplane[kMaxComp];
   const int t = threadIdx.x;
-  for (int i = t; i < d->ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][i % 64];
+  const int ncomp = d->ncomp, bpm = d->bpm, mcux = d->mcux;
+  for (int i = t; i < ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][i % 64];
+  if (t < kMaxComp && t < ncomp) {
+    const CompDesc& cd = d->comp[t];
+    const int h = ncomp == 1 ? 1 : cd.h, v = ncomp == 1 ? 1 : cd.v;
+    cstep_x[t] = h * 8;
+    cstep_y[t] = v * 8 * cd.pitch;
+    cpitch[t] = cd.pitch;
+    cplane[t] = cd.plane_off;
+  }
+  if (t < bpm) {
+    const int c = d->blk_comp[t];
+    bcomp[t] = c;
+    boff[t] = ncomp == 1 ? 0 : d->blk_dy[t] * 8 * d->comp[c].pitch + d->blk_dx[t] * 8;
+  }
   __syncthreads();
   const int lb = t >> 3, r = t & 7;
   const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
   uint8_t* planes = scratch + d->off_planes;
-  const int64_t nblocks = d->total_blocks;
-  const int bpm = d->bpm, mcux = d->mcux;
-  for (int64_t g0 = (int64_t)blockIdx.x * kIdctBlocks; g0 < nblocks; g0 += (int64_t)gridDim.x * kIdctBlocks) {
-    const int64_t g = g0 + lb;
+  const int nblocks = (int)d->total_blocks;  // < 2^24 (setup_geometry)
+  for (int g0 = blockIdx.x * kIdctBlocks; g0 < nblocks; g0 += gridDim.x * kIdctBlocks) {
+    const int g = g0 + lb;
     const bool valid = g < nblocks;
-    int c = 0, bx = 0, by = 0;
+    int c = 0;
+    int64_t dst_off = 0;
     if (valid) {
-      int64_t m = g / bpm;
-      int b = (int)(g - m * bpm);
-      c = d->blk_comp[b];
-      int mx = (int)(m % mcux), my = (int)(m / mcux);
-      if (d->ncomp == 1) {
-        bx = mx;
-        by = my;
-      } else {
-        bx = mx * d->comp[c].h + d->blk_dx[b];
-        by = my * d->comp[c].v + d->blk_dy[b];
-      }
+      const int m = g / bpm, b = g - m * bpm;
+      const int my = m / mcux, mx = m - my * mcux;
+      c = bcomp[b];
+      dst_off = cplane[c] + boff[b] + (int64_t)my * cstep_y[c] + mx * cstep_x[c] + r * cpitch[c];
       // row r of the block, dequantised (DEQUANTIZE: coef * quantval)
-      const int16_t* cp = coef + g * 64 + r * 8;
-      uint4 raw = *reinterpret_cast<const uint4*>(cp);
+      const uint4 raw = *reinterpret_cast<const uint4*>(coef + (int64_t)g * 64 + r * 8);
       int16_t v[8];
       *reinterpret_cast<uint4*>(v) = raw;
-      for (int k = 0; k < 8; k++) ws[lb * kWsStride + r * 8 + k] = (int)v[k] * (int)qt[c][r * 8 + k];
+      for (int k = 0; k < 8; k++) ws[lb * kWsStride + r * 8 + k] = (int)v[k] * qt[c][r * 8 + k];
     }
     __syncthreads();
     // pass 1: column r
@@ -544,9 +555,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
       uint32_t lo = 0, hi = 0;
       for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
       for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
-      const CompDesc& cd = d->comp[c];
-      uint8_t* dst = planes + cd.plane_off + (int64_t)(by * 8 + r) * cd.pitch + bx * 8;
-      *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+      *reinterpret_cast<uint2*>(planes + dst_off) = make_uint2(lo, hi);
     }
     __syncthreads();
   }

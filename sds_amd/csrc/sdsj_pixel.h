@@ -29,6 +29,15 @@ __device__ __forceinline__ void ycc_px(int y, int cb, int cr, int& r, int& g, in
 // 22-bit fixed point) -- exact in a 24-bit multiply (v_mad_i32_i24, full rate)
 __device__ __forceinline__ int32_t tap(int32_t px, int32_t k) { return __mul24(px, k); }
 
+// Packs three uint8 results as R | G << 8 | B << 16.  The values go through an empty asm first:
+// otherwise hipcc (ROCm 7.2, gfx950) fuses "clip8(a) | clip8(b) << 8" into v_ashr_pk_u8_i32 and
+// then ORs the third byte in as if that instruction zeroed bits 16-31 -- on the hardware they keep
+// the register's old contents (measured: channel 2 of k_rs420 corrupted; tools/case_diff.py).
+__device__ __forceinline__ uint32_t pack3(int a, int b, int c) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c));
+  return (uint32_t)a | ((uint32_t)b << 8) | ((uint32_t)c << 16);
+}
+
 enum { kLayGeneric = 0, kLay420 = 1, kLayFull = 2 };
 
 // Output addressing: element (channel c, pixel p) at base + p * ps + c * cs (elements).

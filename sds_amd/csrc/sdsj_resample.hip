@@ -311,7 +311,7 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
         }
         const int r = ra + q;
         ring[(r & A.rmask) * A.rstride] =
-            (uint32_t)rs_clip8(s0) | ((uint32_t)rs_clip8(s1) << 8) | ((uint32_t)rs_clip8(s2) << 16);
+            pack3(rs_clip8(s0), rs_clip8(s1), rs_clip8(s2));
         // V. output rows whose window [vmin, vmin + vcnt) ends at row r (ring_rows >= ksv keeps
         // the whole window; own column only, so no barrier)
         for (;;) {

@@ -19,6 +19,9 @@
 #ifndef SDSJ_RS_TIMING
 #define SDSJ_RS_TIMING 0
 #endif
+#ifndef SDSJ_RS_EXP
+#define SDSJ_RS_EXP 0  // experiments (tools/rs_timing.py): 1 = no output stores, 2 = no vertical gather
+#endif
 
 namespace sdsj {
 
@@ -37,6 +40,24 @@ struct LdsF {
   int32_t vw[kMaxStrip][kVTaps];          // strip rows: vertical weights
   int32_t rinfo[kFRows][8];               // step row q: byte offsets of its Y, Cb i/f, Cr i/f rows
 };
+
+// Pillow horizontal pass of one channel at one output column: KT taps from the byte window that
+// starts hsh bytes into dword w[0] (accumulator from 1 << 21, clip8 after >> 22).
+template <int KT>
+__device__ __forceinline__ int htaps(const uint32_t* w, int hsh, const int32_t* cf) {
+  constexpr int ND = (KT + 3 + 3) / 4 + 1;  // dwords covering hsh + KT bytes, + 1 for the realign
+  uint32_t d[ND];
+#pragma unroll
+  for (int i = 0; i < ND; i++) d[i] = w[i];
+  int32_t acc = 1 << 21;
+#pragma unroll
+  for (int g = 0; g * 4 < KT; g++) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(d[g + 1], d[g], hsh);  // bytes hsh + 4g ..
+#pragma unroll
+    for (int k = 0; k < 4 && g * 4 + k < KT; k++) acc += tap((int32_t)((v >> (8 * k)) & 0xFF), cf[g * 4 + k]);
+  }
+  return rs_clip8(acc);
+}
 
 template <int KT>
 __global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
@@ -105,7 +126,8 @@ __global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __res
     int32_t cf[KT];
 #pragma unroll
     for (int j = 0; j < KT; j++) cf[j] = active && j < hc ? kh[(int64_t)xx * KT + j] : 0;
-    const uint8_t* hp = &L.rgb[0][0][0] + hm;
+    const uint32_t* hw = reinterpret_cast<const uint32_t*>(&L.rgb[0][0][0]) + (hm >> 2);
+    const int hsh = hm & 3;
     uint32_t* ring = L.ring + t;
     const int ox = fl ? ow - 1 - xx : xx;
     int nb = oy0;
@@ -223,20 +245,15 @@ __global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __res
 #pragma unroll
         for (int q = 0; q < kFRows; q++) {
           if (q >= nr) break;
-          // H. KT taps of step row q -> ring slot
-          int32_t s0 = 1 << 21, s1 = 1 << 21, s2 = 1 << 21;
-          const uint8_t* pr = hp + q * 3 * kFRgbW;
-#pragma unroll
-          for (int j = 0; j < KT; j++) {
-            s0 += tap(pr[j], cf[j]);
-            s1 += tap(pr[kFRgbW + j], cf[j]);
-            s2 += tap(pr[2 * kFRgbW + j], cf[j]);
-          }
+          // H. KT taps of step row q -> ring slot.  Each channel's window comes in as aligned dwords
+          // (unaligned sub-dword LDS reads are slow) and is realigned with v_alignbyte.
+          const int s0 = htaps<KT>(hw + q * 3 * (kFRgbW / 4), hsh, cf);
+          const int s1 = htaps<KT>(hw + (q * 3 + 1) * (kFRgbW / 4), hsh, cf);
+          const int s2 = htaps<KT>(hw + (q * 3 + 2) * (kFRgbW / 4), hsh, cf);
           const int r = ra + q;
-          ring[(r & rmask) * rstride] =
-              (uint32_t)rs_clip8(s0) | ((uint32_t)rs_clip8(s1) << 8) | ((uint32_t)rs_clip8(s2) << 16);
+          ring[(r & rmask) * rstride] = pack3(s0, s1, s2);
           // V. output rows whose window ends at row r
-          while (nb < oy1) {
+          while (!(SDSJ_RS_EXP & 2) && nb < oy1) {
             const int vmin = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][0]);
             const int vcnt = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][1]);
             if (vmin + vcnt > r + 1) break;
@@ -249,7 +266,10 @@ __global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __res
               v1 += tap((int32_t)((h >> 8) & 0xFF), w);
               v2 += tap((int32_t)(h >> 16), w);
             }
-            put3(out, om, lut, (int64_t)nb * ow + ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
+            if (SDSJ_RS_EXP & 1)
+              asm volatile("" ::"v"(v0), "v"(v1), "v"(v2));
+            else
+              put3(out, om, lut, (int64_t)nb * ow + ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
             nb++;
           }
         }

@@ -18,4 +18,6 @@ for path in glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv
     for (k, _, c), v in per.items():
         acc[k][c].append(v)
 out = {k: {c: sum(v) / len(v) for c, v in sorted(cs.items())} for k, cs in sorted(acc.items())}
-json.dump({"note": "rocprofv3 --pmc, mean per dispatch", "kernels": out}, sys.stdout, indent=1)
+batch = int(sys.argv[2]) if len(sys.argv) > 2 else None
+json.dump({"note": "rocprofv3 --pmc, mean per dispatch (bench.py --steps 2 --warmup 1)", "batch": batch,
+           "kernels": out}, sys.stdout, indent=1)

@@ -20,13 +20,16 @@ def main():
     pool = make_pool(256, 16)
     jpgs = [pool[i % 256] for i in range(n)]
     eng = JpegEngine("cuda:0", max_batch=n, scratch_bytes=int(n * 3.2e6) + (256 << 20))
-    for _ in range(2):
-        out, st = eng.decode_resize(jpgs, (256, 256))
+    out, st = eng.decode_resize(jpgs, (256, 256))
+    eng.set_timing(True)
+    out, st = eng.decode_resize(jpgs, (256, 256))
     torch.cuda.synchronize()
+    rs_ms = eng.stage_times().get("resample")
+    eng.set_timing(False)
     descs, _ = snapshot(eng, n)
     waves = n * 4 * 4  # strips x waves per workgroup (256x256 output, 64-row strips)
     tot = [sum(d.t_rs[k] for d in descs) for k in range(3)]
-    print({"images": n, "ticks_per_wg_wave": [round(t / waves) for t in tot],
+    print({"images": n, "resample_ms": rs_ms, "ticks_per_wg_wave": [round(t / waves) for t in tot],
            "names": ["stage+barrier", "convert+barrier", "H+V"]})
 
 
