@@ -38,7 +38,7 @@ constexpr int kEntThreads = kDecodeThreads;
 constexpr int kLutEntries = 1 << 13;  // LDS lookup capacity: 4 tables x 2^11 or 8 x 2^10
 constexpr int kStageStride = 64;      // int16 per lane staging block (one 128-byte block)
 constexpr int kBudget0 = 64;          // first sync stage's symbol budget
-constexpr int kMaxTasks = 1024;
+constexpr int kMaxTasks = kEntThreads;  // per round (more: picked up by the next round)
 constexpr int kMaxSlots = 2 * kMaxComp;  // a DC and an AC table per component at most
 
 // ------------------------------------------------------------------------------------------
@@ -271,9 +271,14 @@ __device__ inline int block_excl_scan(int v, int* tmp, int* total) {
 // ------------------------------------------------------------------------------------------
 struct LdsSync {
   EntTables T;
-  int32_t scan[5][kEntThreads];
-  int32_t flag[kEntThreads];
-  int32_t task[2][kMaxTasks];
+  int32_t tmp[kEntThreads];  // block_excl_scan scratch
+  union {                    // sync rounds | final segmented scan (never live together)
+    int32_t task[2][kMaxTasks];
+    struct {
+      int32_t scan[4][kEntThreads];
+      int32_t flag[kEntThreads];
+    } fs;
+  } u;
   int32_t nsub, rounds, stages;
   unsigned long long sym[2];
   unsigned long long t0, t1, t2;
@@ -449,7 +454,7 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
 }
 
 template <int LB>
-__global__ void __launch_bounds__(kEntThreads) k_entsync(int n, ImgDesc* __restrict__ descs,
+__global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(5))) k_entsync(int n, ImgDesc* __restrict__ descs,
                                                          const ImgTables* __restrict__ tables,
                                                          uint8_t* __restrict__ scratch) {
   const int img = blockIdx.x;
@@ -488,7 +493,7 @@ __global__ void __launch_bounds__(kEntThreads) k_entsync(int n, ImgDesc* __restr
         cnt = b1 > b0 ? (int)((b1 - b0 + SB - 1) / SB) : 1;
       }
       int total;
-      const int off = carry + block_excl_scan(cnt, L.scan[0], &total);
+      const int off = carry + block_excl_scan(cnt, L.tmp, &total);
       if (s < nseg) {
         for (int k = 0; k < cnt; k++) {
           const int j = off + k;
@@ -539,9 +544,9 @@ __global__ void __launch_bounds__(kEntThreads) k_entsync(int n, ImgDesc* __restr
         need = ep != sub[j].entry_p || ebz != sub[j].entry_bz;
       }
       int tot;
-      const int off = block_excl_scan(need ? 1 : 0, L.scan[0], &tot);
+      const int off = block_excl_scan(need ? 1 : 0, L.tmp, &tot);
       if (need && ntask + off < kMaxTasks) {
-        L.task[0][ntask + off] = j;
+        L.u.task[0][ntask + off] = j;
         SubState& S = sub[j];
         S.new_entry_p = ep;
         S.new_entry_bz = ebz;
@@ -566,7 +571,7 @@ __global__ void __launch_bounds__(kEntThreads) k_entsync(int n, ImgDesc* __restr
       bool pending = false;
       int my_task = -1;
       if (t < nt) {
-        my_task = L.task[cur][t];
+        my_task = L.u.task[cur][t];
         int k = 0;
         pending = !sync_step<LB>(L.T, K, src, sub[my_task], recs + (int64_t)my_task * kRec, budget, &k);
         nsym_sync += k;
@@ -574,13 +579,13 @@ __global__ void __launch_bounds__(kEntThreads) k_entsync(int n, ImgDesc* __restr
       }
       for (int i = t + kEntThreads; i < nt; i += kEntThreads) {  // beyond one task per thread: no budget
         int k = 0;
-        const int j = L.task[cur][i];
+        const int j = L.u.task[cur][i];
         sync_step<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, 1 << 30, &k);
         nsym_sync += k;
       }
       int tot;
-      const int off = block_excl_scan(pending ? 1 : 0, L.scan[0], &tot);
-      if (pending) L.task[cur ^ 1][off] = my_task;
+      const int off = block_excl_scan(pending ? 1 : 0, L.tmp, &tot);
+      if (pending) L.u.task[cur ^ 1][off] = my_task;
       if (t == 0) {
         L.stages++;
         for (int w = 0; w < kEntThreads / 64; w++) L.it[1] += 64ull * L.wmax[w];
@@ -592,13 +597,13 @@ __global__ void __launch_bounds__(kEntThreads) k_entsync(int n, ImgDesc* __restr
     }
     // commit every task of the round (entries first: they were read from cur_exit of j-1)
     for (int i = t; i < ntask; i += kEntThreads) {
-      SubState& S = sub[L.task[0][i]];
+      SubState& S = sub[L.u.task[0][i]];
       S.entry_p = S.new_entry_p;
       S.entry_bz = S.new_entry_bz;
     }
     __syncthreads();
     for (int i = t; i < ntask; i += kEntThreads) {
-      SubState& S = sub[L.task[0][i]];
+      SubState& S = sub[L.u.task[0][i]];
       S.cur_exit_p = S.new_exit_p;
       S.cur_exit_bz = S.new_exit_bz;
       S.cur_nblk = S.new_nblk;
@@ -625,35 +630,35 @@ __global__ void __launch_bounds__(kEntThreads) k_entsync(int n, ImgDesc* __restr
         v[3] = S.cur_dc[2];
         f = S.first;
       }
-      for (int q = 0; q < 4; q++) L.scan[q][t] = v[q];
-      L.flag[t] = f;
+      for (int q = 0; q < 4; q++) L.u.fs.scan[q][t] = v[q];
+      L.u.fs.flag[t] = f;
       __syncthreads();
       for (int off = 1; off < kEntThreads; off <<= 1) {
         int a[4] = {0, 0, 0, 0}, af = 0;
         const bool take = t >= off;
         if (take) {
-          for (int q = 0; q < 4; q++) a[q] = L.scan[q][t - off];
-          af = L.flag[t - off];
+          for (int q = 0; q < 4; q++) a[q] = L.u.fs.scan[q][t - off];
+          af = L.u.fs.flag[t - off];
         }
         __syncthreads();
-        if (take && !L.flag[t])
-          for (int q = 0; q < 4; q++) L.scan[q][t] += a[q];
-        if (take) L.flag[t] |= af;
+        if (take && !L.u.fs.flag[t])
+          for (int q = 0; q < 4; q++) L.u.fs.scan[q][t] += a[q];
+        if (take) L.u.fs.flag[t] |= af;
         __syncthreads();
       }
       if (j < nsub) {
         SubState& S = sub[j];
-        const int hit = L.flag[t];
+        const int hit = L.u.fs.flag[t];
         int ex[4];
-        for (int q = 0; q < 4; q++) ex[q] = S.first ? 0 : L.scan[q][t] - v[q] + (hit ? 0 : carry[q]);
+        for (int q = 0; q < 4; q++) ex[q] = S.first ? 0 : L.u.fs.scan[q][t] - v[q] + (hit ? 0 : carry[q]);
         S.nblk_ex = ex[0];
         S.dc_ex[0] = ex[1];
         S.dc_ex[1] = ex[2];
         S.dc_ex[2] = ex[3];
       }
       __syncthreads();
-      const int any = L.flag[kEntThreads - 1];
-      for (int q = 0; q < 4; q++) carry[q] = L.scan[q][kEntThreads - 1] + (any ? 0 : carry[q]);
+      const int any = L.u.fs.flag[kEntThreads - 1];
+      for (int q = 0; q < 4; q++) carry[q] = L.u.fs.scan[q][kEntThreads - 1] + (any ? 0 : carry[q]);
       __syncthreads();
     }
   }

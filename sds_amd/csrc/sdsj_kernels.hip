@@ -478,6 +478,15 @@ __device__ __forceinline__ uint32_t range_limit(int x) {
   return (uint32_t)(s < 0 ? 0 : s > 255 ? 255 : s);
 }
 
+// Work unit = one wave: 8 horizontally adjacent blocks of one component (a "group"), so each of
+// the 8 row stores of the wave writes 64 contiguous bytes of a plane row.  8 threads per block
+// (thread r: row r, then column r); the 8 threads of a block share a wave, so the LDS transposes
+// need only in-wave ordering, no workgroup barrier.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __restrict__ descs,
                                                        const ImgTables* __restrict__ tables,
                                                        uint8_t* __restrict__ scratch) {
@@ -487,54 +496,63 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
   __shared__ int ws[kIdctBlocks * kWsStride];
   __shared__ int32_t qt[kMaxComp][64];
-  // per MCU block b: component, byte offset of its top-left pixel inside an MCU's footprint, and
-  // the per-MCU steps (x: h * 8 bytes, y: v * 8 rows of pitch) of its component (jdcoefct order)
-  __shared__ int32_t bcomp[kMaxBlocksPerMcu], boff[kMaxBlocksPerMcu];
-  __shared__ int32_t cstep_x[kMaxComp], cstep_y[kMaxComp], cpitch[kMaxComp];
+  __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
+  __shared__ int32_t gstart[kMaxComp + 1], ngx[kMaxComp], cbw[kMaxComp], ch_[kMaxComp], cv_[kMaxComp], cpitch[kMaxComp];
   __shared__ int64_t cplane[kMaxComp];
   const int t = threadIdx.x;
   const int ncomp = d->ncomp, bpm = d->bpm, mcux = d->mcux;
   for (int i = t; i < ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][i % 64];
-  if (t < kMaxComp && t < ncomp) {
-    const CompDesc& cd = d->comp[t];
-    const int h = ncomp == 1 ? 1 : cd.h, v = ncomp == 1 ? 1 : cd.v;
-    cstep_x[t] = h * 8;
-    cstep_y[t] = v * 8 * cd.pitch;
-    cpitch[t] = cd.pitch;
-    cplane[t] = cd.plane_off;
-  }
-  if (t < bpm) {
-    const int c = d->blk_comp[t];
-    bcomp[t] = c;
-    boff[t] = ncomp == 1 ? 0 : d->blk_dy[t] * 8 * d->comp[c].pitch + d->blk_dx[t] * 8;
+  if (t < bpm) binv[d->blk_comp[t]][d->blk_dy[t] * 4 + d->blk_dx[t]] = t;
+  if (t == 0) {
+    int acc = 0;
+    for (int c = 0; c < ncomp; c++) {
+      const CompDesc& cd = d->comp[c];
+      gstart[c] = acc;
+      ngx[c] = (cd.bw + 7) >> 3;
+      cbw[c] = cd.bw;
+      ch_[c] = ncomp == 1 ? 1 : cd.h;
+      cv_[c] = ncomp == 1 ? 1 : cd.v;
+      cpitch[c] = cd.pitch;
+      cplane[c] = cd.plane_off;
+      acc += ngx[c] * cd.bh;
+    }
+    gstart[ncomp] = acc;
   }
   __syncthreads();
-  const int lb = t >> 3, r = t & 7;
+  const int lane = t & 63, wv = t >> 6, lb = lane >> 3, r = lane & 7;
+  int* W = ws + (wv * 8 + lb) * kWsStride;
   const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
   uint8_t* planes = scratch + d->off_planes;
-  const int nblocks = (int)d->total_blocks;  // < 2^24 (setup_geometry)
-  for (int g0 = blockIdx.x * kIdctBlocks; g0 < nblocks; g0 += gridDim.x * kIdctBlocks) {
-    const int g = g0 + lb;
-    const bool valid = g < nblocks;
-    int c = 0;
-    int64_t dst_off = 0;
-    if (valid) {
-      const int m = g / bpm, b = g - m * bpm;
-      const int my = m / mcux, mx = m - my * mcux;
-      c = bcomp[b];
-      dst_off = cplane[c] + boff[b] + (int64_t)my * cstep_y[c] + mx * cstep_x[c] + r * cpitch[c];
-      // row r of the block, dequantised (DEQUANTIZE: coef * quantval)
-      const uint4 raw = *reinterpret_cast<const uint4*>(coef + (int64_t)g * 64 + r * 8);
-      int16_t v[8];
-      *reinterpret_cast<uint4*>(v) = raw;
-      for (int k = 0; k < 8; k++) ws[lb * kWsStride + r * 8 + k] = (int)v[k] * qt[c][r * 8 + k];
+  const int ngroups = gstart[ncomp];
+  // block of this lane in group grp: component, block coordinates, decode-order index
+  auto locate = [&](int grp, int& c, int& by, int& bx, int& g) {
+    c = ncomp > 1 && grp >= gstart[1] ? (ncomp > 2 && grp >= gstart[2] ? 2 : 1) : 0;
+    const int local = grp - gstart[c];
+    by = local / ngx[c];
+    bx = (local - by * ngx[c]) * 8 + lb;
+    g = -1;
+    if (grp < ngroups && bx < cbw[c]) {
+      const int h = ch_[c], v = cv_[c];
+      const int mx = bx / h, my = by / v;
+      g = (my * mcux + mx) * bpm + binv[c][(by - my * v) * 4 + (bx - mx * h)];
     }
-    __syncthreads();
+  };
+  const int gstride = gridDim.x * 4;
+  // transform + store the block of this lane (g < 0: none) from its coefficient row `raw`
+  auto process = [&](const uint4& raw, int c, int by, int bx, int g) {
+    const bool valid = g >= 0;
+    if (valid) {
+      // row r of the block, dequantised (DEQUANTIZE: coef * quantval)
+      int16_t vv[8];
+      *reinterpret_cast<uint4*>(vv) = raw;
+      for (int k = 0; k < 8; k++) W[r * 8 + k] = (int)vv[k] * qt[c][r * 8 + k];
+    }
+    wave_lds_sync();
     // pass 1: column r
     int col[8];
     if (valid) {
       int x[8];
-      for (int k = 0; k < 8; k++) x[k] = ws[lb * kWsStride + k * 8 + r];
+      for (int k = 0; k < 8; k++) x[k] = W[k * 8 + r];
       if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
         for (int k = 0; k < 8; k++) col[k] = x[0] * 4;  // << PASS1_BITS
       } else {
@@ -543,21 +561,36 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
         for (int k = 0; k < 8; k++) col[k] = (o[k] + (1 << 10)) >> 11;  // DESCALE(, CONST_BITS-PASS1_BITS)
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     if (valid)
-      for (int k = 0; k < 8; k++) ws[lb * kWsStride + k * 8 + r] = col[k];
-    __syncthreads();
-    // pass 2: row r
+      for (int k = 0; k < 8; k++) W[k * 8 + r] = col[k];
+    wave_lds_sync();
+    // pass 2: row r -> 8 bytes of plane row by * 8 + r
     if (valid) {
-      const int* w = &ws[lb * kWsStride + r * 8];
+      const int* w = W + r * 8;
       int o[8];
       islow_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
       uint32_t lo = 0, hi = 0;
       for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
       for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
-      *reinterpret_cast<uint2*>(planes + dst_off) = make_uint2(lo, hi);
+      *reinterpret_cast<uint2*>(planes + cplane[c] + (int64_t)(by * 8 + r) * cpitch[c] + bx * 8) = make_uint2(lo, hi);
     }
-    __syncthreads();
+    wave_lds_sync();
+  };
+  // two groups in flight per wave (ping-pong registers: a loop-carried copy would force the wait)
+  int c0, by0, bx0, g0, c1, by1, bx1, g1;
+  int grp = blockIdx.x * 4 + wv;
+  locate(grp, c0, by0, bx0, g0);
+  uint4 rawA, rawB;
+  rawA = *reinterpret_cast<const uint4*>(coef + (int64_t)(g0 >= 0 ? g0 : 0) * 64 + r * 8);
+  for (; grp < ngroups; grp += 2 * gstride) {
+    locate(grp + gstride, c1, by1, bx1, g1);
+    rawB = *reinterpret_cast<const uint4*>(coef + (int64_t)(g1 >= 0 ? g1 : 0) * 64 + r * 8);  // unconditional: keeps vmcnt countable
+    process(rawA, c0, by0, bx0, g0);
+    if (grp + gstride >= ngroups) break;
+    locate(grp + 2 * gstride, c0, by0, bx0, g0);
+    rawA = *reinterpret_cast<const uint4*>(coef + (int64_t)(g0 >= 0 ? g0 : 0) * 64 + r * 8);
+    process(rawB, c1, by1, bx1, g1);
   }
 }
 
