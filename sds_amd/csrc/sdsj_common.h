@@ -24,6 +24,7 @@ constexpr int kLutBits = 11;          // Huffman lookup width built by k_parse (
 constexpr int kRec = 64;              // block-boundary records kept per subsequence by k_entsync
 constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
+constexpr int kWarmBits = 4000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
 constexpr int kUPad = 128;            // zero bytes after each unstuffed stream (bit-reader prefetch)
 constexpr int kMaxSpan = 960;         // source columns per fused-resample tile (LDS row width)
 constexpr int kRingDW = 3072;         // fused-resample ring (dwords): ring_rows x (3072 / ring_rows) columns
@@ -115,11 +116,17 @@ struct ImgDesc {
   int32_t rs_fast;  // > 0: tap count of the specialised 4:2:0 kernel (k_rs420<rs_fast>), 0: generic k_resample
   // k_resample phase ticks (s_memtime, summed over the image's workgroups; experiment builds only)
   int64_t t_rs[4];
+  // entropy warm-up: a subsequence's speculative decode starts up to warm_bits before its first bit
+  // (inside its segment) and takes the first block boundary at or after that bit as its entry
+  int32_t warm_bits, pad1;
 };
 
 // Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).
-// State at a symbol boundary = (bit position p, MCU block index blk, zig-zag index z); bz packs
-// (blk << 8) | z.  "spec" = the speculative decode from the subsequence's first bit, "cur" = the
+// Subsequence j owns the blocks whose DC symbol starts in [entry_j, exit_j): entry_j = the first
+// block boundary at or after start_bit, exit_j = the first at or after end_bit.  State at a block
+// boundary = (bit position p, MCU block index blk); bz packs (blk << 8) | z (z = 0 at entry/exit,
+// non-zero only in a suspended sync stage).  "spec" = the speculative decode (warm-up from
+// start_bit - warm_bits, then the subsequence), "cur" = the
 // decode from the current entry estimate; after k_entsync, entry is verified and nblk_ex / dc_ex
 // hold the exclusive (segmented) prefix of blocks and DC differences before the entry.
 struct SubState {

@@ -7,6 +7,7 @@
 // device-resident entry point.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -29,6 +30,7 @@ struct sdsj_engine {
   int max_batch = 4096;
   int64_t capacity = 0;
   bool grow = true;
+  int warm_bits = -1;  // entropy warm-up override (SDSJ_WARM_BITS, experiments); < 0 = plan default
   uint8_t* scratch = nullptr;
   ImgDesc* descs = nullptr;
   ImgTables* tables = nullptr;
@@ -141,7 +143,7 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
     if (evs) (void)hipEventRecord((*evs)[k], s);
   };
   mark(0);
-  SDSJ_HIP(e, launch_parse(n, d_blob, d_offsets, d_lengths, op, e->descs, e->tables, s));
+  SDSJ_HIP(e, launch_parse(n, d_blob, d_offsets, d_lengths, op, e->warm_bits, e->descs, e->tables, s));
   mark(1);
   SDSJ_HIP(e, launch_plan(n, e->descs, e->capacity, e->d_total, s));
   mark(2);
@@ -209,6 +211,7 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   sdsj_engine* e = new (std::nothrow) sdsj_engine();
   if (!e) return SDSJ_ENOMEM;
   e->device = hip_device;
+  if (const char* w = getenv("SDSJ_WARM_BITS")) e->warm_bits = atoi(w);
   if (cfg && cfg->max_batch > 0) e->max_batch = cfg->max_batch;
   DeviceGuard g(hip_device);
   int st = SDSJ_OK;

@@ -286,16 +286,26 @@ struct LdsSync {
   int32_t wmax[kEntThreads / 64];
 };
 
-// Speculative decode of subsequence S from its first bit (state: block 0, DC); records boundaries.
+// Speculative decode of subsequence S.  Warm-up: decode from `warm` bits before start_bit (not
+// before the segment start) assuming (block 0, DC), and take the first block boundary at or after
+// start_bit as the entry; by then the decode has almost always merged with the true path (JPEG's
+// Huffman self-synchronisation; the MCU phase takes ~1k bits to lock on).  Then decode to the first
+// block boundary at or after end_bit, recording every block boundary.  A segment's first
+// subsequence starts exactly at its (known) state.
 template <int LB>
-__device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec) {
+__device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
+                         uint32_t seg_start, uint32_t warm) {
   const uint32_t start = S.start_bit, end = S.end_bit;
+  const uint32_t ws = S.first ? start : (start - seg_start > warm ? start - warm : seg_start);
   Bits b;
-  bits_init(b, src, start);
+  bits_init(b, src, ws);
   int blk = 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
   int d0 = 0, d1 = 0, d2 = 0;
   int c = ctx_c(K, 0), sdc = ctx_dc(K, 0), sac = ctx_ac(K, 0);
-  bool run = b.pos < end;
+  uint32_t entry = start;
+  int entry_blk = 0;
+  bool warmup = b.pos < start;
+  bool run = warmup || b.pos < end;
   while (__builtin_amdgcn_ballot_w64(run)) {
     if (run) bits_fill(b);
     for (;;) {
@@ -307,22 +317,29 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
         decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
         nsym++;
         dcd = isdc ? val : dcd;
-        add_dc(c, isdc ? val : 0, d0, d1, d2);
+        add_dc(c, isdc && !warmup ? val : 0, d0, d1, d2);
         if (next_z(z, s, r)) {
-          if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
-          nrec++;
+          if (!warmup) {
+            if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
+            nrec++;
+            nblk++;
+          }
           blk = blk + 1 == K.bpm ? 0 : blk + 1;
           c = ctx_c(K, blk);
           sdc = ctx_dc(K, blk);
           sac = ctx_ac(K, blk);
-          nblk++;
+          if (warmup && b.pos >= start) {
+            warmup = false;
+            entry = b.pos;
+            entry_blk = blk;
+          }
         }
-        run = b.pos < end;
+        run = warmup || b.pos < end || z != 0;
       }
     }
   }
-  S.entry_p = start;
-  S.entry_bz = 0;
+  S.entry_p = entry;
+  S.entry_bz = (uint16_t)(entry_blk << 8);
   S.spec_exit_p = S.cur_exit_p = b.pos;
   S.spec_exit_bz = S.cur_exit_bz = (uint16_t)((blk << 8) | z);
   S.spec_nblk = S.cur_nblk = nblk;
@@ -367,7 +384,7 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
   int nr = 0, done_blk = 0;
   uint32_t P = 0;
   bool adv = false, merged = false;  // adv: records up to boundary P still to be passed
-  bool run = b.pos < end && budget > 0;
+  bool run = (b.pos < end || z != 0) && budget > 0;
   while (__builtin_amdgcn_ballot_w64(run)) {
     if (run) {
       bits_fill(b);
@@ -416,7 +433,7 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
             adv = false;
           }
         }
-        run = !merged && (adv || (b.pos < end && nsym < budget));
+        run = !merged && (adv || ((b.pos < end || z != 0) && nsym < budget));
       }
     }
   }
@@ -431,7 +448,7 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
     S.new_dc[2] = d2 + S.spec_dc[2] - q2;
     return true;
   }
-  if (b.pos >= end) {
+  if (b.pos >= end && z == 0) {
     S.new_exit_p = b.pos;
     S.new_exit_bz = (uint16_t)((blk << 8) | z);
     S.new_nblk = nblk;
@@ -519,7 +536,8 @@ __global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_e
   if ((t & 63) == 0) L.wmax[t >> 6] = 0;
   __syncthreads();
   for (int j = t; j < nsub; j += kEntThreads) {
-    const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec);
+    const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, (uint32_t)seg[sub[j].seg] * 8u,
+                                (uint32_t)d->warm_bits);
     nsym_spec += k;
     atomicMax(&L.wmax[t >> 6], k);
   }

@@ -6,7 +6,7 @@
 
 namespace sdsj {
 hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, const int32_t* lengths, const sdsj_op& op,
-                        ImgDesc* descs, ImgTables* tables, hipStream_t s);
+                        int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s);
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, hipStream_t s);
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);

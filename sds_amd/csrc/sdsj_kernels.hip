@@ -123,6 +123,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
     d->rs_fast = d->ksh;
   d->sub_bits = (int32_t)align_up((d->entropy_len * 8 + kDecodeThreads - 1) / kDecodeThreads, 32);
   if (d->sub_bits < kMinSubBits) d->sub_bits = kMinSubBits;
+  d->warm_bits = d->sub_bits * 3 / 2 < kWarmBits ? d->sub_bits * 3 / 2 : kWarmBits;
   d->nsub_cap = (int32_t)((d->entropy_len * 8 + d->sub_bits - 1) / d->sub_bits) + d->nseg + 1;
   // scratch layout (relative offsets; k_plan adds the image base)
   int64_t o = 0;
@@ -149,8 +150,8 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
 }
 
 __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
-                                              const int32_t* __restrict__ lengths, sdsj_op op, ImgDesc* __restrict__ descs,
-                                              ImgTables* __restrict__ tables) {
+                                              const int32_t* __restrict__ lengths, sdsj_op op, int warm_bits,
+                                              ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables) {
   const int img = blockIdx.x;
   if (img >= n) return;
   const int lane = threadIdx.x;
@@ -171,6 +172,7 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
     int status = parse_headers(rd, len, &sd, &st);
     if (status == SDSJ_OK) status = setup_geometry(&sd, &st);
     if (status == SDSJ_OK) plan_image(&sd, op);
+    if (warm_bits >= 0) sd.warm_bits = warm_bits;
     sd.status = status;
     for (int k = 0; k < 4; k++) sd.t_rs[k] = 0;
     s_status = status;
@@ -881,8 +883,8 @@ __global__ void __launch_bounds__(256) k_vpass(int n, const ImgDesc* __restrict_
 // Host-side launchers (called by the engine; all asynchronous on `stream`).
 // ------------------------------------------------------------------------------------------
 hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, const int32_t* lengths, const sdsj_op& op,
-                        ImgDesc* descs, ImgTables* tables, hipStream_t s) {
-  hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, offsets, lengths, op, descs, tables);
+                        int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s) {
+  hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, offsets, lengths, op, warm_bits, descs, tables);
   return hipGetLastError();
 }
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, hipStream_t s) {
