@@ -132,7 +132,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
     o += align_up(bytes, 256);
     return r;
   };
-  d->off_ustream = take(d->entropy_len + kUPad);
+  d->off_ustream = take(d->entropy_len + kUPad + 32);  // + the 16-byte granule of the final pad store
   d->ustream_cap = d->entropy_len + kUPad;
   d->off_seg = take((int64_t)(d->nseg + 2) * 4);
   d->off_sub = take((int64_t)d->nsub_cap * sizeof(SubState));
@@ -299,25 +299,22 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
 // ------------------------------------------------------------------------------------------
 // k_unstuff: one 256-thread workgroup per image.  Removes FF00 stuffing and fill bytes, splits at
 // RSTn markers and stops at the first other marker (jdhuff.c jpeg_fill_bit_buffer semantics).
+// Tiles of 8 KiB: each thread classifies 32 consecutive bytes (read as realigned dwords), one
+// packed (emitted, RSTn) scan places them, the tile is assembled in LDS and leaves as aligned
+// 16-byte stores (the unaligned tail rides into the next tile).
 // ------------------------------------------------------------------------------------------
 constexpr int kUnstuffThreads = 256;
-constexpr int kUnstuffBytes = 16;
+constexpr int kUsBytes = 32;
+constexpr int kUsTile = kUnstuffThreads * kUsBytes;
 
-__device__ inline int block_excl_scan_256(int v, int* tmp, int* total) {
-  // Hillis-Steele in LDS; tmp has 256 ints.
-  const int t = threadIdx.x;
-  tmp[t] = v;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    int a = t >= off ? tmp[t - off] : 0;
-    __syncthreads();
-    tmp[t] += a;
-    __syncthreads();
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int a = __shfl_up(v, o, 64);
+    v += lane >= o ? a : 0;
   }
-  int incl = tmp[t];
-  *total = tmp[255];
-  __syncthreads();
-  return incl - v;
+  return v;
 }
 
 __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_t* __restrict__ blob,
@@ -327,81 +324,130 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
   if (img >= n) return;
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
-  __shared__ int scan_tmp[256];
-  __shared__ int s_end;
-  const int t = threadIdx.x;
+  __shared__ alignas(16) uint8_t buf[kUsTile + 32];  // [carried tail][this tile's output]
+  __shared__ int wsum[kUnstuffThreads / 64];
+  __shared__ int s_end, s_cut;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint8_t* e = blob + offsets[img] + d->entropy_off;
   const int64_t L = d->entropy_len;
-  uint8_t* out = scratch + d->off_ustream;
+  const uintptr_t e_end = (uintptr_t)(e + L);  // dwords starting below this lie in mapped pages
+  uint8_t* out = scratch + d->off_ustream;  // 256-byte aligned
   int32_t* seg = reinterpret_cast<int32_t*>(scratch + d->off_seg);
   const int nseg = d->nseg;
-
   if (t == 0) seg[0] = 0;
 
-  int64_t out_pos = 0;
+  int64_t out_pos = 0;  // bytes emitted so far; [out_pos & ~15, out_pos) sit in buf[0, carry)
   int rst_count = 0;
   bool ended = false;
-  for (int64_t base = 0; base < L && !ended; base += kUnstuffThreads * kUnstuffBytes) {
-    if (t == 0) s_end = 0x7fffffff;
-    __syncthreads();
-    const int64_t my0 = base + (int64_t)t * kUnstuffBytes;
-    uint8_t b[kUnstuffBytes];
-    int prev = my0 > 0 && my0 - 1 < L ? e[my0 - 1] : 0;
-    int prev_first = prev;
-    uint32_t kind = 0;  // 2 bits per byte: 0 skip, 1 emit, 2 RST, 3 END
-    for (int k = 0; k < kUnstuffBytes; k++) {
-      int64_t i = my0 + k;
-      int c = i < L ? e[i] : -1;
-      int kd;
-      if (c < 0) kd = 3;
-      else if (prev == 0xFF) {
-        if (c == 0x00) { kd = 1; c = 0xFF; }
-        else if (c == 0xFF) kd = 0;
-        else if (c >= 0xD0 && c <= 0xD7) kd = 2;
-        else kd = 3;
-      } else {
-        kd = c == 0xFF ? 0 : 1;
-      }
-      b[k] = (uint8_t)c;
-      kind |= (uint32_t)kd << (2 * k);
-      prev = i < L ? e[i] : -1;
+  for (int64_t base = 0; base < L && !ended; base += kUsTile) {
+    if (t == 0) {
+      s_end = 0x7fffffff;
+      s_cut = 0x7fffffff;
     }
-    (void)prev_first;
-    // first END inside this tile
-    int my_end = 0x7fffffff;
-    for (int k = 0; k < kUnstuffBytes; k++)
-      if (((kind >> (2 * k)) & 3) == 3) { my_end = t * kUnstuffBytes + k; break; }
-    if (my_end != 0x7fffffff) atomicMin(&s_end, my_end);
+    // bytes [my0 - 4, my0 + 32) as 9 realigned dwords u[0..8] (u[0] holds the 4 preceding bytes;
+    // entropy_off >= 4, so they are header bytes of the same image)
+    const int64_t my0 = base + (int64_t)t * kUsBytes;
+    const uintptr_t a = (uintptr_t)(e + my0);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>((a & ~(uintptr_t)3) - 4);
+    const int sh = (int)(a & 3);
+    uint32_t v[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) v[k] = (uintptr_t)(w + k) < e_end ? w[k] : 0u;
+    uint32_t u[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) u[k] = (uint32_t)((((uint64_t)v[k + 1] << 32) | v[k]) >> (8 * sh));
+    // classify: 0 skip, 1 emit, 2 RSTn, 3 end (other marker or end of input)
+    uint64_t kind = 0;
+    int prev = my0 > 0 ? (int)(u[0] >> 24) : 0;
+    int my_end = kUsBytes;
+#pragma unroll
+    for (int k = 0; k < kUsBytes; k++) {
+      const int c = (int)(u[1 + (k >> 2)] >> (8 * (k & 3))) & 0xFF;
+      int kd;
+      if (my0 + k >= L) kd = 3;
+      else if (prev == 0xFF) kd = c == 0x00 ? 1 : (c == 0xFF ? 0 : ((c >= 0xD0 && c <= 0xD7) ? 2 : 3));
+      else kd = c == 0xFF ? 0 : 1;
+      kind |= (uint64_t)kd << (2 * k);
+      if (kd == 3 && my_end == kUsBytes) my_end = k;
+      prev = c;
+    }
+    __syncthreads();  // s_end initialised; buf tail of the previous tile settled
+    if (my_end < kUsBytes) atomicMin(&s_end, t * kUsBytes + my_end);
     __syncthreads();
     const int tile_end = s_end;
+    int lim = tile_end - t * kUsBytes;
+    lim = lim < 0 ? 0 : (lim > kUsBytes ? kUsBytes : lim);
     int nemit = 0, nrst = 0;
-    for (int k = 0; k < kUnstuffBytes; k++) {
-      if (t * kUnstuffBytes + k >= tile_end) break;
-      int kd = (kind >> (2 * k)) & 3;
-      nemit += kd == 1;
-      nrst += kd == 2;
+#pragma unroll
+    for (int k = 0; k < kUsBytes; k++) {
+      const int kd = (int)(kind >> (2 * k)) & 3;
+      nemit += (k < lim && kd == 1) ? 1 : 0;
+      nrst += (k < lim && kd == 2) ? 1 : 0;
     }
-    int emit_total, rst_total;
-    int emit_off = block_excl_scan_256(nemit, scan_tmp, &emit_total);
-    int rst_off = block_excl_scan_256(nrst, scan_tmp, &rst_total);
-    int64_t pos = out_pos + emit_off;
-    int r = rst_count + rst_off;
-    for (int k = 0; k < kUnstuffBytes; k++) {
-      if (t * kUnstuffBytes + k >= tile_end) break;
-      int kd = (kind >> (2 * k)) & 3;
-      if (kd == 1) out[pos++] = b[k];
-      else if (kd == 2) {
+    const int packed = nemit | (nrst << 16);
+    const int incl = wave_incl_scan(packed);
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int q = 0; q < kUnstuffThreads / 64; q++) {
+      before += q < wv ? wsum[q] : 0;
+      total += wsum[q];
+    }
+    const int excl = before + incl - packed;
+    const int carry = (int)(out_pos & 15);
+    int pos = excl & 0xFFFF;
+    int r = rst_count + (excl >> 16);
+#pragma unroll
+    for (int k = 0; k < kUsBytes; k++) {
+      const int kd = (int)(kind >> (2 * k)) & 3;
+      // an emitted byte is itself, or 0xFF for the stuffed 0x00 of an FF00 pair
+      const uint32_t raw = (u[1 + (k >> 2)] >> (8 * (k & 3))) & 0xFF;
+      if (k < lim && kd == 1) buf[carry + pos++] = (uint8_t)(raw == 0 && (k ? (u[1 + ((k - 1) >> 2)] >> (8 * ((k - 1) & 3))) & 0xFF : (my0 > 0 ? u[0] >> 24 : 0)) == 0xFF ? 0xFF : raw);
+      if (k < lim && kd == 2) {
         r++;
-        if (r < nseg) seg[r] = (int32_t)pos;
+        if (r < nseg) seg[r] = (int32_t)(out_pos + pos);
+        else atomicMin(&s_cut, pos);  // more RSTn than restart intervals: a foreign marker, the scan ends
       }
     }
-    out_pos += emit_total;
-    rst_count += rst_total;
-    if (tile_end != 0x7fffffff) ended = true;
     __syncthreads();
+    const int cut = s_cut;
+    const int temit = cut != 0x7fffffff ? cut : (total & 0xFFFF);
+    // full 16-byte chunks of [out_pos & ~15, out_pos + temit) leave; the tail is carried
+    const int have = carry + temit, full = have >> 4;
+    uint4* dst = reinterpret_cast<uint4*>(out + (out_pos & ~(int64_t)15));
+    const uint4* src = reinterpret_cast<const uint4*>(buf);
+    for (int i = t; i < full; i += kUnstuffThreads) dst[i] = src[i];
+    const int rem = have & 15;
+    uint8_t tail = t < rem ? buf[full * 16 + t] : 0;
+    __syncthreads();
+    if (t < rem) buf[t] = tail;
+    out_pos += temit;
+    rst_count += total >> 16;
+    if (rst_count > nseg - 1) rst_count = nseg - 1;
+    if (tile_end != 0x7fffffff || cut != 0x7fffffff) ended = true;
   }
-  // zero pad after the stream so the bit reader can over-read safely
-  for (int k = t; k < kUPad; k += kUnstuffThreads) out[out_pos + k] = 0;
+  __syncthreads();
+  // the carried tail, then zero padding so the bit reader can over-read safely
+  {
+    const int rem = (int)(out_pos & 15);
+    const int64_t a0 = out_pos & ~(int64_t)15;
+    const int nchunks = (rem + kUPad + 15) >> 4;
+    for (int i = t; i < nchunks; i += kUnstuffThreads) {
+      uint32_t wds[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+          const int o = i * 16 + q * 4 + bb;
+          x |= (uint32_t)(o < rem ? buf[o] : 0) << (8 * bb);
+        }
+        wds[q] = x;
+      }
+      reinterpret_cast<uint4*>(out + a0)[i] = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+    }
+  }
   if (t == 0) {
     seg[nseg] = (int32_t)out_pos;
     d->ulen = out_pos;

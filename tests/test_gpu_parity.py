@@ -159,3 +159,61 @@ def test_4k_vs_oracle(engine):
     got, st = engine.decode_resize([jpg], (512, 512), flip=[True])
     assert st[0] == 0
     np.testing.assert_array_equal(got[0].cpu().numpy(), O.pipeline(jpg, (512, 512), flip=True))
+
+
+def _oracle_result(jpg, res):
+    try:
+        return O.OK, O.pipeline(jpg, res)
+    except O.OracleError as e:
+        return e.status, None
+
+
+def _mutations(seed, n):
+    """Truncations, byte flips and marker-like insertions inside the entropy segment of synthetic JPEGs
+    (the FF00 / fill-byte / RSTn / foreign-marker paths of jdhuff.c jpeg_fill_bit_buffer)."""
+    from tests.golden.synth import encode_jpeg, synth_rgb
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        kw = {"restart_marker_blocks": 2} if i % 3 == 0 else {}
+        jpg = bytearray(encode_jpeg(synth_rgb(rng, int(rng.integers(40, 200)), int(rng.integers(40, 200))), 90, **kw))
+        _, info = O.probe(bytes(jpg))
+        lo, hi = int(info.entropy_offset), len(jpg) - 2
+        kind = i % 5
+        p = int(rng.integers(lo, hi))
+        if kind == 0:
+            jpg = jpg[:p]                                   # truncated
+        elif kind == 1:
+            jpg[p] ^= int(rng.integers(1, 256))             # flipped byte (may break or keep the stream)
+        elif kind == 2:
+            jpg[p:p] = b"\xff\xff\xff\x00"                  # fill bytes before a stuffed zero
+        elif kind == 3:
+            jpg[p:p] = b"\xff\xd9"                          # a foreign marker mid-scan (EOI)
+        else:
+            jpg[p:p] = b"\xff\xd3"                          # an unexpected RSTn
+        out.append(bytes(jpg))
+    return out
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_mutated_streams_match_oracle_status_and_pixels(engine, seed):
+    """Status per sample equals the oracle's (OK / CORRUPT); OK samples are bit-exact."""
+    jpgs = _mutations(seed, 40)
+    res = (48, 64)
+    got, st = engine.decode_resize(jpgs, res)
+    for k, j in enumerate(jpgs):
+        ost, ref = _oracle_result(j, res)
+        assert int(st[k]) == ost, f"sample {k}: gpu {int(st[k])} vs oracle {ost}"
+        if ost == O.OK:
+            np.testing.assert_array_equal(got[k].cpu().numpy(), ref, err_msg=f"sample {k}")
+
+
+def test_empty_batch_and_single_pixel(engine):
+    got, st = engine.decode_resize([], (32, 32))
+    assert got.shape[0] == 0 and len(st) == 0
+    from tests.golden.synth import encode_jpeg
+    jpg = encode_jpeg(np.full((1, 1, 3), 200, np.uint8), 90)
+    got, st = engine.decode_resize([jpg] * 3, (5, 7))
+    assert (st == 0).all()
+    for k in range(3):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(jpg, (5, 7)))
