@@ -20,7 +20,6 @@ namespace sdsj {
 
 constexpr int kMaxComp = 3;
 constexpr int kMaxBlocksPerMcu = 10;  // D_MAX_BLOCKS_IN_MCU
-constexpr int kLutBits = 11;          // Huffman lookup width built by k_parse (99.7% of code lengths)
 constexpr int kRec = 64;              // block-boundary records kept per subsequence by k_entsync
 constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
@@ -38,22 +37,33 @@ struct HuffSpec {
   uint8_t vals[256];
 };
 
-// Per-image table block in device scratch: quantisation tables (natural order) + Huffman specs
-// + derived decode tables (jdhuff.c jpeg_make_d_derived_tbl + a 2^kLutBits lookahead table).
-struct HuffDerived {
-  int32_t maxcode[18];    // maxcode[l] for l = 1..16, maxcode[17] sentinel
-  int32_t valoffset[18];
-  uint16_t lut[1 << kLutBits];  // len | size << 4 | run << 8 (len = 0 -> slow path)
-  uint8_t vals[256];
-};
-
+// Per-image table block in device scratch: quantisation tables (natural order) + the raw Huffman
+// specs.  The entropy kernels derive their decode tables (jdhuff.c jpeg_make_d_derived_tbl plus a
+// lookahead table) from the specs in LDS, in parallel.
 struct ImgTables {
   uint16_t qt[4][64];
   uint8_t qt_defined[4];
   uint8_t pad[12];
   HuffSpec dc_spec[4], ac_spec[4];
-  HuffDerived dc[4], ac[4];
 };
+
+// jdhuff.c jpeg_make_d_derived_tbl validation of a table the scan uses: the canonical code
+// assignment must not overflow, and DC symbols must lie in 0..15 (JERR_BAD_HUFF_TABLE otherwise).
+// Tables the scan does not use are never validated (start_pass_huff_decoder).
+SDSJ_HD inline bool huff_table_ok(const HuffSpec& h, bool dc) {
+  int code = 0, p = 0;
+  for (int l = 1; l <= 16; l++) {
+    code += h.bits[l];
+    p += h.bits[l];
+    if (code >= (1 << l)) return false;  // codes of length <= l overflow (the all-ones code is reserved)
+    code <<= 1;
+  }
+  if (p > 256) return false;
+  if (dc)
+    for (int i = 0; i < p; i++)
+      if (h.vals[i] > 15) return false;
+  return true;
+}
 
 struct CompDesc {
   int32_t h, v, tq, td, ta;
@@ -118,7 +128,11 @@ struct ImgDesc {
   int64_t t_rs[4];
   // entropy warm-up: a subsequence's speculative decode starts up to warm_bits before its first bit
   // (inside its segment) and takes the first block boundary at or after that bit as its entry
-  int32_t warm_bits, pad1;
+  int32_t warm_bits;
+  // how the entropy-coded data ended (k_unstuff): the marker code (-1: end of input) and the
+  // entropy-relative index of its last FF byte
+  int32_t scan_end_code;
+  int64_t scan_end_raw;
 };
 
 // Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).
@@ -137,6 +151,8 @@ struct SubState {
   int32_t cur_dc[kMaxComp], spec_dc[kMaxComp], new_dc[kMaxComp], res_dc[kMaxComp], res_q[kMaxComp];
   int32_t nblk_ex, dc_ex[kMaxComp];
   int32_t first, seg;
+  uint32_t lim_bit;  // end of the interval's data: bits at or beyond it read as zeros (jpeg_fill_bit_buffer)
+  int32_t pad;
 };
 
 // One block boundary met by the speculative decode (for early sync detection).
@@ -146,6 +162,32 @@ struct SyncRec {
   uint8_t blk;      // MCU block index of the completed block
   uint8_t pad;
 };
+
+// Restart-interval table (scratch at off_seg).  Interval k = the k-th restart interval (the whole
+// scan without DRI).  k_unstuff fills [lo[k], hi[k]) = the unstuffed bytes it decodes, chosen the way
+// libjpeg's read_restart_marker / jpeg_resync_to_restart consume the markers it found (flag kEmpty:
+// the marker was left unread, libjpeg decodes an empty segment).  k_entwrite sets vend[k] (blocks
+// from vend[k] on stay zero: jdhuff.c insufficient_data) and kIns when the interval ran out of data.
+constexpr int kMarkerSlack = 64;  // marker-list entries beyond one per restart
+constexpr int32_t kSegEmpty = 1, kSegIns = 2;
+struct SegView {
+  int32_t *lo, *hi, *vend, *flag, *mk_out, *mk_raw, *mk_code;
+  int cap;
+};
+SDSJ_HD inline int64_t seg_bytes(int nseg) { return ((int64_t)(nseg + 1) * 2 + (int64_t)nseg * 2 + (int64_t)(nseg + kMarkerSlack) * 3) * 4; }
+SDSJ_HD inline SegView seg_view(uint8_t* base, int nseg) {
+  int32_t* p = reinterpret_cast<int32_t*>(base);
+  SegView v;
+  v.cap = nseg + kMarkerSlack;
+  v.lo = p;
+  v.hi = v.lo + nseg + 1;
+  v.vend = v.hi + nseg + 1;
+  v.flag = v.vend + nseg;
+  v.mk_out = v.flag + nseg;
+  v.mk_raw = v.mk_out + v.cap;
+  v.mk_code = v.mk_raw + v.cap;
+  return v;
+}
 
 SDSJ_HD inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 SDSJ_HD inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
@@ -163,10 +205,24 @@ inline int natural_order(int k) {
   return t[k];
 }
 
-// Parses markers up to the first SOS (jdmarker.c subset).  `rd(i)` returns byte i; `t` must be
-// non-null (no null checks: on the device it points into LDS).
+// Copies DHT values / DQT entries as the parser meets them (host probe and host planning).  The
+// device parser substitutes a sink that records the copies and runs them on all lanes.
 template <class Reader>
-SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t) {
+struct CopySink {
+  const Reader& rd;
+  SDSJ_HD void dht(HuffSpec* h, int64_t src, int cnt) const {
+    for (int q = 0; q < 256; q++) h->vals[q] = q < cnt ? (uint8_t)rd(src + q) : 0;
+  }
+  SDSJ_HD void dqt(uint16_t* qt, int pq, int64_t src) const {
+    for (int q = 0; q < 64; q++)
+      qt[natural_order(q)] = (uint16_t)(pq ? ((rd(src + 2 * q) << 8) | rd(src + 2 * q + 1)) : rd(src + q));
+  }
+};
+
+// Parses markers up to the first SOS (jdmarker.c subset).  `rd(i)` returns byte i; `t` must be
+// non-null (no null checks: on the device it points into LDS).  Bulk table bytes go through `sink`.
+template <class Reader, class Sink>
+SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t, const Sink& sink) {
   d->status = SDSJ_OK;
   d->width = d->height = d->ncomp = 0;
   d->restart_interval = 0;
@@ -236,7 +292,7 @@ SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t)
           }
           if (cnt > 256 || k + 17 + cnt > sl) return SDSJ_CORRUPT;
           h->bits[0] = 0;
-          for (int q = 0; q < 256; q++) h->vals[q] = q < cnt ? (uint8_t)rd(s + k + 17 + q) : 0;
+          sink.dht(h, s + k + 17, cnt);
           h->defined = 1;
           k += 17 + cnt;
         }
@@ -249,10 +305,7 @@ SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t)
           if (tq > 3 || pq > 1) return SDSJ_CORRUPT;
           int need = 1 + 64 * (pq ? 2 : 1);
           if (k + need > sl) return SDSJ_CORRUPT;
-          for (int q = 0; q < 64; q++) {
-            int v = pq ? ((rd(s + k + 1 + 2 * q) << 8) | rd(s + k + 2 + 2 * q)) : rd(s + k + 1 + q);
-            t->qt[tq][natural_order(q)] = (uint16_t)v;
-          }
+          sink.dqt(t->qt[tq], pq, s + k + 1);
           t->qt_defined[tq] = 1;
           k += need;
         }

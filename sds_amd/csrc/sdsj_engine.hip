@@ -148,6 +148,7 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
   SDSJ_HIP(e, launch_plan(n, e->descs, e->capacity, e->d_total, s));
   mark(2);
   SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, e->descs, e->scratch, s));
+  SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, e->descs, e->scratch, s));
   mark(3);
   SDSJ_HIP(e, launch_entsync(n, e->descs, e->tables, e->scratch, s));
   mark(4);
@@ -187,11 +188,14 @@ int sdsj_probe(const uint8_t* jpg, size_t n, sdsj_info* out) {
     const uint8_t* p;
     int operator()(int64_t i) const { return p[i]; }
   } rd{jpg};
-  int st = parse_headers(rd, (int64_t)n, &d, &t);
+  int st = parse_headers(rd, (int64_t)n, &d, &t, CopySink<R>{rd});
   out->width = d.width;
   out->height = d.height;
   out->ncomp = d.ncomp;
   if (st == SDSJ_OK) st = setup_geometry(&d, &t);
+  for (int c = 0; st == SDSJ_OK && c < d.ncomp; c++)
+    if (!huff_table_ok(t.dc_spec[d.comp[c].td], true) || !huff_table_ok(t.ac_spec[d.comp[c].ta], false))
+      st = SDSJ_CORRUPT;
   for (int c = 0; c < d.ncomp && c < 3; c++) {
     out->h_samp[c] = d.comp[c].h;
     out->v_samp[c] = d.comp[c].v;

@@ -96,25 +96,45 @@ __device__ int load_tables(EntTables& T, const ImgDesc* d, const ImgTables* tb) 
   __syncthreads();
   const int ns = T.nslots;
   if (!variant_owns<LB>(ns)) return ns;
-  constexpr int shift = kLutBits - LB;  // scratch tables are 2^kLutBits wide
-  for (int i = t; i < (ns << LB); i += blockDim.x) {
-    const int q = i >> LB, k = i & ((1 << LB) - 1);
-    const int key = T.slot_src[q];
-    const HuffDerived& h = (key & 4) ? tb->ac[key & 3] : tb->dc[key & 3];
-    const uint16_t e = h.lut[k << shift];
-    T.lut[i] = (e & 15) > LB ? (uint16_t)0 : e;  // codes longer than LB take the slow path
-  }
-  for (int i = t; i < ns * 18; i += blockDim.x) {
-    const int q = i / 18, k = i % 18;
-    const int key = T.slot_src[q];
-    const HuffDerived& h = (key & 4) ? tb->ac[key & 3] : tb->dc[key & 3];
-    T.maxcode[q][k] = h.maxcode[k];
-    T.valoff[q][k] = h.valoffset[k];
+  // canonical code bounds per slot (jdhuff.c jpeg_make_d_derived_tbl: maxcode / valoffset)
+  if (t < ns) {
+    const int key = T.slot_src[t];
+    const HuffSpec& h = (key & 4) ? tb->ac_spec[key & 3] : tb->dc_spec[key & 3];
+    int code = 0, p = 0;
+    for (int l = 1; l <= 16; l++) {
+      const int cnt = h.bits[l];
+      T.maxcode[t][l] = cnt ? code + cnt - 1 : -1;
+      T.valoff[t][l] = cnt ? p - code : 0;
+      p += cnt;
+      code = (code + cnt) << 1;
+    }
+    T.maxcode[t][0] = -1;
+    T.valoff[t][0] = 0;
+    T.maxcode[t][17] = 0xFFFFF;  // sentinel: the search stops at length 17 (bad code)
+    T.valoff[t][17] = 0;
   }
   for (int i = t; i < ns * 256; i += blockDim.x) {
     const int q = i >> 8, k = i & 255;
     const int key = T.slot_src[q];
-    T.vals[q][k] = (key & 4) ? tb->ac[key & 3].vals[k] : tb->dc[key & 3].vals[k];
+    T.vals[q][k] = (key & 4) ? tb->ac_spec[key & 3].vals[k] : tb->dc_spec[key & 3].vals[k];
+  }
+  __syncthreads();
+  // 2^LB lookahead entries: the shortest length whose code prefix is <= maxcode (len | size << 4 |
+  // run << 8); codes longer than LB bits (entry 0) take the canonical search in decode_sym
+  for (int i = t; i < (ns << LB); i += blockDim.x) {
+    const int q = i >> LB, k = i & ((1 << LB) - 1);
+    const bool dc = (T.slot_src[q] & 4) == 0;
+    uint16_t e = 0;
+    for (int l = 1; l <= LB; l++) {
+      const int code = k >> (LB - l);
+      if (code <= T.maxcode[q][l]) {
+        const int sym = T.vals[q][(code + T.valoff[q][l]) & 0xFF];
+        const int sz = dc ? sym : (sym & 15), run = dc ? 0 : (sym >> 4);
+        e = sz > 15 ? (uint16_t)0 : (uint16_t)(l | (sz << 4) | (run << 8));
+        break;
+      }
+    }
+    T.lut[i] = e;
   }
   __syncthreads();
   return ns;
@@ -136,13 +156,23 @@ struct Bits {
   int nq;        // valid words in q
   uint32_t wi;   // word index of q[0]
   uint32_t pos;  // absolute bit position of the next unconsumed bit
+  uint32_t lim;  // bits at or beyond lim read as zeros (the data ran into a marker)
   uint32_t q[kQ];
 };
 
-__device__ __forceinline__ void bits_init(Bits& b, const uint32_t* src, uint32_t p) {
+// Word w of the stream (MSB-first bits [32w, 32w + 32)), zeroed from bit `lim` on.
+__device__ __forceinline__ uint32_t load_word(const uint32_t* src, uint32_t w, uint32_t lim) {
+  const uint32_t b0 = w * 32u;
+  if (b0 >= lim) return 0u;
+  const uint32_t v = __builtin_bswap32(src[w]), keep = lim - b0;
+  return keep >= 32u ? v : (v & ~(0xFFFFFFFFu >> keep));
+}
+
+__device__ __forceinline__ void bits_init(Bits& b, const uint32_t* src, uint32_t p, uint32_t lim) {
   b.src = src;
+  b.lim = lim;
   const uint32_t w = p >> 5;
-  const uint32_t hi = __builtin_bswap32(src[w]), lo = __builtin_bswap32(src[w + 1]);
+  const uint32_t hi = load_word(src, w, lim), lo = load_word(src, w + 1, lim);
   const int sh = p & 31;
   b.buf = (((uint64_t)hi << 32) | lo) << sh;
   b.nb = 64 - sh;
@@ -155,8 +185,13 @@ __device__ __forceinline__ void bits_init(Bits& b, const uint32_t* src, uint32_t
 
 // Wave-synchronous refill: re-reads kQ words from wi (the ustream carries kUPad bytes of slack).
 __device__ __forceinline__ void bits_fill(Bits& b) {
+  if ((b.wi + kQ) * 32u <= b.lim) {  // the common case: all kQ words lie before the limit
 #pragma unroll
-  for (int k = 0; k < kQ; k++) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+    for (int k = 0; k < kQ; k++) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kQ; k++) b.q[k] = load_word(b.src, b.wi + k, b.lim);
+  }
   b.nq = kQ;
 }
 
@@ -213,8 +248,8 @@ __device__ __forceinline__ void decode_sym(const EntTables& T, Bits& b, int slot
 #pragma unroll
     for (int k = 16; k >= 1; k--) ll = (int32_t)(peek >> (16 - k)) <= T.maxcode[slot][k] ? k : ll;
     if (ll > 16) {
-      bad = 1;  // JWRN_HUFF_BAD_CODE
-      l = 16;
+      bad = 1;  // JWRN_HUFF_BAD_CODE: 17 bits consumed, symbol 0 (libjpeg warns and goes on)
+      l = 17;
       s = 0;
       r = 0;
     } else {
@@ -295,10 +330,11 @@ struct LdsSync {
 template <int LB>
 __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
                          uint32_t seg_start, uint32_t warm) {
+  // (bits at or beyond S.lim_bit read as zeros)
   const uint32_t start = S.start_bit, end = S.end_bit;
   const uint32_t ws = S.first ? start : (start - seg_start > warm ? start - warm : seg_start);
   Bits b;
-  bits_init(b, src, ws);
+  bits_init(b, src, ws, S.lim_bit);
   int blk = 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
   int d0 = 0, d1 = 0, d2 = 0;
   int c = ctx_c(K, 0), sdc = ctx_dc(K, 0), sac = ctx_ac(K, 0);
@@ -373,7 +409,7 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
   const uint32_t end = S.end_bit;
   const int nrec = S.nrec;
   Bits b;
-  bits_init(b, src, S.res_p);
+  bits_init(b, src, S.res_p, S.lim_bit);
   int blk = S.res_bz >> 8, z = S.res_bz & 0xFF;
   int nblk = S.res_nblk, ri = S.res_ri;
   int d0 = S.res_dc[0], d1 = S.res_dc[1], d2 = S.res_dc[2];
@@ -490,13 +526,13 @@ __global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_e
   }
   const BlkCtx K = make_ctx(L.T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
-  const int32_t* seg = reinterpret_cast<const int32_t*>(scratch + d->off_seg);
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
   SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
   SyncRec* recs = reinterpret_cast<SyncRec*>(scratch + d->off_rec);
   const int nseg = d->nseg;
   const uint32_t SB = (uint32_t)d->sub_bits;
 
-  // --- subsequence layout: segment s (bytes [seg[s], seg[s+1])) -> max(1, ceil(bits / SB)) ---
+  // --- subsequence layout: restart interval s (bytes [lo[s], hi[s])) -> max(1, ceil(bits / SB)) ---
   {
     int carry = 0;
     for (int base = 0; base < nseg; base += kEntThreads) {
@@ -504,8 +540,8 @@ __global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_e
       int cnt = 0;
       uint32_t b0 = 0, b1 = 0;
       if (s < nseg) {
-        b0 = (uint32_t)seg[s] * 8u;
-        b1 = (uint32_t)seg[s + 1] * 8u;
+        b0 = (uint32_t)sv.lo[s] * 8u;
+        b1 = (uint32_t)sv.hi[s] * 8u;
         if (b1 < b0) b1 = b0;
         cnt = b1 > b0 ? (int)((b1 - b0 + SB - 1) / SB) : 1;
       }
@@ -521,6 +557,7 @@ __global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_e
           S.end_bit = e < b1 ? e : b1;
           S.first = k == 0;
           S.seg = s;
+          S.lim_bit = b1;
         }
       }
       carry += total;
@@ -536,7 +573,7 @@ __global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_e
   if ((t & 63) == 0) L.wmax[t >> 6] = 0;
   __syncthreads();
   for (int j = t; j < nsub; j += kEntThreads) {
-    const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, (uint32_t)seg[sub[j].seg] * 8u,
+    const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, (uint32_t)sv.lo[sub[j].seg] * 8u,
                                 (uint32_t)d->warm_bits);
     nsym_spec += k;
     atomicMax(&L.wmax[t >> 6], k);
@@ -735,10 +772,10 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
   const EntTables& T = L.T;
   const BlkCtx K = make_ctx(T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
-  const int32_t* seg = reinterpret_cast<const int32_t*>(scratch + d->off_seg);
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
   const SubState* sub = reinterpret_cast<const SubState*>(scratch + d->off_sub);
   int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
-  const int nsub = d->nsub, nseg = d->nseg;
+  const int nsub = d->nsub;
   const int64_t blocks_per_seg = d->restart_interval ? (int64_t)d->restart_interval * K.bpm : d->total_blocks;
   const int my_base = t * kStageStride, sink_base = kEntThreads * kStageStride;
   int bad = 0;
@@ -750,7 +787,8 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
     Bits b;
     int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, sdc = 0, sac = 0;
     int64_t g = 0, gend = 0;
-    uint32_t end_bit = 0, done_p = 0, seg_end_bit = 0;
+    uint32_t end_bit = 0, lim = 0;
+    int s_int = 0;
     bool writing = false, last_of_seg = false, run = false;
     if (active) {
       const SubState& S = sub[j];
@@ -769,10 +807,13 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
       sac = ctx_ac(K, blk);
       writing = z == 0;
       end_bit = S.end_bit;
-      seg_end_bit = (uint32_t)seg[s + 1 <= nseg ? s + 1 : nseg] * 8u;
+      s_int = s;
+      lim = S.lim_bit;
       last_of_seg = (j + 1 == nsub) || sub[j + 1].first;
-      bits_init(b, src, S.entry_p);
-      run = g < gend && (b.pos < end_bit || z != 0);
+      bits_init(b, src, S.entry_p, S.lim_bit);
+      // the interval's last subsequence decodes every remaining block; when its data runs out
+      // (bits past lim, read as zeros) it finishes that MCU and stops: jdhuff.c insufficient_data
+      run = g < gend && (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
     }
     while (__builtin_amdgcn_ballot_w64(run)) {
       if (run) bits_fill(b);
@@ -804,9 +845,8 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
             sac = ctx_ac(K, blk);
             g++;
             writing = true;
-            if (g == gend) done_p = b.pos;
           }
-          run = g < gend && (b.pos < end_bit || z != 0);
+          run = g < gend && (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
         }
         // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
         const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
@@ -834,11 +874,11 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
       }
     }
     if (active && last_of_seg) {
-      if (g < gend) bad = 1;                    // segment ended before its last block
-      else if (done_p > seg_end_bit) bad = 1;   // last block needed bits past the segment
+      if (g < gend) sv.vend[s_int] = (int32_t)g;            // the rest of the interval stays zero
+      if (b.pos > lim) sv.flag[s_int] |= kSegIns;          // ran out of data (JWRN_HIT_MARKER)
     }
   }
-  if (bad) atomicOr(&L.bad, 1);
+  if (bad) atomicOr(&L.bad, 1);  // bad Huffman codes: libjpeg warns and decodes symbol 0 (statistics only)
   atomicAdd(&L.sym, nsym);
   if (lane == 0) atomicAdd(&L.it, 64ull * witers);
   __syncthreads();
@@ -846,7 +886,6 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
     d->sym_write = (int64_t)L.sym;
     d->it_write = (int64_t)L.it;
     d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - L.t0);
-    if (L.bad) d->status = SDSJ_CORRUPT;
   }
 }
 

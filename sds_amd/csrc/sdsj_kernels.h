@@ -10,6 +10,8 @@ hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, cons
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, hipStream_t s);
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
+hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
+                          hipStream_t s);
 hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
 hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);

@@ -134,7 +134,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
   };
   d->off_ustream = take(d->entropy_len + kUPad + 32);  // + the 16-byte granule of the final pad store
   d->ustream_cap = d->entropy_len + kUPad;
-  d->off_seg = take((int64_t)(d->nseg + 2) * 4);
+  d->off_seg = take(seg_bytes(d->nseg));
   d->off_sub = take((int64_t)d->nsub_cap * sizeof(SubState));
   d->off_rec = take((int64_t)d->nsub_cap * kRec * sizeof(SyncRec));
   d->off_coef = take(d->total_blocks * 128);
@@ -149,27 +149,58 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
   return o;
 }
 
+// Device sink of the shared parser: lane 0 records the DHT/DQT copies (the last definition of a
+// table wins, as with sequential copying); every lane then performs them.
+struct ParseJob {
+  int32_t kind;  // 0 DHT values, 1 DQT entries (pq = 0), 2 DQT entries (pq = 1)
+  int32_t cnt;
+  int64_t src;
+  void* dst;
+};
+constexpr int kMaxJobs = 16;
+
+struct DevSink {
+  ParseJob* jobs;
+  int* njobs;
+  const DevReader& rd;
+  __device__ void add(int kind, void* dst, int64_t src, int cnt) const {
+    for (int q = 0; q < *njobs; q++)
+      if (jobs[q].dst == dst) {
+        jobs[q] = ParseJob{kind, cnt, src, dst};
+        return;
+      }
+    if (*njobs < kMaxJobs) {
+      jobs[(*njobs)++] = ParseJob{kind, cnt, src, dst};
+      return;
+    }
+    // (more distinct tables than kMaxJobs cannot happen: 8 Huffman + 4 quantisation tables)
+  }
+  __device__ void dht(HuffSpec* h, int64_t src, int cnt) const { add(0, h->vals, src, cnt); }
+  __device__ void dqt(uint16_t* qt, int pq, int64_t src) const { add(pq ? 2 : 1, qt, src, 64); }
+};
+
 __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
                                               const int32_t* __restrict__ lengths, sdsj_op op, int warm_bits,
                                               ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables) {
   const int img = blockIdx.x;
   if (img >= n) return;
   const int lane = threadIdx.x;
-  __shared__ uint8_t hdr[kHdrStage];
+  __shared__ alignas(16) uint8_t hdr[kHdrStage];
   __shared__ ImgDesc sd;
   __shared__ ImgTables st;
-  __shared__ int16_t huffsize[257];
-  __shared__ int32_t huffcode[257];
-  __shared__ int s_status;
+  __shared__ ParseJob jobs[kMaxJobs];
+  __shared__ int njobs, s_status;
 
   const uint8_t* g = blob + offsets[img];
   const int64_t len = lengths[img];
   const int64_t nstage = len < kHdrStage ? len : kHdrStage;
   for (int64_t i = lane; i < nstage; i += 64) hdr[i] = g[i];
+  if (lane == 0) njobs = 0;
   __syncthreads();
+  DevReader rd{hdr, nstage, g};
   if (lane == 0) {
-    DevReader rd{hdr, nstage, g};
-    int status = parse_headers(rd, len, &sd, &st);
+    DevSink sink{jobs, &njobs, rd};
+    int status = parse_headers(rd, len, &sd, &st, sink);
     if (status == SDSJ_OK) status = setup_geometry(&sd, &st);
     if (status == SDSJ_OK) plan_image(&sd, op);
     if (warm_bits >= 0) sd.warm_bits = warm_bits;
@@ -178,65 +209,26 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
     s_status = status;
   }
   __syncthreads();
-  if (s_status == SDSJ_OK) {
-    // Derived Huffman tables for every defined table (jdhuff.c jpeg_make_d_derived_tbl).
-    for (int tix = 0; tix < 8; tix++) {
-      const HuffSpec& hs = tix < 4 ? st.dc_spec[tix] : st.ac_spec[tix - 4];
-      HuffDerived& hd = tix < 4 ? st.dc[tix] : st.ac[tix - 4];
-      if (!hs.defined) continue;
-      if (lane == 0) {
-        int p = 0;
-        for (int l = 1; l <= 16; l++)
-          for (int i = 0; i < hs.bits[l]; i++) huffsize[p++] = (int16_t)l;
-        huffsize[p] = 0;
-        int code = 0, si = huffsize[0];
-        p = 0;
-        bool bad = false;
-        while (huffsize[p]) {
-          while (huffsize[p] == si) huffcode[p++] = code++;
-          if (code >= (1 << si)) bad = true;
-          code <<= 1;
-          si++;
-        }
-        p = 0;
-        for (int l = 1; l <= 16; l++) {
-          if (hs.bits[l]) {
-            hd.valoffset[l] = p - huffcode[p];
-            p += hs.bits[l];
-            hd.maxcode[l] = huffcode[p - 1];
-          } else {
-            hd.maxcode[l] = -1;
-            hd.valoffset[l] = 0;
-          }
-        }
-        hd.maxcode[0] = -1;
-        hd.valoffset[0] = 0;
-        hd.maxcode[17] = 0xFFFFF;
-        hd.valoffset[17] = 0;
-        huffsize[256] = (int16_t)p;  // symbol count
-        if (bad) s_status = SDSJ_CORRUPT;
-      }
-      __syncthreads();
-      for (int i = lane; i < (1 << kLutBits); i += 64) hd.lut[i] = 0;
-      for (int i = lane; i < 256; i += 64) hd.vals[i] = hs.vals[i];
-      __syncthreads();
-      const int nsym = huffsize[256];
-      for (int k = lane; k < nsym; k += 64) {
-        int l = huffsize[k];
-        if (l <= kLutBits) {
-          int base = huffcode[k] << (kLutBits - l);
-          int cnt = 1 << (kLutBits - l);
-          const int sym = hs.vals[k];
-          const int sz = tix < 4 ? sym : (sym & 15);  // DC: category; AC: size
-          const int run = tix < 4 ? 0 : (sym >> 4);
-          // (len | size << 4 | run << 8); DC categories > 15 take the slow path (flagged there)
-          uint16_t e = sz > 15 ? (uint16_t)0 : (uint16_t)(l | (sz << 4) | (run << 8));
-          for (int r = 0; r < cnt; r++) hd.lut[base + r] = e;
-        }
-      }
-      __syncthreads();
+  // the recorded table copies, all lanes (values beyond a DHT's count are zero, jdmarker.c get_dht)
+  const int nj = njobs;
+  for (int q = 0; q < nj; q++) {
+    const ParseJob jb = jobs[q];
+    if (jb.kind == 0) {
+      uint8_t* v = static_cast<uint8_t*>(jb.dst);
+      for (int i = lane; i < 256; i += 64) v[i] = i < jb.cnt ? (uint8_t)rd(jb.src + i) : 0;
+    } else {
+      uint16_t* qt = static_cast<uint16_t*>(jb.dst);
+      const int i = lane;
+      qt[natural_order(i)] = (uint16_t)(jb.kind == 2 ? ((rd(jb.src + 2 * i) << 8) | rd(jb.src + 2 * i + 1)) : rd(jb.src + i));
     }
-    if (lane == 0) sd.status = s_status;
+  }
+  __syncthreads();
+  // validation of the tables the scan uses (jdhuff.c jpeg_make_d_derived_tbl), one lane per table
+  if (s_status == SDSJ_OK && lane < 2 * sd.ncomp) {
+    const int c = lane >> 1;
+    const bool dc = (lane & 1) == 0;
+    const HuffSpec& h = dc ? st.dc_spec[sd.comp[c].td] : st.ac_spec[sd.comp[c].ta];
+    if (!huff_table_ok(h, dc)) sd.status = SDSJ_CORRUPT;
   }
   __syncthreads();
   // write back
@@ -317,6 +309,122 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
+// jdmarker.c read_markers after the scan, up to EOI, from the marker whose last FF is raw[pos]
+// (thread-serial; normally one step: EOI).
+__device__ int post_scan_markers(const uint8_t* raw, int64_t n, int64_t pos) {
+  for (int guard = 0; guard < 4096; guard++) {
+    if (pos + 1 >= n) return SDSJ_OK;
+    const int m = raw[pos + 1];
+    const int64_t body = pos + 2;
+    if (m == 0xD9) return SDSJ_OK;
+    if ((m >= 0xD0 && m <= 0xD7) || m == 0x01) {
+      pos = body;
+    } else {
+      const bool is_seg = (m >= 0xE0 && m <= 0xEF) || m == 0xFE || m == 0xDC || m == 0xCC || m == 0xDD || m == 0xC4 ||
+                          m == 0xDB;
+      if (!is_seg) return SDSJ_CORRUPT;  // second SOI/SOF/SOS, JPGn, unknown (JERR_*)
+      if (body + 2 > n) return SDSJ_OK;
+      const int64_t len = (raw[body] << 8) | raw[body + 1];
+      if (len < 2) return SDSJ_CORRUPT;
+      if (body + len > n) return SDSJ_OK;
+      const uint8_t* q = raw + body + 2;
+      const int64_t sl = len - 2;
+      if (m == 0xDD && len != 4) return SDSJ_CORRUPT;
+      if (m == 0xC4) {
+        for (int64_t k = 0; k < sl;) {
+          if (k + 17 > sl || (q[k] >> 4) > 1 || (q[k] & 15) > 3) return SDSJ_CORRUPT;
+          int64_t cnt = 0;
+          for (int l = 1; l <= 16; l++) cnt += q[k + l];
+          if (cnt > 256 || k + 17 + cnt > sl) return SDSJ_CORRUPT;
+          k += 17 + cnt;
+        }
+      }
+      if (m == 0xDB) {
+        for (int64_t k = 0; k < sl;) {
+          if ((q[k] & 15) > 3) return SDSJ_CORRUPT;
+          const int64_t need = 1 + 64 * ((q[k] >> 4) ? 2 : 1);
+          if (k + need > sl) return SDSJ_CORRUPT;
+          k += need;
+        }
+      }
+      pos = body + len;
+    }
+    // next_marker: skip data bytes, fill bytes and FF00 pairs
+    for (;;) {
+      while (pos < n && raw[pos] != 0xFF) pos++;
+      if (pos >= n) return SDSJ_OK;
+      int64_t p = pos + 1;
+      while (p < n && raw[p] == 0xFF) p++;
+      if (p >= n) return SDSJ_OK;
+      if (raw[p] != 0) {
+        pos = p - 1;
+        break;
+      }
+      pos = p + 1;
+    }
+  }
+  return SDSJ_CORRUPT;
+}
+
+// Restart intervals -> data segments, then the markers after the scan (one thread; kept out of line
+// so its registers do not weigh on the tile loop).
+__device__ void finish_scan(ImgDesc* d, const SegView sv, const uint8_t* raw, int64_t L, int m, int end_code,
+                                       int64_t end_raw, int64_t out_pos, int overflow) {
+  const int nseg = d->nseg;
+  int status = SDSJ_OK;
+  if (overflow) status = SDSJ_CORRUPT;
+  // the input ended inside the scan (no marker): Pillow reports "image file is truncated"
+  if (end_code < 0) status = SDSJ_CORRUPT;
+  // Restart intervals -> data segments D_0 = [0, mk_out[0]), D_i = [mk_out[i-1], mk_out[i]),
+  // D_m = [mk_out[m-1], out_pos); the marker after D_i is mk[i] (i < m) or the end marker.
+  // jdhuff.c process_restart -> jdmarker.c read_restart_marker / jpeg_resync_to_restart.
+  auto d_lo = [&](int i) { return i == 0 ? 0 : sv.mk_out[i - 1]; };
+  auto d_hi = [&](int i) { return i < m ? sv.mk_out[i] : (int32_t)out_pos; };
+  int cand = 0;  // the data segment being read / the marker after it
+  sv.lo[0] = 0;
+  sv.hi[0] = d_hi(0);
+  sv.flag[0] = 0;
+  for (int k = 1; k < nseg && status == SDSJ_OK; k++) {
+    const int desired = (k - 1) & 7;
+    for (;;) {
+      const int mc = cand < m ? sv.mk_code[cand] : end_code;
+      int action;
+      if (mc == 0xD0 + desired) action = 1;
+      else if (mc < 0xC0) action = 2;
+      else if (mc < 0xD0 || mc > 0xD7) action = 3;
+      else if (mc == 0xD0 + ((desired + 1) & 7) || mc == 0xD0 + ((desired + 2) & 7)) action = 3;
+      else if (mc == 0xD0 + ((desired - 1) & 7) || mc == 0xD0 + ((desired - 2) & 7)) action = 2;
+      else action = 1;
+      if (action == 1) {  // marker consumed: the interval decodes the next data segment
+        cand++;
+        sv.lo[k] = d_lo(cand);
+        sv.hi[k] = d_hi(cand);
+        sv.flag[k] = 0;
+        break;
+      }
+      if (action == 3) {  // marker left unread: an empty segment
+        sv.lo[k] = sv.hi[k] = d_hi(cand);
+        sv.flag[k] = kSegEmpty;
+        break;
+      }
+      if (cand >= m) {  // (unreachable: the end marker is >= SOF0, an end of input failed above)
+        status = SDSJ_CORRUPT;
+        break;
+      }
+      cand++;  // action 2: skip to the next marker
+    }
+  }
+  // jpeg_finish_decompress: markers from the one after the last decoded data up to EOI
+  for (; status == SDSJ_OK && cand < m; cand++) {
+    const int mc = sv.mk_code[cand];
+    if (!((mc >= 0xD0 && mc <= 0xD7) || mc == 0x01)) status = SDSJ_CORRUPT;  // unknown marker
+  }
+  if (status == SDSJ_OK)
+    status = post_scan_markers(raw, d->entropy_off + L, d->entropy_off + end_raw);
+  sv.lo[nseg] = sv.hi[nseg] = (int32_t)out_pos;
+  if (status != SDSJ_OK) d->status = status;
+}
+
 __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_t* __restrict__ blob,
                                                              const int64_t* __restrict__ offsets,
                                                              ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch) {
@@ -326,24 +434,26 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
   if (d->status != SDSJ_OK) return;
   __shared__ alignas(16) uint8_t buf[kUsTile + 32];  // [carried tail][this tile's output]
   __shared__ int wsum[kUnstuffThreads / 64];
-  __shared__ int s_end, s_cut;
+  __shared__ int s_end, s_end_code, s_overflow;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint8_t* e = blob + offsets[img] + d->entropy_off;
+  const uint8_t* raw = blob + offsets[img];
+  const uint8_t* e = raw + d->entropy_off;
   const int64_t L = d->entropy_len;
   const uintptr_t e_end = (uintptr_t)(e + L);  // dwords starting below this lie in mapped pages
   uint8_t* out = scratch + d->off_ustream;  // 256-byte aligned
-  int32_t* seg = reinterpret_cast<int32_t*>(scratch + d->off_seg);
   const int nseg = d->nseg;
-  if (t == 0) seg[0] = 0;
+  const SegView sv = seg_view(scratch + d->off_seg, nseg);
+  if (t == 0) {
+    s_overflow = 0;
+    s_end_code = -1;
+  }
 
   int64_t out_pos = 0;  // bytes emitted so far; [out_pos & ~15, out_pos) sit in buf[0, carry)
-  int rst_count = 0;
+  int nmk = 0;          // split markers (RSTn, and codes below SOF0) met so far
+  int64_t end_raw = -1; // entropy-relative index of the last FF of the terminating marker
   bool ended = false;
   for (int64_t base = 0; base < L && !ended; base += kUsTile) {
-    if (t == 0) {
-      s_end = 0x7fffffff;
-      s_cut = 0x7fffffff;
-    }
+    if (t == 0) s_end = 0x7fffffff;
     // bytes [my0 - 4, my0 + 32) as 9 realigned dwords u[0..8] (u[0] holds the 4 preceding bytes;
     // entropy_off >= 4, so they are header bytes of the same image)
     const int64_t my0 = base + (int64_t)t * kUsBytes;
@@ -356,35 +466,52 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
     uint32_t u[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) u[k] = (uint32_t)((((uint64_t)v[k + 1] << 32) | v[k]) >> (8 * sh));
-    // classify: 0 skip, 1 emit, 2 RSTn, 3 end (other marker or end of input)
-    uint64_t kind = 0;
-    int prev = my0 > 0 ? (int)(u[0] >> 24) : 0;
-    int my_end = kUsBytes;
+    // classify the 32 bytes as bit masks (bit k = byte k): FF bytes are skipped (fill / stuffing
+    // prefix); a byte after FF is a stuffed zero (emitted as 0xFF) or a marker code; markers split
+    // the data (RSTn, and codes below SOF0: the restart logic decides) or end it (any other marker,
+    // or the end of the input)
+    uint32_t isff = 0, isz = 0;
 #pragma unroll
-    for (int k = 0; k < kUsBytes; k++) {
-      const int c = (int)(u[1 + (k >> 2)] >> (8 * (k & 3))) & 0xFF;
-      int kd;
-      if (my0 + k >= L) kd = 3;
-      else if (prev == 0xFF) kd = c == 0x00 ? 1 : (c == 0xFF ? 0 : ((c >= 0xD0 && c <= 0xD7) ? 2 : 3));
-      else kd = c == 0xFF ? 0 : 1;
-      kind |= (uint64_t)kd << (2 * k);
-      if (kd == 3 && my_end == kUsBytes) my_end = k;
-      prev = c;
+    for (int q = 0; q < 8; q++) {
+      const uint32_t x = u[1 + q], y = ~x;
+      const uint32_t zz = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // zero bytes
+      const uint32_t zf = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;  // 0xFF bytes
+      isz |= (((zz >> 7) & 1) | ((zz >> 14) & 2) | ((zz >> 21) & 4) | ((zz >> 28) & 8)) << (4 * q);
+      isff |= (((zf >> 7) & 1) | ((zf >> 14) & 2) | ((zf >> 21) & 4) | ((zf >> 28) & 8)) << (4 * q);
     }
+    const uint32_t prevff = (isff << 1) | ((my0 > 0 && (u[0] >> 24) == 0xFF) ? 1u : 0u);
+    const int64_t nvalid = L - my0;
+    const uint32_t vmask = nvalid >= kUsBytes ? 0xFFFFFFFFu : (nvalid <= 0 ? 0u : ((1u << nvalid) - 1u));
+    const uint32_t marker = prevff & ~isz & ~isff & vmask;
+    const uint32_t stuffed = prevff & isz;
+    const uint32_t emit = ~isff & ~marker & vmask;
+    uint32_t split = 0, endm = ~vmask;  // the first byte past the input ends it as well
+    for (uint32_t mk = marker; mk;) {   // rare: one iteration per marker
+      const int k = __builtin_ctz(mk);
+      mk &= mk - 1;
+      uint32_t dw = 0;
+#pragma unroll
+      for (int q = 0; q < 8; q++) dw = q == (k >> 2) ? u[1 + q] : dw;
+      const int c = (int)(dw >> (8 * (k & 3))) & 0xFF;
+      if ((c >= 0xD0 && c <= 0xD7) || c < 0xC0) split |= 1u << k;
+      else endm |= 1u << k;
+    }
+    const int my_end = endm ? __builtin_ctz(endm) : kUsBytes;
     __syncthreads();  // s_end initialised; buf tail of the previous tile settled
     if (my_end < kUsBytes) atomicMin(&s_end, t * kUsBytes + my_end);
     __syncthreads();
     const int tile_end = s_end;
+    if (my_end < kUsBytes && tile_end == t * kUsBytes + my_end) {  // the earliest end: its marker code
+      uint32_t dw = 0;
+#pragma unroll
+      for (int q = 0; q < 8; q++) dw = q == (my_end >> 2) ? u[1 + q] : dw;
+      s_end_code = ((vmask >> my_end) & 1) ? (int)(dw >> (8 * (my_end & 3))) & 0xFF : -1;
+    }
     int lim = tile_end - t * kUsBytes;
     lim = lim < 0 ? 0 : (lim > kUsBytes ? kUsBytes : lim);
-    int nemit = 0, nrst = 0;
-#pragma unroll
-    for (int k = 0; k < kUsBytes; k++) {
-      const int kd = (int)(kind >> (2 * k)) & 3;
-      nemit += (k < lim && kd == 1) ? 1 : 0;
-      nrst += (k < lim && kd == 2) ? 1 : 0;
-    }
-    const int packed = nemit | (nrst << 16);
+    const uint32_t below = lim >= kUsBytes ? 0xFFFFFFFFu : ((1u << lim) - 1u);
+    const uint32_t em = emit & below, sp = split & below;
+    const int packed = __popc(em) | (__popc(sp) << 16);
     const int incl = wave_incl_scan(packed);
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
@@ -397,22 +524,29 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
     const int excl = before + incl - packed;
     const int carry = (int)(out_pos & 15);
     int pos = excl & 0xFFFF;
-    int r = rst_count + (excl >> 16);
 #pragma unroll
     for (int k = 0; k < kUsBytes; k++) {
-      const int kd = (int)(kind >> (2 * k)) & 3;
       // an emitted byte is itself, or 0xFF for the stuffed 0x00 of an FF00 pair
-      const uint32_t raw = (u[1 + (k >> 2)] >> (8 * (k & 3))) & 0xFF;
-      if (k < lim && kd == 1) buf[carry + pos++] = (uint8_t)(raw == 0 && (k ? (u[1 + ((k - 1) >> 2)] >> (8 * ((k - 1) & 3))) & 0xFF : (my0 > 0 ? u[0] >> 24 : 0)) == 0xFF ? 0xFF : raw);
-      if (k < lim && kd == 2) {
-        r++;
-        if (r < nseg) seg[r] = (int32_t)(out_pos + pos);
-        else atomicMin(&s_cut, pos);  // more RSTn than restart intervals: a foreign marker, the scan ends
+      const uint32_t rawb = (u[1 + (k >> 2)] >> (8 * (k & 3))) & 0xFF;
+      if ((em >> k) & 1) buf[carry + pos++] = (uint8_t)(((stuffed >> k) & 1) ? 0xFF : rawb);
+    }
+    int r = nmk + (excl >> 16);
+    for (uint32_t mk = sp; mk; r++) {  // rare: the split markers, in order
+      const int k = __builtin_ctz(mk);
+      mk &= mk - 1;
+      uint32_t dw = 0;
+#pragma unroll
+      for (int q = 0; q < 8; q++) dw = q == (k >> 2) ? u[1 + q] : dw;
+      if (r < sv.cap) {
+        sv.mk_out[r] = (int32_t)(out_pos + (excl & 0xFFFF) + __popc(em & ((1u << k) - 1u)));
+        sv.mk_raw[r] = (int32_t)(my0 + k - 1);
+        sv.mk_code[r] = (int32_t)(dw >> (8 * (k & 3))) & 0xFF;
+      } else {
+        s_overflow = 1;
       }
     }
     __syncthreads();
-    const int cut = s_cut;
-    const int temit = cut != 0x7fffffff ? cut : (total & 0xFFFF);
+    const int temit = total & 0xFFFF;
     // full 16-byte chunks of [out_pos & ~15, out_pos + temit) leave; the tail is carried
     const int have = carry + temit, full = have >> 4;
     uint4* dst = reinterpret_cast<uint4*>(out + (out_pos & ~(int64_t)15));
@@ -423,9 +557,11 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
     __syncthreads();
     if (t < rem) buf[t] = tail;
     out_pos += temit;
-    rst_count += total >> 16;
-    if (rst_count > nseg - 1) rst_count = nseg - 1;
-    if (tile_end != 0x7fffffff || cut != 0x7fffffff) ended = true;
+    nmk += total >> 16;
+    if (tile_end != 0x7fffffff) {
+      ended = true;
+      end_raw = base + tile_end - 1;
+    }
   }
   __syncthreads();
   // the carried tail, then zero padding so the bit reader can over-read safely
@@ -448,12 +584,31 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
       reinterpret_cast<uint4*>(out + a0)[i] = make_uint4(wds[0], wds[1], wds[2], wds[3]);
     }
   }
-  if (t == 0) {
-    seg[nseg] = (int32_t)out_pos;
-    d->ulen = out_pos;
-    d->useg_found = 1 + rst_count;
-    if (1 + rst_count < nseg) d->status = SDSJ_CORRUPT;  // missing restart markers
+  const int64_t bps = d->restart_interval ? (int64_t)d->restart_interval * d->bpm : d->total_blocks;
+  for (int k = t; k < nseg; k += kUnstuffThreads) {
+    const int64_t ge = (int64_t)(k + 1) * bps;
+    sv.vend[k] = (int32_t)(ge < d->total_blocks ? ge : d->total_blocks);
   }
+  __syncthreads();
+  if (t == 0) {
+    d->ulen = out_pos;
+    d->useg_found = 1 + nmk;
+    d->scan_end_code = ended ? s_end_code : -1;
+    d->scan_end_raw = end_raw;
+    if (s_overflow) d->status = SDSJ_CORRUPT;
+  }
+}
+
+// k_scanmap: one thread per image -- restart intervals -> data segments and the markers after the scan
+// (finish_scan), from what k_unstuff recorded.
+__global__ void __launch_bounds__(64) k_scanmap(int n, const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
+                                                ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.x * 64 + threadIdx.x;
+  if (img >= n) return;
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK) return;
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+  finish_scan(d, sv, blob + offsets[img], d->entropy_len, d->useg_found - 1, d->scan_end_code, d->scan_end_raw, d->ulen, 0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -572,6 +727,17 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
   uint8_t* planes = scratch + d->off_planes;
   const int ngroups = gstart[ncomp];
+  // blocks the entropy decoder left zero (jdhuff.c insufficient_data): from vend[k] to the end of
+  // restart interval k, and all of an empty interval entered out of data
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+  const int nseg = d->nseg;
+  const int bps = d->restart_interval ? d->restart_interval * bpm : (int)d->total_blocks;
+  const int vend0 = sv.vend[0];
+  auto zero_block = [&](int g) {
+    if (nseg == 1) return g >= vend0;
+    const int k = g / bps;
+    return g >= sv.vend[k] || (k > 0 && (sv.flag[k] & kSegEmpty) && (sv.flag[k - 1] & kSegIns));
+  };
   // block of this lane in group grp: component, block coordinates, decode-order index
   auto locate = [&](int grp, int& c, int& by, int& bx, int& g) {
     c = ncomp > 1 && grp >= gstart[1] ? (ncomp > 2 && grp >= gstart[2] ? 2 : 1) : 0;
@@ -592,7 +758,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
     if (valid) {
       // row r of the block, dequantised (DEQUANTIZE: coef * quantval)
       int16_t vv[8];
-      *reinterpret_cast<uint4*>(vv) = raw;
+      *reinterpret_cast<uint4*>(vv) = zero_block(g) ? make_uint4(0, 0, 0, 0) : raw;
       for (int k = 0; k < 8; k++) W[r * 8 + k] = (int)vv[k] * qt[c][r * 8 + k];
     }
     wave_lds_sync();
@@ -942,6 +1108,11 @@ hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, Im
   hipLaunchKernelGGL(k_unstuff, dim3(n), dim3(kUnstuffThreads), 0, s, n, blob, offsets, descs, scratch);
   return hipGetLastError();
 }
+hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_scanmap, dim3((n + 63) / 64), dim3(64), 0, s, n, blob, offsets, descs, scratch);
+  return hipGetLastError();
+}
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
   hipLaunchKernelGGL(k_idct, dim3(64, n), dim3(kIdctThreads), 0, s, n, descs, tables, scratch);
   return hipGetLastError();
@@ -977,7 +1148,7 @@ int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* st
   ImgDesc d;
   static thread_local ImgTables t;
   HostReader rd{jpg};
-  int st = parse_headers(rd, n, &d, &t);
+  int st = parse_headers(rd, n, &d, &t, CopySink<HostReader>{rd});
   if (st == SDSJ_OK) st = setup_geometry(&d, &t);
   int64_t need = 0;
   if (st == SDSJ_OK) need = plan_image(&d, op);

@@ -51,3 +51,30 @@ def synth_mixed(n: int, seed: int = 4321, quality: int = 90, max_side: int = 384
         w, h = pool[int(rng.integers(0, len(pool)))]
         out.append(encode_jpeg(synth_rgb(rng, w, h), quality))
     return out
+
+
+def mutated_jpegs(seed: int, n: int) -> list[bytes]:
+    """Truncations, byte flips and marker-like insertions inside the entropy segment of synthetic JPEGs
+    (the FF00 / fill-byte / RSTn / foreign-marker paths of jdhuff.c jpeg_fill_bit_buffer)."""
+    from oracle import oracle as O  # only to locate the entropy segment (test infrastructure)
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        kw = {"restart_marker_blocks": 2} if i % 3 == 0 else {}
+        jpg = bytearray(encode_jpeg(synth_rgb(rng, int(rng.integers(40, 200)), int(rng.integers(40, 200))), 90, **kw))
+        _, info = O.probe(bytes(jpg))
+        lo, hi = int(info.entropy_offset), len(jpg) - 2
+        kind = i % 5
+        p = int(rng.integers(lo, hi))
+        if kind == 0:
+            jpg = jpg[:p]                                   # truncated
+        elif kind == 1:
+            jpg[p] ^= int(rng.integers(1, 256))             # flipped byte (may break or keep the stream)
+        elif kind == 2:
+            jpg[p:p] = b"\xff\xff\xff\x00"                  # fill bytes before a stuffed zero
+        elif kind == 3:
+            jpg[p:p] = b"\xff\xd9"                          # a foreign marker mid-scan (EOI)
+        else:
+            jpg[p:p] = b"\xff\xd3"                          # an unexpected RSTn
+        out.append(bytes(jpg))
+    return out

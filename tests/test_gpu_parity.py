@@ -168,37 +168,11 @@ def _oracle_result(jpg, res):
         return e.status, None
 
 
-def _mutations(seed, n):
-    """Truncations, byte flips and marker-like insertions inside the entropy segment of synthetic JPEGs
-    (the FF00 / fill-byte / RSTn / foreign-marker paths of jdhuff.c jpeg_fill_bit_buffer)."""
-    from tests.golden.synth import encode_jpeg, synth_rgb
-    rng = np.random.default_rng(seed)
-    out = []
-    for i in range(n):
-        kw = {"restart_marker_blocks": 2} if i % 3 == 0 else {}
-        jpg = bytearray(encode_jpeg(synth_rgb(rng, int(rng.integers(40, 200)), int(rng.integers(40, 200))), 90, **kw))
-        _, info = O.probe(bytes(jpg))
-        lo, hi = int(info.entropy_offset), len(jpg) - 2
-        kind = i % 5
-        p = int(rng.integers(lo, hi))
-        if kind == 0:
-            jpg = jpg[:p]                                   # truncated
-        elif kind == 1:
-            jpg[p] ^= int(rng.integers(1, 256))             # flipped byte (may break or keep the stream)
-        elif kind == 2:
-            jpg[p:p] = b"\xff\xff\xff\x00"                  # fill bytes before a stuffed zero
-        elif kind == 3:
-            jpg[p:p] = b"\xff\xd9"                          # a foreign marker mid-scan (EOI)
-        else:
-            jpg[p:p] = b"\xff\xd3"                          # an unexpected RSTn
-        out.append(bytes(jpg))
-    return out
-
-
 @pytest.mark.parametrize("seed", [11, 12])
 def test_mutated_streams_match_oracle_status_and_pixels(engine, seed):
     """Status per sample equals the oracle's (OK / CORRUPT); OK samples are bit-exact."""
-    jpgs = _mutations(seed, 40)
+    from tests.golden.synth import mutated_jpegs
+    jpgs = mutated_jpegs(seed, 40)
     res = (48, 64)
     got, st = engine.decode_resize(jpgs, res)
     for k, j in enumerate(jpgs):
@@ -217,3 +191,19 @@ def test_empty_batch_and_single_pixel(engine):
     assert (st == 0).all()
     for k in range(3):
         np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(jpg, (5, 7)))
+
+
+def test_g5_edge_cases(engine):
+    """Huffman-table validation, scan termination, premature markers and post-scan markers as the reference
+    loader behaves (tests/golden/make_edge.py): decodable cases bit-exact at full resolution."""
+    import base64
+    from sds_amd import _lib
+    for c in G.load_json("g5_edge.json")["cases"]:
+        jpg = base64.b64decode(c["jpg_b64"])
+        if c["outcome"] != "ok":
+            assert _status(engine, jpg) == _lib.CORRUPT, c["name"]
+            continue
+        w, h = c["size"]
+        full, st = engine.decode_resize([jpg], (h, w), layout="hwc")
+        assert st[0] == 0, c["name"]
+        assert G.sha(full[0].cpu().numpy()) == c["rgb_sha256"], c["name"]

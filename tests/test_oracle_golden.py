@@ -50,3 +50,37 @@ def test_g3_mixed_sizes_flip_normalize():
         assert G.sha(jpg) == im["jpg_sha256"]
         assert G.sha(O.pipeline(jpg, (512, 512), flip=im["flip"])) == im["u8_512_sha256"]
         assert G.sha(O.pipeline(jpg, (512, 512), flip=im["flip"], normalize=True)) == im["f32_512_sha256"]
+
+
+def test_g5_edge_cases():
+    """Table validation, scan termination and post-scan markers as the reference loader behaves."""
+    import base64
+    for c in G.load_json("g5_edge.json")["cases"]:
+        jpg = base64.b64decode(c["jpg_b64"])
+        if c["outcome"] == "ok":
+            assert G.sha(O.decode(jpg)) == c["rgb_sha256"], c["name"]
+        else:
+            with pytest.raises(O.OracleError):
+                O.decode(jpg)
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_oracle_status_matches_pil_on_mutated_streams(seed):
+    """Truncations, byte flips, fill bytes, premature EOI / RSTn: decodable exactly when PIL decodes them
+    (libjpeg-turbo's warning-and-continue recovery).  Pixels are compared where no garbage coefficients
+    are involved (premature markers); garbage blocks follow libjpeg's C IDCT, not the x86 SIMD one."""
+    import io
+    Image = pytest.importorskip("PIL.Image")
+    from tests.golden.synth import mutated_jpegs
+    for i, jpg in enumerate(mutated_jpegs(seed, 40)):
+        try:
+            ref = np.asarray(Image.open(io.BytesIO(jpg)).convert("RGB"))
+        except OSError:
+            ref = None
+        try:
+            got = O.decode(jpg)
+        except O.OracleError:
+            got = None
+        assert (ref is None) == (got is None), f"sample {i}"
+        if ref is not None and i % 5 in (3, 4):
+            np.testing.assert_array_equal(got, ref, err_msg=f"sample {i}")
