@@ -62,23 +62,33 @@ def _make_pool_image(i: int) -> bytes:
     return encode_jpeg(synth_rgb(np.random.default_rng(1234 + i), 640, 480), 90)
 
 
-def make_pool(n: int, workers: int) -> list[bytes]:
+def _make_mixed_image(i: int) -> bytes:
+    # configs[2]: size drawn uniformly from the VGA..4K landscape sizes and their
+    # portrait transposes, content from the same seeded generator
+    from tests.golden.synth import MIXED_SIZES, encode_jpeg, synth_rgb
+    rng = np.random.default_rng(4321 + i)
+    w, h = MIXED_SIZES[int(rng.integers(0, len(MIXED_SIZES)))]
+    return encode_jpeg(synth_rgb(rng, w, h), 90)
+
+
+def make_pool(n: int, workers: int, maker=_make_pool_image) -> list[bytes]:
     if workers <= 1:
-        return [_make_pool_image(i) for i in range(n)]
+        return [maker(i) for i in range(n)]
     with mp.get_context("spawn").Pool(workers) as p:
-        return p.map(_make_pool_image, range(n), chunksize=8)
+        return p.map(maker, range(n), chunksize=4)
 
 
 # ---------------------------------------------------------------- CPU baseline (reference ops)
-def _pil_pipeline(jpg: bytes):
-    """functional.py:94-110 + presets.py:716-733 op order: open/convert, crop, resize, to tensor."""
+def _pil_pipeline(jpg: bytes, res: int = 256, flip: bool = False, normalize: bool = False):
+    """functional.py:94-110 + presets.py:716-733 op order: open/convert, crop, resize, to tensor
+    (+ the user hflip of README.md:99-108, + NormalizeFramesTransform presets.py:154-162)."""
     import io
 
     import torch
     from PIL import Image
     img = Image.open(io.BytesIO(jpg)).convert("RGB")
     w, h = img.size
-    ar = 256 / 256
+    ar = res / res
     if w / h > ar:
         nw = int(h * ar)
         left = (w - nw) // 2
@@ -87,29 +97,34 @@ def _pil_pipeline(jpg: bytes):
         nh = int(w / ar)
         top = (h - nh) // 2
         img = img.crop((0, top, w, top + nh))
-    if img.size != (256, 256):
-        img = img.resize((256, 256), Image.BILINEAR)
-    return torch.from_numpy(np.array(img)).permute(2, 0, 1)
+    if img.size != (res, res):
+        img = img.resize((res, res), Image.BILINEAR)
+    x = torch.from_numpy(np.array(img)).permute(2, 0, 1)
+    if flip:
+        x = torch.flip(x, dims=[2])
+    if normalize:
+        x = x.float() / 127.5 - 1.0
+    return x
 
 
 def _cpu_worker(args):
-    jpgs, seconds = args
+    jpgs, seconds, res, mixed = args
     import torch
     torch.set_num_threads(1)
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        _pil_pipeline(jpgs[n % len(jpgs)])
+        _pil_pipeline(jpgs[n % len(jpgs)], res, flip=mixed and n % 2 == 1, normalize=mixed)
         n += 1
     return n, time.perf_counter() - t0
 
 
-def cpu_baseline(pool: list[bytes], procs: int, seconds: float) -> float:
+def cpu_baseline(pool: list[bytes], procs: int, seconds: float, res: int = 256, mixed: bool = False) -> float:
     if procs <= 1:
-        n, dt = _cpu_worker((pool, seconds))
+        n, dt = _cpu_worker((pool, seconds, res, mixed))
         return n / dt
     with mp.get_context("spawn").Pool(procs) as p:
-        res = p.map(_cpu_worker, [(pool[k::procs] or pool, seconds) for k in range(procs)])
-    return sum(n for n, _ in res) / max(dt for _, dt in res)
+        res_ = p.map(_cpu_worker, [(pool[k::procs] or pool, seconds, res, mixed) for k in range(procs)])
+    return sum(n for n, _ in res_) / max(dt for _, dt in res_)
 
 
 def host_cores() -> int:
@@ -125,14 +140,23 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--rows", type=int, default=100_000, help="rows resident per GPU")
-    ap.add_argument("--pool", type=int, default=1024, help="distinct encoded images")
-    ap.add_argument("--res", type=int, default=256)
+    ap.add_argument("--workload", choices=["vga256", "mixed512"], default="vga256",
+                    help="vga256 = configs[1] (the headline metric); mixed512 = configs[2]: VGA..4K -> centre crop + "
+                         "resize 512 + hflip(p=0.5) + CHW float normalise")
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--rows", type=int, default=None, help="rows resident per GPU")
+    ap.add_argument("--pool", type=int, default=None, help="distinct encoded images")
+    ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
     args = ap.parse_args()
+    mixed = args.workload == "mixed512"
+    defaults = {"batch": 512, "rows": 16384, "pool": 96, "res": 512} if mixed else \
+        {"batch": 4096, "rows": 100_000, "pool": 1024, "res": 256}
+    for k, v in defaults.items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
 
     import torch
     import torch.distributed as dist
@@ -150,7 +174,7 @@ def main():
     from sds_amd.engine import JpegEngine
 
     workers = max(1, min(16, host_cores()) // max(1, world))
-    pool = make_pool(args.pool, workers)
+    pool = make_pool(args.pool, workers, _make_mixed_image if mixed else _make_pool_image)
 
     # this rank's slice of the R*N-row index: row i holds pool image i % POOL.  The slice is laid
     # out as a repeated template of one pool period (16-byte aligned rows), tiled on the device, so
@@ -181,9 +205,15 @@ def main():
     torch.cuda.synchronize()
 
     B = args.batch
-    eng = JpegEngine(dev, max_batch=B, scratch_bytes=int(B * 3.2e6) + (256 << 20))
-    out = torch.empty((B, 3, args.res, args.res), dtype=torch.uint8, device=dev)
+    if mixed:  # per-image scratch grows with the pixel count (4K: ~30 MB)
+        scratch = int(B * 22e6) + (1 << 30)
+    else:
+        scratch = int(B * 3.2e6) + (256 << 20)
+    eng = JpegEngine(dev, max_batch=B, scratch_bytes=scratch)
+    out = torch.empty((B, 3, args.res, args.res), dtype=torch.float32 if mixed else torch.uint8, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
+    # hflip flags for every row, seeded (the user HorizontalFlipTransform, p = 0.5)
+    flips = torch.from_numpy((np.random.default_rng(99 + rank).random(nrows) < 0.5).astype(np.uint8)).to(dev)
     cursor = [0]
 
     def step():
@@ -191,7 +221,7 @@ def main():
         if s + B > nrows:
             s = 0
         eng.decode_resize_device(blob, d_offs[s:s + B], d_lens[s:s + B], (args.res, args.res), out=out,
-                                 status=status)
+                                 status=status, normalize=mixed, flip=flips[s:s + B] if mixed else None)
         cursor[0] = s + B
 
     # correctness gate before timing: the first batch's statuses are all OK
@@ -217,6 +247,9 @@ def main():
     t1 = time.perf_counter()
     barrier()
     stages = eng.stage_times()  # summed over the timed steps (HIP events on the launch stream)
+    n_bad = int((status != 0).sum().item())  # the last timed batch decoded completely as well
+    if n_bad:
+        raise SystemExit(f"rank {rank}: {n_bad} samples of the last timed batch failed to decode")
     eng.set_timing(False)
     elapsed = max_over_ranks(t1 - t0, device=dev)
     imgs = B * args.steps * world
@@ -225,7 +258,7 @@ def main():
         print(json.dumps({"stage_ms_per_step": {k: v / args.steps for k, v in stages.items()}}), file=sys.stderr)
 
     mean_in = float(np.mean(t_lens))
-    out_bytes = 3 * args.res * args.res
+    out_bytes = 3 * args.res * args.res * (4 if mixed else 1)
     alg_bytes_per_img = mean_in + out_bytes
     dom = max(stages, key=stages.get)
     dom_ms = stages[dom] / args.steps  # mean duration of the dominant kernel per launch (1 launch / step)
@@ -237,24 +270,32 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         procs = min(16, host_cores())
         sample = pool[:256]
-        v1 = cpu_baseline(sample, 1, args.cpu_seconds / 2)
-        vp = cpu_baseline(sample, procs, args.cpu_seconds)
+        v1 = cpu_baseline(sample, 1, args.cpu_seconds / 2, args.res, mixed)
+        vp = cpu_baseline(sample, procs, args.cpu_seconds, args.res, mixed)
         import platform
+        what = (f"centre crop, BILINEAR resize {args.res}x{args.res}, to CHW tensor, hflip every other image, "
+                f"x/127.5-1) over the {len(sample)} mixed VGA..4K pool JPEGs" if mixed else
+                f"centre crop, BILINEAR resize {args.res}x{args.res}, to CHW tensor) over 256 of the same 640x480 "
+                f"q90 JPEGs")
         cpu = {"value": round(vp, 1), "unit": "images/s", "cores": procs, "kind": "reference",
                "sample": f"PIL {__import__('PIL').__version__}/libjpeg-turbo pipeline (functional.py:94-110 op order: "
-                         f"open+convert RGB, centre crop, BILINEAR resize 256x256, to CHW tensor) over 256 of the "
-                         f"same 640x480 q90 JPEGs from host memory, {procs} processes x {args.cpu_seconds:.0f} s "
+                         f"open+convert RGB, {what} from host memory, {procs} processes x {args.cpu_seconds:.0f} s "
                          f"(single process: {v1:.1f} images/s)",
                "single_core_value": round(v1, 1), "host": platform.processor() or platform.machine()}
 
     if rank == 0:
+        workload = (f"configs[2]: synthetic mixed VGA..4K q90 4:2:0 baseline JPEGs resident in HBM -> centre crop + "
+                    f"bilinear resize {args.res}x{args.res} + hflip (p=0.5, seeded) + float32 CHW x/127.5-1"
+                    if mixed else
+                    "configs[1]: synthetic 640x480 q90 4:2:0 baseline JPEGs resident in HBM -> "
+                    f"centre crop + bilinear resize {args.res}x{args.res} uint8 CHW")
         line = {
-            "metric": "images/s device-resident JPEG decode+resize@256, 1/2/4/8 MI355X; %HBM roofline",
+            "metric": ("images/s device-resident JPEG decode+crop+resize@512+hflip+normalise (mixed VGA..4K)" if mixed
+                       else "images/s device-resident JPEG decode+resize@256, 1/2/4/8 MI355X; %HBM roofline"),
             "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "configs[1]: synthetic 640x480 q90 4:2:0 baseline JPEGs resident in HBM -> "
-                                   f"centre crop + bilinear resize {args.res}x{args.res} uint8 CHW",
+            "config": {"workload": workload,
                        "rows_per_gpu": nrows, "distinct_images": args.pool, "global_batch": B * world,
                        "mean_jpeg_bytes": round(mean_in, 1), "parallelism": f"index-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
