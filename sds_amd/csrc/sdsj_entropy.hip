@@ -148,6 +148,9 @@ __device__ int load_tables(EntTables& T, const ImgDesc* d, const ImgTables* tb) 
 // would also wait for every coefficient/record store issued since.)
 // ------------------------------------------------------------------------------------------
 constexpr int kQ = 8;
+constexpr int kSpecGroup = 4;   // symbols decoded between two wave-uniform refill checks (spec pass)
+constexpr int kWriteGroup = 4;  // (write pass)
+static_assert(kSpecGroup < kQ && kWriteGroup < kQ, "a fresh refill must pass the group check");
 
 struct Bits {
   const uint32_t* src;
@@ -345,33 +348,39 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
   while (__builtin_amdgcn_ballot_w64(run)) {
     if (run) bits_fill(b);
     for (;;) {
-      // leave to refill as soon as any running lane is dry
-      if (__builtin_amdgcn_ballot_w64(run && !bits_can(b)) || !__builtin_amdgcn_ballot_w64(run)) break;
-      if (run) {
-        int s, r, val;
-        const bool isdc = z == 0;
-        decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
-        nsym++;
-        dcd = isdc ? val : dcd;
-        add_dc(c, isdc && !warmup ? val : 0, d0, d1, d2);
-        if (next_z(z, s, r)) {
-          if (!warmup) {
-            if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
-            nrec++;
-            nblk++;
+      // kSpecGroup symbols per wave-uniform check: every running lane holds >= bits for them
+#pragma unroll
+      for (int u = 0; u < kSpecGroup; u++) {
+        if (run) {
+          int s, r, val;
+          const bool isdc = z == 0;
+          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+          nsym++;
+          dcd = isdc ? val : dcd;
+          add_dc(c, isdc && !warmup ? val : 0, d0, d1, d2);
+          if (next_z(z, s, r)) {
+            if (!warmup) {
+              if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
+              nrec++;
+              nblk++;
+            }
+            blk = blk + 1 == K.bpm ? 0 : blk + 1;
+            c = ctx_c(K, blk);
+            sdc = ctx_dc(K, blk);
+            sac = ctx_ac(K, blk);
+            if (warmup && b.pos >= start) {
+              warmup = false;
+              entry = b.pos;
+              entry_blk = blk;
+            }
           }
-          blk = blk + 1 == K.bpm ? 0 : blk + 1;
-          c = ctx_c(K, blk);
-          sdc = ctx_dc(K, blk);
-          sac = ctx_ac(K, blk);
-          if (warmup && b.pos >= start) {
-            warmup = false;
-            entry = b.pos;
-            entry_blk = blk;
-          }
+          run = warmup || b.pos < end || z != 0;
         }
-        run = warmup || b.pos < end || z != 0;
       }
+      // leave to refill when a running lane may not hold kSpecGroup more symbols (<= 32 bits each)
+      if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kSpecGroup + 1)) ||
+          !__builtin_amdgcn_ballot_w64(run))
+        break;
     }
   }
   S.entry_p = entry;
@@ -818,7 +827,8 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
     while (__builtin_amdgcn_ballot_w64(run)) {
       if (run) bits_fill(b);
       for (;;) {
-        if (__builtin_amdgcn_ballot_w64(run && !bits_can(b)) || !__builtin_amdgcn_ballot_w64(run)) break;
+#pragma unroll
+       for (int u = 0; u < kWriteGroup; u++) {
         witers++;
         bool ready = false;
         uint32_t gdone = 0;
@@ -871,6 +881,10 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_wave_barrier();
         }
+       }
+        if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kWriteGroup + 1)) ||
+            !__builtin_amdgcn_ballot_w64(run))
+          break;
       }
     }
     if (active && last_of_seg) {
