@@ -344,7 +344,50 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
   uint32_t entry = start;
   int entry_blk = 0;
   bool warmup = b.pos < start;
-  bool run = warmup || b.pos < end;
+  // warm-up: only the MCU position matters (no values, no records): code length + size per symbol
+  while (__builtin_amdgcn_ballot_w64(warmup)) {
+    if (warmup) bits_fill(b);
+    for (;;) {
+#pragma unroll
+      for (int u = 0; u < kSpecGroup; u++) {
+        if (warmup) {
+          bits_pull(b);
+          const bool isdc = z == 0;
+          const int slot = isdc ? sdc : sac;
+          const uint32_t hi = (uint32_t)(b.buf >> 32);
+          const uint32_t e = T.lut[(slot << LB) + (hi >> (32 - LB))];
+          int l = e & 15, sz = (e >> 4) & 15, r = (e >> 8) & 15;
+          if (l == 0) {
+            int s2, r2, v2;
+            decode_sym<LB>(T, b, slot, isdc, s2, r2, v2, bad);  // long code: the canonical search
+            sz = s2;
+            r = r2;
+          } else {
+            const int tot = l + sz;
+            b.buf <<= tot;
+            b.nb -= tot;
+            b.pos += tot;
+          }
+          nsym++;
+          if (next_z(z, sz, r)) {
+            blk = blk + 1 == K.bpm ? 0 : blk + 1;
+            sdc = ctx_dc(K, blk);
+            sac = ctx_ac(K, blk);
+            if (b.pos >= start) {
+              warmup = false;
+              entry = b.pos;
+              entry_blk = blk;
+              c = ctx_c(K, blk);
+            }
+          }
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(warmup && b.nb + 32 * b.nq < 32 * (kSpecGroup + 1)) ||
+          !__builtin_amdgcn_ballot_w64(warmup))
+        break;
+    }
+  }
+  bool run = b.pos < end || z != 0;
   while (__builtin_amdgcn_ballot_w64(run)) {
     if (run) bits_fill(b);
     for (;;) {
@@ -357,24 +400,17 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
           nsym++;
           dcd = isdc ? val : dcd;
-          add_dc(c, isdc && !warmup ? val : 0, d0, d1, d2);
+          add_dc(c, isdc ? val : 0, d0, d1, d2);
           if (next_z(z, s, r)) {
-            if (!warmup) {
-              if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
-              nrec++;
-              nblk++;
-            }
+            if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
+            nrec++;
+            nblk++;
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
             c = ctx_c(K, blk);
             sdc = ctx_dc(K, blk);
             sac = ctx_ac(K, blk);
-            if (warmup && b.pos >= start) {
-              warmup = false;
-              entry = b.pos;
-              entry_blk = blk;
-            }
           }
-          run = warmup || b.pos < end || z != 0;
+          run = b.pos < end || z != 0;
         }
       }
       // leave to refill when a running lane may not hold kSpecGroup more symbols (<= 32 bits each)
