@@ -189,6 +189,22 @@ SDSJ_HD inline SegView seg_view(uint8_t* base, int nseg) {
   return v;
 }
 
+// Work routes: k_plan sorts the batch's images into per-variant lists.  A variant kernel maps its
+// workgroups to its own list (the main variants: one workgroup column per entry, the surplus exits
+// at once; the rare unfused path: a small grid striding over its list), so no workgroup is spent
+// on an image another variant decodes.  Layout of the engine's route buffer (int32):
+// [counts (kRouteSlots)][kNumRoutes lists of cap entries].
+enum Route : int32_t {
+  kRtUnfused = 0,  // k_color -> k_hpass -> k_vpass
+  kRtGeneric,      // k_resample
+  kRt3, kRt5, kRt7, kRt9, kRt11,  // k_rs420<KT>
+  kRtEnt10, kRtEnt11,             // entropy kernels by lookahead width
+  kNumRoutes
+};
+constexpr int kRouteSlots = 16;  // counts [0, kNumRoutes), the rest zero
+SDSJ_HD inline const int32_t* route_list(const int32_t* routes, int cap, int r) { return routes + kRouteSlots + r * cap; }
+SDSJ_HD inline int rs_route(int kt) { return kRt3 + (kt - 3) / 2; }
+
 SDSJ_HD inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 SDSJ_HD inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 

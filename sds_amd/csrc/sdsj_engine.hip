@@ -35,6 +35,7 @@ struct sdsj_engine {
   ImgDesc* descs = nullptr;
   ImgTables* tables = nullptr;
   int64_t* d_total = nullptr;
+  int32_t* d_routes = nullptr;  // per-variant image lists built by k_plan (sdsj_common.h Route)
   float* d_lut = nullptr;
   // host-bytes path
   uint8_t* h_stage = nullptr;
@@ -145,26 +146,28 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
   mark(0);
   SDSJ_HIP(e, launch_parse(n, d_blob, d_offsets, d_lengths, op, e->warm_bits, e->descs, e->tables, s));
   mark(1);
-  SDSJ_HIP(e, launch_plan(n, e->descs, e->capacity, e->d_total, s));
+  const int cap = e->max_batch;
+  SDSJ_HIP(e, launch_plan(n, e->descs, e->capacity, e->d_total, e->d_routes, cap, s));
   mark(2);
   SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, e->descs, e->scratch, s));
   SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, e->descs, e->scratch, s));
   mark(3);
-  SDSJ_HIP(e, launch_entsync(n, e->descs, e->tables, e->scratch, s));
+  SDSJ_HIP(e, launch_entsync(n, e->descs, e->tables, e->scratch, e->d_routes, cap, s));
   mark(4);
-  SDSJ_HIP(e, launch_entwrite(n, e->descs, e->tables, e->scratch, s));
+  SDSJ_HIP(e, launch_entwrite(n, e->descs, e->tables, e->scratch, e->d_routes, cap, s));
   mark(5);
   SDSJ_HIP(e, launch_idct(n, e->descs, e->tables, e->scratch, s));
   mark(6);
-  SDSJ_HIP(e, launch_color(n, e->descs, e->scratch, s));
+  SDSJ_HIP(e, launch_color(n, e->descs, e->scratch, e->d_routes, cap, s));
   mark(7);
   SDSJ_HIP(e, launch_coeffs(n, e->descs, op, e->scratch, s));
   mark(8);
-  SDSJ_HIP(e, launch_hpass(n, e->descs, op, e->scratch, s));
+  SDSJ_HIP(e, launch_hpass(n, e->descs, op, e->scratch, e->d_routes, cap, s));
   mark(9);
-  SDSJ_HIP(e, launch_vpass(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_lut, s));
+  SDSJ_HIP(e, launch_vpass(n, e->descs, op, e->scratch, d_flip, d_out, e->d_routes, cap, e->d_lut, s));
   mark(10);
-  SDSJ_HIP(e, launch_resample(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_lut, s));
+  SDSJ_HIP(e, launch_resample(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_routes, cap, e->d_lut, s));
+  SDSJ_HIP(e, launch_finish(n, e->descs, op, d_out, d_status, e->d_lut, s));
   mark(11);
   return SDSJ_OK;
 }
@@ -226,6 +229,8 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   if (hipMalloc(&e->descs, sizeof(ImgDesc) * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->tables, sizeof(ImgTables) * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_total, sizeof(int64_t)) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMalloc(&e->d_routes, sizeof(int32_t) * (kRouteSlots + (size_t)kNumRoutes * e->max_batch)) != hipSuccess)
+    return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_lut, sizeof(float) * 256) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   {
     // presets.py:161 `x.float() / 127.5 - 1.0` in float32 (IEEE division then subtraction)
@@ -254,6 +259,7 @@ int sdsj_engine_destroy(sdsj_engine* e) {
   (void)hipFree(e->descs);
   (void)hipFree(e->tables);
   (void)hipFree(e->d_total);
+  (void)hipFree(e->d_routes);
   (void)hipFree(e->d_lut);
   (void)hipFree(e->d_blob);
   (void)hipFree(e->d_offsets);

@@ -552,11 +552,8 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
 }
 
 template <int LB>
-__global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(5))) k_entsync(int n, ImgDesc* __restrict__ descs,
-                                                         const ImgTables* __restrict__ tables,
-                                                         uint8_t* __restrict__ scratch) {
-  const int img = blockIdx.x;
-  if (img >= n) return;
+__device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
+                              uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
   __shared__ LdsSync L;
@@ -792,11 +789,8 @@ struct LdsWrite {
 };
 
 template <int LB>
-__global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __restrict__ descs,
-                                                          const ImgTables* __restrict__ tables,
-                                                          uint8_t* __restrict__ scratch) {
-  const int img = blockIdx.x;
-  if (img >= n) return;
+__device__ void entwrite_image(int img, ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
+                               uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
   __shared__ LdsWrite L;
@@ -939,15 +933,55 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(int n, ImgDesc* __rest
   }
 }
 
-hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
-  hipLaunchKernelGGL(k_entsync<11>, dim3(n), dim3(kEntThreads), 0, s, n, descs, tables, scratch);
-  hipLaunchKernelGGL(k_entsync<10>, dim3(n), dim3(kEntThreads), 0, s, n, descs, tables, scratch);
+// The entropy kernels take images from their route's list.  The main route (LB = 11) runs one
+// workgroup per list entry (grid = batch size, surplus workgroups exit at once); the rare LB = 10
+// route strides a small grid over its list.
+template <int LB, bool WRITE>
+__device__ __forceinline__ void ent_feed(ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes,
+                                         int cap) {
+  const int r = LB == 11 ? kRtEnt11 : kRtEnt10;
+  const int cnt = routes[r];
+  const int32_t* list = route_list(routes, cap, r);
+  if (LB == 11) {
+    if ((int)blockIdx.x >= cnt) return;
+    if (WRITE) entwrite_image<LB>(list[blockIdx.x], descs, tables, scratch);
+    else entsync_image<LB>(list[blockIdx.x], descs, tables, scratch);
+    return;
+  }
+  for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
+    if (WRITE) entwrite_image<LB>(list[li], descs, tables, scratch);
+    else entsync_image<LB>(list[li], descs, tables, scratch);
+    __syncthreads();  // LDS reuse by the next image
+  }
+}
+
+template <int LB>
+__global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(5)))
+k_entsync(ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables, uint8_t* __restrict__ scratch,
+          int32_t* __restrict__ routes, int cap) {
+  ent_feed<LB, false>(descs, tables, scratch, routes, cap);
+}
+
+template <int LB>
+__global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
+                                                          uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
+                                                          int cap) {
+  ent_feed<LB, true>(descs, tables, scratch, routes, cap);
+}
+
+hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes, int cap,
+                          hipStream_t s) {
+  const int g = n;  // one workgroup per image on the main route
+  hipLaunchKernelGGL(k_entsync<11>, dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL(k_entsync<10>, dim3(g < 256 ? g : 256), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 
-hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
-  hipLaunchKernelGGL(k_entwrite<11>, dim3(n), dim3(kEntThreads), 0, s, n, descs, tables, scratch);
-  hipLaunchKernelGGL(k_entwrite<10>, dim3(n), dim3(kEntThreads), 0, s, n, descs, tables, scratch);
+hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes, int cap,
+                           hipStream_t s) {
+  const int g = n;  // one workgroup per image on the main route
+  hipLaunchKernelGGL(k_entwrite<11>, dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL(k_entwrite<10>, dim3(g < 256 ? g : 256), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 

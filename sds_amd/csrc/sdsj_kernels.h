@@ -7,23 +7,29 @@
 namespace sdsj {
 hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, const int32_t* lengths, const sdsj_op& op,
                         int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s);
-hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, hipStream_t s);
+hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, int32_t* routes, int cap, hipStream_t s);
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
-hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
-hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
+hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes, int cap,
+                          hipStream_t s);
+hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes, int cap,
+                           hipStream_t s);
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
-hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, hipStream_t s);
+hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s);
 hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s);
-hipError_t launch_hpass(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s);
+hipError_t launch_hpass(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, const int32_t* routes, int cap,
+                        hipStream_t s);
 hipError_t launch_vpass(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
-                        void* out, int32_t* status, const float* lut, hipStream_t s);
+                        void* out, const int32_t* routes, int cap, const float* lut, hipStream_t s);
 hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
-                           void* out, int32_t* status, const float* lut, hipStream_t s);
+                           void* out, int32_t* status, const int32_t* routes, int cap, const float* lut, hipStream_t s);
 hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
-                              const uint8_t* flip, void* out, const float* lut, hipStream_t s);
+                              const uint8_t* flip, void* out, const int32_t* routes, int cap, const float* lut,
+                              hipStream_t s);
+hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
+                         hipStream_t s);
 // host-side planning (same code as k_parse): returns the scratch bytes image `jpg` needs, or < 0
 int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status);
 }  // namespace sdsj

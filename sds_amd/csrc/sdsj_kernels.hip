@@ -246,10 +246,12 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
 // k_plan: one workgroup; exclusive scan of per-image scratch needs -> absolute offsets.
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ descs, int64_t capacity,
-                                               int64_t* __restrict__ total_out) {
+                                               int64_t* __restrict__ total_out, int32_t* __restrict__ routes, int cap) {
   __shared__ int64_t part[1024];
   __shared__ int64_t carry;
+  __shared__ int rcnt[kNumRoutes];
   if (threadIdx.x == 0) carry = 0;
+  if (threadIdx.x < kNumRoutes) rcnt[threadIdx.x] = 0;
   __syncthreads();
   for (int base = 0; base < n; base += 1024) {
     int i = base + threadIdx.x;
@@ -279,6 +281,24 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         d.off_tmp += start;
         d.off_kh += start;
         d.off_kv += start;
+        // routes: entropy variant by the Huffman tables in use (slots as load_tables counts them),
+        // resample variant as plan_image chose it
+        int keys[2 * kMaxComp], ns = 0;
+        for (int c = 0; c < d.ncomp; c++)
+          for (int k = 0; k < 2; k++) {
+            const int key = k ? (4 | d.comp[c].ta) : d.comp[c].td;
+            bool seen = false;
+            for (int q = 0; q < ns; q++) seen |= keys[q] == key;
+            if (!seen) keys[ns++] = key;
+          }
+        const int re = ns <= 4 ? kRtEnt11 : kRtEnt10;
+        int32_t* lst = routes + kRouteSlots + re * cap;
+        lst[atomicAdd(&rcnt[re], 1)] = i;
+        if (d.geo != kGeoZeros) {
+          const int rr = !d.fused ? kRtUnfused : (d.rs_fast ? rs_route(d.rs_fast) : kRtGeneric);
+          lst = routes + kRouteSlots + rr * cap;
+          lst[atomicAdd(&rcnt[rr], 1)] = i;
+        }
       }
     }
     __syncthreads();
@@ -286,6 +306,30 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
     __syncthreads();
   }
   if (threadIdx.x == 0) *total_out = carry;
+  if (threadIdx.x < kNumRoutes) routes[threadIdx.x] = rcnt[threadIdx.x];
+  else if (threadIdx.x < kRouteSlots) routes[threadIdx.x] = 0;  // work counters
+}
+
+// k_finish: publishes every sample's status and writes the zeros of failed samples and of empty
+// crops (presets.py:160-162 normalise maps them to -1.0 through the LUT, as zeros would).
+__global__ void __launch_bounds__(256) k_finish(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+                                                void* __restrict__ out, int32_t* __restrict__ status,
+                                                const float* __restrict__ lut) {
+  const int img = blockIdx.x;
+  if (img >= n) return;
+  const ImgDesc* d = &descs[img];
+  const int st = d->status;
+  if (threadIdx.x == 0) status[img] = st;
+  if (st == SDSJ_OK && d->geo != kGeoZeros) return;
+  const int64_t plane = (int64_t)op.out_h * op.out_w, total = plane * 3;
+  if (op.out_dtype == SDSJ_DTYPE_F32) {
+    float* o = reinterpret_cast<float*>(out) + img * total;
+    const float z = lut[0];
+    for (int64_t i = threadIdx.x; i < total; i += blockDim.x) o[i] = z;
+  } else {
+    uint8_t* o = reinterpret_cast<uint8_t*>(out) + img * total;
+    for (int64_t i = threadIdx.x; i < total; i += blockDim.x) o[i] = 0;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -860,11 +904,13 @@ __device__ __forceinline__ void ycc_to_rgb(int y, int cb, int cr, uint32_t* r, u
   *b = clamp255(y + cb_b);
 }
 
-__global__ void __launch_bounds__(256) k_color(int n, const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch) {
-  const int img = blockIdx.y;
-  if (img >= n) return;
+__global__ void __launch_bounds__(256) k_color(int n, const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                               const int32_t* __restrict__ routes, int cap) {
+ const int32_t* rl = route_list(routes, cap, kRtUnfused);
+ for (int li = blockIdx.y; li < routes[kRtUnfused]; li += gridDim.y) {
+  const int img = rl[li];
   const ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK || d->geo == kGeoZeros || d->fused) return;
+  if (d->status != SDSJ_OK || d->geo == kGeoZeros || d->fused) continue;
   const int w = d->src_w, h = d->src_y1 - d->src_y0;
   const int64_t total = (int64_t)w * h;
   const uint8_t* planes = scratch + d->off_planes;
@@ -886,6 +932,7 @@ __global__ void __launch_bounds__(256) k_color(int n, const ImgDesc* __restrict_
     o[1] = (uint8_t)G;
     o[2] = (uint8_t)B;
   }
+ }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -978,11 +1025,12 @@ __device__ __forceinline__ uint32_t clip8(int32_t v) {
 // k_hpass: rows [yf, yl) of the crop, out_w columns; taps clamp to the crop window.
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_hpass(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
-                                               uint8_t* __restrict__ scratch) {
-  const int img = blockIdx.y;
-  if (img >= n) return;
+                                               uint8_t* __restrict__ scratch, const int32_t* __restrict__ routes, int cap) {
+ const int32_t* rl = route_list(routes, cap, kRtUnfused);
+ for (int li = blockIdx.y; li < routes[kRtUnfused]; li += gridDim.y) {
+  const int img = rl[li];
   const ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK || !d->need_h || d->fused) return;
+  if (d->status != SDSJ_OK || !d->need_h || d->fused) continue;
   const int rows = d->yl - d->yf, ow = op.out_w;
   const int64_t total = (int64_t)rows * ow;
   const int32_t* bounds = reinterpret_cast<const int32_t*>(scratch + d->off_kh);
@@ -1007,6 +1055,7 @@ __global__ void __launch_bounds__(256) k_hpass(int n, const ImgDesc* __restrict_
     o[1] = (uint8_t)clip8(s1);
     o[2] = (uint8_t)clip8(s2);
   }
+ }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1015,17 +1064,17 @@ __global__ void __launch_bounds__(256) k_hpass(int n, const ImgDesc* __restrict_
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_vpass(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
-                                               void* __restrict__ out, int32_t* __restrict__ status,
+                                               void* __restrict__ out, const int32_t* __restrict__ routes, int cap,
                                                const float* __restrict__ lut) {
-  const int img = blockIdx.y;
-  if (img >= n) return;
+ const int32_t* rl = route_list(routes, cap, kRtUnfused);
+ for (int li = blockIdx.y; li < routes[kRtUnfused]; li += gridDim.y) {
+  const int img = rl[li];
   const ImgDesc* d = &descs[img];
   const int oh = op.out_h, ow = op.out_w;
   const int64_t plane = (int64_t)oh * ow;
   const int64_t total = plane;
-  // failed / empty-crop / fused images are written (and their status published) by k_resample
-  if (d->status != SDSJ_OK || d->geo == kGeoZeros || d->fused) return;
-  (void)status;
+  // failed / empty-crop images are written (and every status published) by k_finish
+  if (d->status != SDSJ_OK || d->geo == kGeoZeros || d->fused) continue;
   const bool zeros = false;
   const bool fl = flip ? flip[img] != 0 : false;
   const bool f32 = op.out_dtype == SDSJ_DTYPE_F32;
@@ -1089,6 +1138,7 @@ __global__ void __launch_bounds__(256) k_vpass(int n, const ImgDesc* __restrict_
       }
     }
   }
+ }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1099,13 +1149,18 @@ hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, cons
   hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, offsets, lengths, op, warm_bits, descs, tables);
   return hipGetLastError();
 }
-hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, hipStream_t s) {
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, n, descs, capacity, total);
+hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, int32_t* routes, int cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, n, descs, capacity, total, routes, cap);
   return hipGetLastError();
 }
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s) {
   hipLaunchKernelGGL(k_unstuff, dim3(n), dim3(kUnstuffThreads), 0, s, n, blob, offsets, descs, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_finish, dim3(n), dim3(256), 0, s, n, descs, op, out, status, lut);
   return hipGetLastError();
 }
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
@@ -1117,8 +1172,8 @@ hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uin
   hipLaunchKernelGGL(k_idct, dim3(64, n), dim3(kIdctThreads), 0, s, n, descs, tables, scratch);
   return hipGetLastError();
 }
-hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, hipStream_t s) {
-  hipLaunchKernelGGL(k_color, dim3(64, n), dim3(256), 0, s, n, descs, scratch);
+hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_color, dim3(64, n < 64 ? n : 64), dim3(256), 0, s, n, descs, scratch, routes, cap);
   return hipGetLastError();
 }
 hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s) {
@@ -1126,13 +1181,14 @@ hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t
   hipLaunchKernelGGL(k_coeffs, dim3((mx + 255) / 256, n), dim3(256), 0, s, n, descs, op, scratch);
   return hipGetLastError();
 }
-hipError_t launch_hpass(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s) {
-  hipLaunchKernelGGL(k_hpass, dim3(32, n), dim3(256), 0, s, n, descs, op, scratch);
+hipError_t launch_hpass(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, const int32_t* routes, int cap,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_hpass, dim3(32, n < 64 ? n : 64), dim3(256), 0, s, n, descs, op, scratch, routes, cap);
   return hipGetLastError();
 }
 hipError_t launch_vpass(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
-                        void* out, int32_t* status, const float* lut, hipStream_t s) {
-  hipLaunchKernelGGL(k_vpass, dim3(32, n), dim3(256), 0, s, n, descs, op, scratch, flip, out, status, lut);
+                        void* out, const int32_t* routes, int cap, const float* lut, hipStream_t s) {
+  hipLaunchKernelGGL(k_vpass, dim3(32, n < 64 ? n : 64), dim3(256), 0, s, n, descs, op, scratch, flip, out, routes, cap, lut);
   return hipGetLastError();
 }
 

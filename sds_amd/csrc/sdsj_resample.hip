@@ -339,12 +339,11 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
     for (int k = 0; k < 3; k++) atomicAdd((unsigned long long*)&A.dmut->t_rs[k], (unsigned long long)tk[k]);
 }
 
-__global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
-                                                         int strip_h, const uint8_t* __restrict__ scratch,
-                                                         const uint8_t* __restrict__ flip, void* __restrict__ out,
-                                                         int32_t* __restrict__ status, const float* __restrict__ lut) {
-  const int img = blockIdx.x;
-  if (img >= n) return;
+// One image's share (output rows of strip blockIdx.y, column tiles from blockIdx.z) of the generic
+// fused colour + resample (route kRtGeneric; status and zero outputs: k_finish).
+__device__ void resample_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
+                               const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
+                               void* __restrict__ out, const float* __restrict__ lut) {
   const ImgDesc* d = &descs[img];
   const int t = threadIdx.x;
   RsArgs A;
@@ -357,18 +356,10 @@ __global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* _
   A.om.cs = op.layout == SDSJ_LAYOUT_HWC ? 1 : plane;
   A.lut = lut;
   A.out = out;
-  const int st = d->status;
-  if (blockIdx.y == 0 && blockIdx.z == 0 && t == 0) status[img] = st;
   A.oy0 = blockIdx.y * strip_h;
   if (A.oy0 >= A.oh) return;
   A.oy1 = A.oy0 + strip_h < A.oh ? A.oy0 + strip_h : A.oh;
-  if (st != SDSJ_OK || d->geo == kGeoZeros) {  // failed or empty crop: zeros (presets.py:160-162)
-    for (int oy = A.oy0; oy < A.oy1; oy++)
-      for (int xx = blockIdx.z * kRsThreads + t; xx < A.ow; xx += gridDim.z * kRsThreads)
-        put3(out, A.om, lut, (int64_t)oy * A.ow + xx, 0, 0, 0);
-    return;
-  }
-  if (!d->fused || d->rs_fast) return;  // unfused path / the specialised 4:2:0 kernel
+  if (d->status != SDSJ_OK) return;  // failed after planning: k_finish writes the zeros
   __shared__ LdsResample L;
   A.d = d;
   A.dmut = const_cast<ImgDesc*>(d);
@@ -411,17 +402,27 @@ __global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* _
   }
 }
 
+__global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+                                                         int strip_h, const uint8_t* __restrict__ scratch,
+                                                         const uint8_t* __restrict__ flip, void* __restrict__ out,
+                                                         const int32_t* __restrict__ routes, int cap,
+                                                         const float* __restrict__ lut) {
+  if ((int)blockIdx.x >= routes[kRtGeneric]) return;  // one workgroup column per list entry
+  resample_image(route_list(routes, cap, kRtGeneric)[blockIdx.x], descs, op, strip_h, scratch, flip, out, lut);
+}
+
 hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
-                           void* out, int32_t* status, const float* lut, hipStream_t s) {
+                           void* out, int32_t* status, const int32_t* routes, int cap, const float* lut, hipStream_t s) {
   // strips of output rows: tall for big batches (less window overlap), short for small ones
   const int strip_h = n >= 512 ? kMaxStrip : 16;
   const int tiles = (op.out_w + kRsThreads - 1) / kRsThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
   hipLaunchKernelGGL(k_resample, dim3(n, strips, tiles), dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip,
-                     out, status, lut);
+                     out, routes, cap, lut);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_resample420(n, descs, op, strip_h, scratch, flip, out, lut, s);
+  (void)status;  // published by k_finish after every resample variant
+  return launch_resample420(n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
 }
 
 }  // namespace sdsj

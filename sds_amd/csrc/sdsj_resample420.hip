@@ -60,12 +60,26 @@ __device__ __forceinline__ int htaps(const uint32_t* w, int hsh, const int32_t* 
 }
 
 template <int KT>
+__device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
+                            const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
+                            void* __restrict__ out, const float* __restrict__ lut);
+
+template <int KT>
 __global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                       int strip_h, const uint8_t* __restrict__ scratch,
                                                       const uint8_t* __restrict__ flip, void* __restrict__ out,
+                                                      const int32_t* __restrict__ routes, int cap,
                                                       const float* __restrict__ lut) {
-  const int img = blockIdx.x;
-  if (img >= n) return;
+  const int r = rs_route(KT);  // one workgroup column per list entry; the surplus exits at once
+  if ((int)blockIdx.x >= routes[r]) return;
+  rs420_image<KT>(route_list(routes, cap, r)[blockIdx.x], descs, op, strip_h, scratch, flip, out, lut);
+}
+
+// One image's share (strip blockIdx.y, column tiles from blockIdx.z) of the 4:2:0 fused resample.
+template <int KT>
+__device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
+                            const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
+                            void* __restrict__ out, const float* __restrict__ lut) {
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->rs_fast != KT) return;
   const int oh = op.out_h, ow = op.out_w;
@@ -284,15 +298,16 @@ __global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __res
 }
 
 hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
-                              const uint8_t* flip, void* out, const float* lut, hipStream_t s) {
+                              const uint8_t* flip, void* out, const int32_t* routes, int cap, const float* lut,
+                              hipStream_t s) {
   const int tiles = (op.out_w + kFThreads - 1) / kFThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
   const dim3 grid(n, strips, tiles);
-  hipLaunchKernelGGL(k_rs420<3>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
-  hipLaunchKernelGGL(k_rs420<5>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
-  hipLaunchKernelGGL(k_rs420<7>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
-  hipLaunchKernelGGL(k_rs420<9>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
-  hipLaunchKernelGGL(k_rs420<11>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, lut);
+  hipLaunchKernelGGL(k_rs420<3>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_rs420<5>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_rs420<7>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_rs420<9>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_rs420<11>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
   return hipGetLastError();
 }
 
