@@ -1,0 +1,115 @@
+"""Batched GPU decode on the consumer side of the DataLoader.
+
+The per-sample drop-in (``presets.create_standard_image_pipeline``) decodes inside whichever
+process iterates the dataset -- for sds that is a DataLoader worker (sds/dataset.py:352-381
+``_iter_chunks_``), so every worker holds its own HIP context and each call decodes one image.
+The batched path keeps the workers CPU-only and decodes a whole collated batch in one engine call
+on the training process's GPU:
+
+    ds = StreamingDataset(..., transforms=create_deferred_image_pipeline("jpg"))   # bytes only
+    loader = torch.utils.data.DataLoader(ds, batch_size=B, num_workers=W)            # default collate
+    decode = GpuDecodeBatch("jpg", (256, 256), device="cuda")
+    for batch in loader:              # or MultiStreamDataLoader's Batch (sds/dataloader.py:49-58)
+        batch = decode(batch)         # batch["image"]: [B', 3, 256, 256] on the GPU
+
+torch's default collate leaves ``bytes`` fields as a list, so ``batch[image_field]`` arrives as the
+B encoded images.  Values equal the per-sample pipeline's (presets.py:716-744) stacked the way
+default_collate stacks them.  A sample the reference would have failed on (its OSError makes
+``_iter_chunks_`` skip the sample, dataset.py:366-371) is dropped from every field of the batch
+(``on_error="drop"``), or raises (``"raise"``).
+"""
+from __future__ import annotations
+
+from typing import Any, Optional, Sequence
+
+import torch
+
+from . import functional as F
+from .engine import ImageDecodeError, UnsupportedImageError, get_engine, raise_for_status
+from .presets import LoadFromDiskTransform, SampleTransform
+
+
+def create_deferred_image_pipeline(image_field: str) -> Sequence[SampleTransform]:
+    """The CPU half of create_standard_image_pipeline (presets.py:716-744) for batched GPU decode:
+    ``LoadFromDiskTransform`` only (presets.py:613-626), so ``sample[image_field]`` holds the encoded
+    bytes when the sample reaches the collate function."""
+    return [LoadFromDiskTransform([image_field])]
+
+
+def _select(value: Any, keep: list[int], n: int) -> Any:
+    """The kept rows of one collated field (tensors along dim 0, lists/tuples by index)."""
+    if isinstance(value, torch.Tensor) and value.ndim > 0 and value.shape[0] == n:
+        return value[torch.as_tensor(keep, dtype=torch.long, device=value.device)]
+    if isinstance(value, list) and len(value) == n:
+        return [value[i] for i in keep]
+    if isinstance(value, tuple) and len(value) == n:
+        return tuple(value[i] for i in keep)
+    if isinstance(value, dict):
+        return {k: _select(v, keep, n) for k, v in value.items()}
+    return value
+
+
+class GpuDecodeBatch:
+    """Decodes ``batch[image_field]`` (a list of encoded images) into ``batch[output_field]`` =
+    ``[B, 3, H, W]`` on the GPU: uint8, or float32 ``x/127.5-1`` with ``normalize`` (presets.py:154-162).
+
+    ``resize_kwargs`` follow lean_resize_frames (functional.py:42-50) for a fixed target:
+    ``crop_before_resize`` and ``interpolation_mode``.  Per-sample target sizes (``random_resize``,
+    ``allow_vertical``) cannot be stacked into one tensor and are rejected, as default_collate
+    rejects the reference's differently sized tensors.  ``hflip_prob`` draws one
+    ``torch.rand(1) < p`` coin per sample in batch order (README.md:99-108 HorizontalFlipTransform).
+    ``return_image_as_single_frame_video`` mirrors presets.py:737-742 on the batch: ``video`` =
+    ``[B, 1, 3, H, W]``, ``image`` removed, ``framerate`` = 960.0 per sample (float64, as
+    default_collate stacks Python floats).
+    """
+
+    def __init__(self, image_field: str, resolution, output_field: str = "image", normalize: bool = False,
+                 resize_kwargs: Optional[dict] = None, device=None, hflip_prob: float = 0.0,
+                 on_error: str = "drop", return_image_as_single_frame_video: bool = False,
+                 video_output_field: str = "video"):
+        self.image_field = image_field
+        self.output_field = output_field
+        self.resolution = tuple(int(v) for v in resolution)
+        assert len(self.resolution) == 2, f"Wrong resolution: {resolution}"
+        self.normalize = bool(normalize)
+        self.resize_kwargs = dict(resize_kwargs or {})
+        F.check_resize_kwargs(self.resize_kwargs)
+        if self.resize_kwargs.get("allow_vertical") or self.resize_kwargs.get("random_resize") is not None:
+            raise ValueError("per-sample target sizes cannot be stacked into one batch; use the per-sample pipeline")
+        if on_error not in ("drop", "raise"):
+            raise ValueError(f"on_error must be 'drop' or 'raise', got {on_error!r}")
+        self.on_error = on_error
+        self.device = device
+        self.hflip_prob = float(hflip_prob)
+        self.as_video = bool(return_image_as_single_frame_video)
+        self.video_output_field = video_output_field
+
+    def __call__(self, batch: dict) -> dict:
+        assert self.image_field in batch, f"Field '{self.image_field}' not found in batch with keys {list(batch.keys())}."
+        encoded = batch[self.image_field]
+        if isinstance(encoded, (bytes, bytearray, memoryview)):
+            encoded = [encoded]
+        encoded = [bytes(e) for e in encoded]
+        n = len(encoded)
+        flip = [bool(torch.rand(1) < self.hflip_prob) for _ in range(n)] if self.hflip_prob > 0.0 else None
+        kw = self.resize_kwargs
+        images, status = get_engine(self.device).decode_resize(
+            encoded, self.resolution, crop_before_resize=kw.get("crop_before_resize", True),
+            filter=F.filter_name(kw.get("interpolation_mode", "bilinear")), normalize=self.normalize, flip=flip)
+        keep = [i for i in range(n) if int(status[i]) == 0]
+        if len(keep) < n:
+            if self.on_error == "raise":
+                bad = next(i for i in range(n) if int(status[i]) != 0)
+                raise_for_status(int(status[bad]), bad)
+            batch = {k: _select(v, keep, n) for k, v in batch.items()}
+            images = images[torch.as_tensor(keep, dtype=torch.long, device=images.device)]
+        if self.as_video:
+            batch.pop(self.output_field, None)
+            batch[self.video_output_field] = images.unsqueeze(1)
+            batch["framerate"] = torch.full((images.shape[0],), 960.0, dtype=torch.float64)
+        else:
+            batch[self.output_field] = images
+        return batch
+
+
+__all__ = ["GpuDecodeBatch", "create_deferred_image_pipeline", "ImageDecodeError", "UnsupportedImageError"]

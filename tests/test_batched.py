@@ -1,0 +1,123 @@
+"""Batched consumer-side decode (sds_amd/batched.py).
+
+CPU tests swap the GPU engine for a stand-in that returns the oracle's pixels, so the batch
+semantics are checked bit-exactly here: default_collate of deferred samples -> one decode call ->
+values equal to the per-sample pipeline stacked by default_collate; failed samples dropped from every
+field; the hflip coin drawn per sample in batch order; the single-frame-video branch.  The GPU test
+runs the real engine through the same path.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+from torch.utils.data import default_collate
+
+from oracle import oracle as O
+from tests import goldens as G
+
+
+class _StandInEngine:
+    def decode_resize(self, jpgs, resolution, crop_before_resize=True, filter="bilinear", normalize=False,
+                      flip=None, layout="chw", out=None):
+        outs, status = [], []
+        h, w = resolution
+        for k, j in enumerate(jpgs):
+            try:
+                outs.append(torch.from_numpy(O.pipeline(j, resolution, crop_before_resize=crop_before_resize,
+                                                        filter=filter, flip=bool(flip[k]) if flip else False,
+                                                        normalize=normalize)))
+                status.append(0)
+            except O.OracleError as e:
+                outs.append(torch.zeros((3, h, w), dtype=torch.float32 if normalize else torch.uint8))
+                status.append(e.status)
+        return torch.stack(outs), np.array(status, np.int32)
+
+
+def _samples(with_corrupt: bool):
+    meta, jpgs = G.g2_jpegs()
+    d = tempfile.mkdtemp()
+    paths = []
+    for i, j in enumerate(jpgs[:5]):
+        if with_corrupt and i == 2:
+            j = j[:len(j) // 2]  # truncated: PIL raises, the sample is skipped by sds
+        p = os.path.join(d, f"{i}.jpg")
+        with open(p, "wb") as f:
+            f.write(j)
+        paths.append(p)
+    return [{"index": i, "jpg": p, "caption": f"c{i}"} for i, p in enumerate(paths)]
+
+
+def _deferred_batch(samples):
+    from sds_amd.batched import create_deferred_image_pipeline
+    out = []
+    for s in samples:
+        for t in create_deferred_image_pipeline("jpg"):
+            s = t(dict(s))
+        out.append(s)
+    return default_collate(out)
+
+
+@pytest.fixture()
+def standin(monkeypatch):
+    import sds_amd.batched as B
+    monkeypatch.setattr(B, "get_engine", lambda device=None: _StandInEngine())
+
+
+def test_batch_equals_per_sample_pipeline_stacked(standin):
+    from sds_amd.batched import GpuDecodeBatch
+    samples = _samples(False)
+    batch = GpuDecodeBatch("jpg", (64, 96), normalize=True)(_deferred_batch(samples))
+    ref = default_collate([{"image": torch.from_numpy(O.pipeline(open(s["jpg"], "rb").read(), (64, 96),
+                                                                   normalize=True))} for s in samples])["image"]
+    assert list(batch.keys()) == ["index", "jpg", "caption", "image"]
+    assert batch["image"].dtype == torch.float32 and torch.equal(batch["image"], ref)
+    assert batch["index"].tolist() == [0, 1, 2, 3, 4]
+
+
+def test_failed_samples_are_dropped_from_every_field(standin):
+    from sds_amd.batched import GpuDecodeBatch
+    from sds_amd.engine import ImageDecodeError
+    batch = _deferred_batch(_samples(True))
+    out = GpuDecodeBatch("jpg", (32, 32))(dict(batch))
+    assert out["index"].tolist() == [0, 1, 3, 4]
+    assert out["caption"] == ["c0", "c1", "c3", "c4"] and len(out["jpg"]) == 4
+    assert out["image"].shape == (4, 3, 32, 32)
+    with pytest.raises(ImageDecodeError):
+        GpuDecodeBatch("jpg", (32, 32), on_error="raise")(dict(batch))
+
+
+def test_hflip_coins_in_batch_order_and_video_branch(standin):
+    from sds_amd.batched import GpuDecodeBatch
+    samples = _samples(False)
+    torch.manual_seed(3)
+    out = GpuDecodeBatch("jpg", (48, 48), hflip_prob=0.5, return_image_as_single_frame_video=True)(
+        _deferred_batch(samples))
+    torch.manual_seed(3)
+    flips = [bool(torch.rand(1) < 0.5) for _ in samples]
+    assert list(out.keys()) == ["index", "jpg", "caption", "video", "framerate"]
+    assert out["video"].shape == (5, 1, 3, 48, 48) and out["framerate"].tolist() == [960.0] * 5
+    for k, s in enumerate(samples):
+        base = torch.from_numpy(O.pipeline(open(s["jpg"], "rb").read(), (48, 48)))
+        assert torch.equal(out["video"][k, 0], torch.flip(base, dims=[2]) if flips[k] else base)
+
+
+def test_per_sample_target_sizes_are_rejected():
+    from sds_amd.batched import GpuDecodeBatch
+    with pytest.raises(ValueError):
+        GpuDecodeBatch("jpg", (64, 64), resize_kwargs={"allow_vertical": True})
+
+
+@pytest.mark.gpu
+def test_gpu_batch_matches_oracle():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sds_amd.batched import GpuDecodeBatch
+    samples = _samples(True)
+    out = GpuDecodeBatch("jpg", (256, 256), device="cuda:0")(_deferred_batch(samples))
+    assert out["index"].tolist() == [0, 1, 3, 4]
+    assert out["image"].is_cuda and out["image"].shape == (4, 3, 256, 256)
+    for k, i in enumerate([0, 1, 3, 4]):
+        ref = O.pipeline(open(samples[i]["jpg"], "rb").read(), (256, 256))
+        np.testing.assert_array_equal(out["image"][k].cpu().numpy(), ref)
