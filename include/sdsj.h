@@ -111,6 +111,16 @@ int sdsj_decode_resize_batch_device(sdsj_engine* eng, int n, const uint8_t* d_bl
                                     const int32_t* d_lengths, const sdsj_op* op, const uint8_t* d_flip,
                                     void* d_out, int32_t* d_status, void* hip_stream);
 
+/* Crop + resize (+flip, +normalise) of n raw RGB frames already in DEVICE memory -- the video path
+ * (sds/transforms/presets.py:121-135 ResizeVideoTransform + ConvertVideoToByteTensorTransform ->
+ * functional.py:42-86 lean_resize_frames on the frames PyAV decoded).  Frame i is uint8 HWC
+ * [height][width][3] at d_frames + i * frame_stride (frame_stride >= width * height * 3).  Same
+ * op, flip, output and status conventions as sdsj_decode_resize_batch_device.  Synchronises
+ * `hip_stream` between chunks of max_batch frames (host-planned descriptors are staged). */
+int sdsj_resize_frames_device(sdsj_engine* eng, int n, const uint8_t* d_frames, int32_t width, int32_t height,
+                              int64_t frame_stride, const sdsj_op* op, const uint8_t* d_flip, void* d_out,
+                              int32_t* d_status, void* hip_stream);
+
 /* Stage timing: sdsj_engine_set_timing(e, 1) starts (and restarts) accumulation; every chunk launched
  * afterwards records HIP events around each kernel on the caller's stream.  sdsj_engine_stage_times
  * waits for the last recorded chunk and returns, per stage, the summed device milliseconds. */

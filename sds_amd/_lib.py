@@ -31,7 +31,7 @@ LAYOUT_CHW, LAYOUT_HWC = 0, 1
 EXPORTS = [
     "sdsj_abi_version", "sdsj_probe", "sdsj_engine_create", "sdsj_engine_destroy", "sdsj_decode_resize_batch",
     "sdsj_decode_resize_batch_device", "sdsj_engine_set_timing", "sdsj_engine_stage_times", "sdsj_last_error",
-    "sdsj_stage_name", "sdsj_engine_debug_buffers",
+    "sdsj_stage_name", "sdsj_engine_debug_buffers", "sdsj_resize_frames_device",
 ]
 
 
@@ -85,6 +85,8 @@ def load() -> ctypes.CDLL:
                                                  ctypes.POINTER(i32), vp]
         lib.sdsj_decode_resize_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, ctypes.POINTER(SdsjOp), vp, vp,
                                                         vp, vp]
+        lib.sdsj_resize_frames_device.argtypes = [vp, ctypes.c_int, vp, i32, i32, i64, ctypes.POINTER(SdsjOp), vp, vp,
+                                                  vp, vp]
         lib.sdsj_engine_set_timing.argtypes = [vp, ctypes.c_int]
         lib.sdsj_engine_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_int)]

@@ -133,6 +133,8 @@ struct ImgDesc {
   // entropy-relative index of its last FF byte
   int32_t scan_end_code;
   int64_t scan_end_raw;
+  int32_t rgb_pitch;  // pixels per row of the RGB rows the unfused passes read (frames: the frame width)
+  int32_t pad2;
 };
 
 // Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).

@@ -36,6 +36,9 @@ struct sdsj_engine {
   ImgTables* tables = nullptr;
   int64_t* d_total = nullptr;
   int32_t* d_routes = nullptr;  // per-variant image lists built by k_plan (sdsj_common.h Route)
+  // frames path: host-planned descriptors and route list, staged through pinned memory
+  ImgDesc* h_fdescs = nullptr;
+  int32_t* h_froutes = nullptr;
   float* d_lut = nullptr;
   // host-bytes path
   uint8_t* h_stage = nullptr;
@@ -260,6 +263,8 @@ int sdsj_engine_destroy(sdsj_engine* e) {
   (void)hipFree(e->tables);
   (void)hipFree(e->d_total);
   (void)hipFree(e->d_routes);
+  (void)hipHostFree(e->h_fdescs);
+  (void)hipHostFree(e->h_froutes);
   (void)hipFree(e->d_lut);
   (void)hipFree(e->d_blob);
   (void)hipFree(e->d_offsets);
@@ -360,6 +365,66 @@ int sdsj_decode_resize_batch(sdsj_engine* e, int n, const uint8_t* const* jpg, c
     SDSJ_HIP(e, hipMemcpyAsync(e->h_status, e->d_status, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s));
     SDSJ_HIP(e, hipStreamSynchronize(s));
     memcpy(status + c0, e->h_status, sizeof(int32_t) * m);
+  }
+  return SDSJ_OK;
+}
+
+int sdsj_resize_frames_device(sdsj_engine* e, int n, const uint8_t* d_frames, int32_t width, int32_t height,
+                              int64_t frame_stride, const sdsj_op* op, const uint8_t* d_flip, void* d_out,
+                              int32_t* d_status, void* hip_stream) {
+  if (!e) return SDSJ_EINVAL;
+  if (n < 0 || (n > 0 && (!d_frames || !d_out || !d_status)) || !valid_op(op) || width <= 0 || height <= 0 ||
+      width > 65535 || height > 65535 || frame_stride < (int64_t)width * height * 3)
+    return fail(e, SDSJ_EINVAL, "invalid argument");
+  if (n == 0) return SDSJ_OK;
+  DeviceGuard g(e->device);
+  hipStream_t s = reinterpret_cast<hipStream_t>(hip_stream);
+  ImgDesc base;
+  const int64_t need = align_up(host_plan_frame(&base, width, height, *op), 256);
+  const int cap = e->max_batch;
+  if (!e->h_fdescs) {
+    SDSJ_HIP(e, hipHostMalloc(&e->h_fdescs, sizeof(ImgDesc) * cap));
+    SDSJ_HIP(e, hipHostMalloc(&e->h_froutes, sizeof(int32_t) * (kRouteSlots + cap)));
+  }
+  const int64_t ob = out_bytes_per_image(*op);
+  for (int c0 = 0; c0 < n; c0 += cap) {
+    const int m = std::min(cap, n - c0);
+    if (!e->scratch || need * m > e->capacity) {
+      if (e->scratch && !e->grow) return fail(e, SDSJ_ECAPACITY, "frames exceed the configured scratch capacity");
+      SDSJ_HIP(e, hipStreamSynchronize(s));
+      int rc = ensure_scratch(e, std::max<int64_t>(need * m, (int64_t)256 << 20));
+      if (rc != SDSJ_OK) return rc;
+    }
+    SDSJ_HIP(e, hipStreamSynchronize(s));  // the pinned staging is reused chunk to chunk
+    for (int k = 0; k < m; k++) {
+      ImgDesc& d = e->h_fdescs[k];
+      d = base;
+      const int64_t o = need * k;
+      d.off_ustream += o;
+      d.off_seg += o;
+      d.off_sub += o;
+      d.off_rec += o;
+      d.off_coef += o;
+      d.off_planes += o;
+      d.off_tmp += o;
+      d.off_kh += o;
+      d.off_kv += o;
+      // the passes read the frame's crop rows in place: scratch + off_rgb = the crop's first pixel
+      const uint8_t* px = d_frames + (int64_t)(c0 + k) * frame_stride + ((int64_t)d.src_y0 * width + d.src_x0) * 3;
+      d.off_rgb = (int64_t)(px - e->scratch);
+      d.rgb_pitch = width;
+    }
+    for (int r = 0; r < kRouteSlots; r++) e->h_froutes[r] = 0;
+    e->h_froutes[kRtUnfused] = m;
+    for (int k = 0; k < m; k++) e->h_froutes[kRouteSlots + kRtUnfused * cap + k] = k;
+    SDSJ_HIP(e, hipMemcpyAsync(e->descs, e->h_fdescs, sizeof(ImgDesc) * m, hipMemcpyHostToDevice, s));
+    SDSJ_HIP(e, hipMemcpyAsync(e->d_routes, e->h_froutes, sizeof(int32_t) * (kRouteSlots + m), hipMemcpyHostToDevice, s));
+    void* out = reinterpret_cast<uint8_t*>(d_out) + c0 * ob;
+    const uint8_t* flip = d_flip ? d_flip + c0 : nullptr;
+    SDSJ_HIP(e, launch_coeffs(m, e->descs, *op, e->scratch, s));
+    SDSJ_HIP(e, launch_hpass(m, e->descs, *op, e->scratch, e->d_routes, cap, s));
+    SDSJ_HIP(e, launch_vpass(m, e->descs, *op, e->scratch, flip, out, e->d_routes, cap, e->d_lut, s));
+    SDSJ_HIP(e, launch_finish(m, e->descs, *op, out, d_status + c0, e->d_lut, s));
   }
   return SDSJ_OK;
 }

@@ -32,4 +32,6 @@ hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* o
                          hipStream_t s);
 // host-side planning (same code as k_parse): returns the scratch bytes image `jpg` needs, or < 0
 int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status);
+// host-side planning of one raw RGB frame (width x height) for the unfused passes; returns scratch bytes
+int64_t host_plan_frame(ImgDesc* d, int width, int height, const sdsj_op& op);
 }  // namespace sdsj

@@ -52,7 +52,9 @@ __device__ __host__ inline void resample_bounds(int in_size, int out_size, doubl
   *xmax_out = xmax - xmin;
 }
 
-__device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
+// frames = true: raw RGB frames (sdsj_resize_frames_device): the unfused passes read the frame rows
+// in place (off_rgb / rgb_pitch are set by the caller), no entropy / plane / RGB-row scratch.
+__device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, bool frames = false) {
   // Geometry: functional.py:78-80 shortcut, :118-147 crop, Pillow ImagingResampleInner.
   const int W = d->width, H = d->height;
   if (W == op.out_w && H == op.out_h) {
@@ -113,6 +115,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
       tw = (tw + 1) / 2;
     }
   }
+  if (frames) d->fused = 0;
   // specialised fused kernel: 4:2:0 (h2v2 fancy chroma), horizontal and vertical passes, odd tap
   // counts 3..11 (sdsj_resample420.hip); everything else takes the generic k_resample
   d->rs_fast = 0;
@@ -141,7 +144,8 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op) {
   int64_t planes = 0;
   for (int c = 0; c < d->ncomp; c++) planes += align_up((int64_t)d->comp[c].pitch * d->comp[c].bh * 8, 256);
   d->off_planes = take(planes);
-  d->off_rgb = take(d->fused ? 0 : (int64_t)d->src_w * (d->src_y1 - d->src_y0) * 3);
+  d->off_rgb = take(d->fused || frames ? 0 : (int64_t)d->src_w * (d->src_y1 - d->src_y0) * 3);
+  d->rgb_pitch = d->src_w;  // k_color packs the crop rows
   d->off_tmp = take(!d->fused && d->need_h ? (int64_t)(d->yl - d->yf) * op.out_w * 3 : 0);
   d->off_kh = take(d->need_h ? ((int64_t)2 * op.out_w + (int64_t)op.out_w * d->ksh) * 4 : 0);
   d->off_kv = take(d->need_v ? ((int64_t)2 * op.out_h + (int64_t)op.out_h * d->ksv) * 4 : 0);
@@ -1037,7 +1041,7 @@ __global__ void __launch_bounds__(256) k_hpass(int n, const ImgDesc* __restrict_
   const int32_t* kk = bounds + 2 * ow;
   const uint8_t* rgb = scratch + d->off_rgb;
   uint8_t* tmp = scratch + d->off_tmp;
-  const int sw = d->src_w, ks = d->ksh;
+  const int sw = d->rgb_pitch, ks = d->ksh;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int yy = (int)(i / ow), xx = (int)(i - (int64_t)yy * ow);
     const int xmin = bounds[2 * xx], xmax = bounds[2 * xx + 1];
@@ -1083,7 +1087,7 @@ __global__ void __launch_bounds__(256) k_vpass(int n, const ImgDesc* __restrict_
   float* of = reinterpret_cast<float*>(out) + (f32 ? img * plane * 3 : 0);
   // source: H-pass output (need_h) or the materialised RGB rows (crop columns)
   const uint8_t* src = zeros ? nullptr : (d->need_h ? scratch + d->off_tmp : scratch + d->off_rgb);
-  const int sw = d->need_h ? ow : d->src_w;
+  const int sw = d->need_h ? ow : d->rgb_pitch;
   const int32_t* bounds = d->need_v ? reinterpret_cast<const int32_t*>(scratch + d->off_kv) : nullptr;
   const int32_t* kk = bounds ? bounds + 2 * oh : nullptr;
   const int ks = d->ksv, yf = d->yf;
@@ -1199,6 +1203,15 @@ struct HostReader {
   const uint8_t* p;
   int operator()(int64_t i) const { return p[i]; }
 };
+
+int64_t host_plan_frame(ImgDesc* d, int width, int height, const sdsj_op& op) {
+  *d = ImgDesc{};
+  d->status = SDSJ_OK;
+  d->width = width;
+  d->height = height;
+  d->ncomp = 3;
+  return plan_image(d, op, true);
+}
 
 int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status) {
   ImgDesc d;

@@ -158,6 +158,34 @@ class JpegEngine:
         self._check(rc, "sdsj_decode_resize_batch_device")
         return out, status
 
+    # -- raw RGB frames (video) --------------------------------------------------------------
+    def resize_frames(self, frames: torch.Tensor, resolution, *, crop_before_resize: bool = True,
+                      filter: str = "bilinear", normalize: bool = False, flip: Optional[torch.Tensor] = None,
+                      layout: str = "chw", out: Optional[torch.Tensor] = None) -> tuple[torch.Tensor, torch.Tensor]:
+        """Crop + resize of uint8 RGB frames [T, H, W, 3] in device memory (lean_resize_frames on PIL
+        frames, functional.py:42-86, then the byte-tensor conversion, presets.py:129-135).
+        Returns ([T, 3, h, w] (or [T, h, w, 3]) device tensor, device int32 status per frame)."""
+        if frames.dim() != 4 or frames.shape[-1] != 3 or frames.dtype != torch.uint8 or frames.device.type != "cuda":
+            raise ValueError("frames must be a cuda uint8 tensor [T, H, W, 3]")
+        frames = frames.contiguous()
+        op = self.make_op(resolution, crop_before_resize, filter, normalize, layout)
+        t, h, w = int(frames.shape[0]), int(frames.shape[1]), int(frames.shape[2])
+        if out is None:
+            out = self._alloc_out(t, op)
+        status = torch.empty(t, dtype=torch.int32, device=f"cuda:{self.device}")
+        if flip is not None:
+            flip = torch.as_tensor(flip, dtype=torch.uint8, device=f"cuda:{self.device}").contiguous()
+        if t == 0:
+            return out, status
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = self.lib.sdsj_resize_frames_device(
+                self._h, t, ctypes.c_void_p(frames.data_ptr()), w, h, h * w * 3, ctypes.byref(op),
+                ctypes.c_void_p(flip.data_ptr()) if flip is not None else None, ctypes.c_void_p(out.data_ptr()),
+                ctypes.c_void_p(status.data_ptr()), ctypes.c_void_p(stream))
+        self._check(rc, "sdsj_resize_frames_device")
+        return out, status
+
     # -- diagnostics -----------------------------------------------------------------------
     def set_timing(self, enable: bool) -> None:
         self.lib.sdsj_engine_set_timing(self._h, int(bool(enable)))

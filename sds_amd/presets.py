@@ -136,6 +136,63 @@ class GpuDecodeResizeImageTransform(BaseTransform):
         return sample
 
 
+def _frames_to_device(frames, device) -> torch.Tensor:
+    """PIL frames / HWC uint8 arrays / a uint8 [T, H, W, 3] tensor -> contiguous uint8 [T, H, W, 3] on the GPU."""
+    if isinstance(frames, torch.Tensor):
+        if frames.dim() != 4 or frames.shape[-1] != 3 or frames.dtype != torch.uint8:
+            raise NotImplementedError("tensor frames must be uint8 [T, H, W, 3]; the reference resizes CHW tensors "
+                                      "with torchvision's tensor kernels, which this path does not restate")
+        return frames.to(device, non_blocking=True).contiguous()
+    arrs = []
+    for f in frames:
+        if isinstance(f, torch.Tensor):
+            raise NotImplementedError("per-frame tensors take torchvision's tensor resize in the reference; "
+                                      "pass PIL frames or HWC uint8 arrays")
+        a = np.asarray(f.convert("RGB") if hasattr(f, "convert") else f)
+        if a.dtype != np.uint8 or a.ndim != 3 or a.shape[2] != 3:
+            raise ValueError(f"frames must be RGB uint8 HWC, got {a.dtype} {a.shape}")
+        arrs.append(a)
+    host = torch.from_numpy(np.stack(arrs)).pin_memory() if torch.cuda.is_available() else torch.from_numpy(np.stack(arrs))
+    return host.to(device, non_blocking=True)
+
+
+class GpuResizeVideoTransform(BaseTransform):
+    """Fused ResizeVideoTransform + ConvertVideoToByteTensorTransform (+ NormalizeFramesTransform)
+    (presets.py:121-135, :154-162) on the GPU: ``sample[input_field]`` = the decoded frames (PIL images,
+    as PyAV's ``to_image`` gives them, or HWC uint8 arrays, or a uint8 [T, H, W, 3] tensor) ->
+    ``sample[output_field]`` = device tensor [T, 3, h, w], uint8 (or float32 ``x/127.5-1``).
+    ``transform_kwargs`` are lean_resize_frames's (functional.py:42-50): ``resolution``,
+    ``crop_before_resize``, ``allow_vertical``, ``random_resize`` (one draw per video, np global RNG),
+    ``interpolation_mode``; the same-size shortcut (functional.py:78-80) holds."""
+
+    def __init__(self, input_field: str, output_field: Optional[str] = None, normalize: bool = False, device=None,
+                 **transform_kwargs):
+        super().__init__(input_field, output_field, **transform_kwargs)
+        assert "resolution" in transform_kwargs, "lean_resize_frames needs a resolution"
+        self.normalize = bool(normalize)
+        self.device = device
+        kw = dict(transform_kwargs)
+        kw.pop("resolution")
+        F.check_resize_kwargs(kw)
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        _validate_fields(sample, present=[self.input_field], absent=[])
+        kw = dict(self.transform_kwargs)
+        eng = get_engine(self.device)
+        frames = _frames_to_device(sample[self.input_field], torch.device("cuda", eng.device))
+        t, h, w = int(frames.shape[0]), int(frames.shape[1]), int(frames.shape[2])
+        resolution = F.target_resolution(w, h, kw["resolution"], kw.get("allow_vertical", False),
+                                         kw.get("random_resize"))
+        out, status = eng.resize_frames(frames, resolution, crop_before_resize=kw.get("crop_before_resize", True),
+                                        filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),
+                                        normalize=self.normalize)
+        bad = torch.nonzero(status != 0)
+        if bad.numel():
+            raise_for_status(int(status[int(bad[0])]), int(bad[0]))
+        sample[self.output_field] = out
+        return sample
+
+
 class ReshapeImageAsVideoTransform(BaseTransform):
     """presets.py:60-66 -> functional.py:88-92."""
 

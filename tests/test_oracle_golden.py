@@ -84,3 +84,19 @@ def test_oracle_status_matches_pil_on_mutated_streams(seed):
         assert (ref is None) == (got is None), f"sample {i}"
         if ref is not None and i % 5 in (3, 4):
             np.testing.assert_array_equal(got, ref, err_msg=f"sample {i}")
+
+
+@pytest.mark.parametrize("size,res,filt", [((97, 61), (64, 80), "bilinear"), ((640, 360), (256, 256), "bilinear"),
+                                           ((320, 240), (512, 512), "bilinear"), ((200, 150), (100, 60), "bicubic"),
+                                           ((64, 48), (48, 64), "lanczos"), ((50, 40), (17, 9), "box")])
+def test_oracle_resize_matches_pil_on_raw_frames(size, res, filt):
+    """The frame path's arithmetic (lean_resize_frames on PIL frames, functional.py:42-86) pinned directly
+    against Pillow, independent of JPEG decoding: crop_to_aspect_ratio then Image.resize."""
+    Image = pytest.importorskip("PIL.Image")
+    from tests.golden.synth import synth_rgb
+    w, h = size
+    out_h, out_w = res
+    rgb = synth_rgb(np.random.default_rng(w * h), w, h)
+    l, t, r, b = O.crop_box(w, h, out_h, out_w)
+    img = Image.fromarray(rgb).crop((l, t, r, b)).resize((out_w, out_h), getattr(Image, filt.upper()))
+    np.testing.assert_array_equal(O.resize(np.ascontiguousarray(rgb[t:b, l:r]), out_h, out_w, filt), np.asarray(img))
