@@ -664,6 +664,10 @@ __global__ void __launch_bounds__(64) k_scanmap(int n, const uint8_t* __restrict
 // ------------------------------------------------------------------------------------------
 constexpr int kIdctThreads = 256;
 constexpr int kIdctBlocks = kIdctThreads / 8;
+#ifndef SDSJ_IDCT_GRID
+#define SDSJ_IDCT_GRID 8
+#endif
+constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides over 8-block groups)
 constexpr int kWsStride = 72;  // ints per block in LDS (conflict-free column reads per half-wave)
 
 #define SDSJ_FIX_0_298631336 2446
@@ -749,6 +753,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   __shared__ int32_t qt[kMaxComp][64];
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
   __shared__ int32_t gstart[kMaxComp + 1], ngx[kMaxComp], cbw[kMaxComp], ch_[kMaxComp], cv_[kMaxComp], cpitch[kMaxComp];
+  __shared__ float rngx[kMaxComp], rch[kMaxComp], rcv[kMaxComp];  // reciprocals for the exact quotients below
   __shared__ int64_t cplane[kMaxComp];
   const int t = threadIdx.x;
   const int ncomp = d->ncomp, bpm = d->bpm, mcux = d->mcux;
@@ -765,6 +770,9 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
       cv_[c] = ncomp == 1 ? 1 : cd.v;
       cpitch[c] = cd.pitch;
       cplane[c] = cd.plane_off;
+      rngx[c] = 1.0f / (float)ngx[c];
+      rch[c] = 1.0f / (float)ch_[c];
+      rcv[c] = 1.0f / (float)cv_[c];
       acc += ngx[c] * cd.bh;
     }
     gstart[ncomp] = acc;
@@ -787,15 +795,22 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
     return g >= sv.vend[k] || (k > 0 && (sv.flag[k] & kSegEmpty) && (sv.flag[k - 1] & kSegIns));
   };
   // block of this lane in group grp: component, block coordinates, decode-order index
+  // a / b for 0 <= a < 2^22, 1 <= b: float estimate, then one correction each way (exact)
+  auto qdiv = [](int a, int b, float rb) {
+    int q = (int)((float)a * rb);
+    q -= q * b > a ? 1 : 0;
+    q += (q + 1) * b <= a ? 1 : 0;
+    return q;
+  };
   auto locate = [&](int grp, int& c, int& by, int& bx, int& g) {
     c = ncomp > 1 && grp >= gstart[1] ? (ncomp > 2 && grp >= gstart[2] ? 2 : 1) : 0;
     const int local = grp - gstart[c];
-    by = local / ngx[c];
+    by = qdiv(local, ngx[c], rngx[c]);
     bx = (local - by * ngx[c]) * 8 + lb;
     g = -1;
     if (grp < ngroups && bx < cbw[c]) {
       const int h = ch_[c], v = cv_[c];
-      const int mx = bx / h, my = by / v;
+      const int mx = qdiv(bx, h, rch[c]), my = qdiv(by, v, rcv[c]);
       g = (my * mcux + mx) * bpm + binv[c][(by - my * v) * 4 + (bx - mx * h)];
     }
   };
@@ -1173,7 +1188,7 @@ hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, Im
   return hipGetLastError();
 }
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
-  hipLaunchKernelGGL(k_idct, dim3(64, n), dim3(kIdctThreads), 0, s, n, descs, tables, scratch);
+  hipLaunchKernelGGL(k_idct, dim3(kIdctGrid, n), dim3(kIdctThreads), 0, s, n, descs, tables, scratch);
   return hipGetLastError();
 }
 hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s) {
