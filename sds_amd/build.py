@@ -47,7 +47,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+           "-ffp-contract=off", "-Wl,-z,defs", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
            "-I", os.path.join(REPO, "include"), "-o", tmp] + sources()
     if verbose:
         print(" ".join(cmd))

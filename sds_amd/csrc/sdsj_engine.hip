@@ -35,6 +35,7 @@ struct sdsj_engine {
   ImgDesc* descs = nullptr;
   ImgTables* tables = nullptr;
   int64_t* d_total = nullptr;
+  void* d_etab = nullptr;       // per-image decode tables built by k_enttab
   int32_t* d_routes = nullptr;  // per-variant image lists built by k_plan (sdsj_common.h Route)
   // frames path: host-planned descriptors and route list, staged through pinned memory
   ImgDesc* h_fdescs = nullptr;
@@ -155,9 +156,9 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
   SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, e->descs, e->scratch, s));
   SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, e->descs, e->scratch, s));
   mark(3);
-  SDSJ_HIP(e, launch_entsync(n, e->descs, e->tables, e->scratch, e->d_routes, cap, s));
+  SDSJ_HIP(e, launch_entsync(n, e->descs, e->tables, e->d_etab, e->scratch, e->d_routes, cap, s));
   mark(4);
-  SDSJ_HIP(e, launch_entwrite(n, e->descs, e->tables, e->scratch, e->d_routes, cap, s));
+  SDSJ_HIP(e, launch_entwrite(n, e->descs, e->d_etab, e->scratch, e->d_routes, cap, s));
   mark(5);
   SDSJ_HIP(e, launch_idct(n, e->descs, e->tables, e->scratch, s));
   mark(6);
@@ -232,6 +233,7 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   if (hipMalloc(&e->descs, sizeof(ImgDesc) * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->tables, sizeof(ImgTables) * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_total, sizeof(int64_t)) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMalloc(&e->d_etab, enttab_bytes() * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_routes, sizeof(int32_t) * (kRouteSlots + (size_t)kNumRoutes * e->max_batch)) != hipSuccess)
     return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_lut, sizeof(float) * 256) != hipSuccess) return cleanup(SDSJ_ENOMEM);
@@ -263,6 +265,7 @@ int sdsj_engine_destroy(sdsj_engine* e) {
   (void)hipFree(e->tables);
   (void)hipFree(e->d_total);
   (void)hipFree(e->d_routes);
+  (void)hipFree(e->d_etab);
   (void)hipHostFree(e->h_fdescs);
   (void)hipHostFree(e->h_froutes);
   (void)hipFree(e->d_lut);

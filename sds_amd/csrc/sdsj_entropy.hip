@@ -39,6 +39,9 @@ constexpr int kLutEntries = 1 << 13;  // LDS lookup capacity: 4 tables x 2^11 or
 constexpr int kStageStride = 64;      // int16 per lane staging block (one 128-byte block)
 constexpr int kBudget0 = 64;          // first sync stage's symbol budget
 constexpr int kMaxTasks = kEntThreads;  // per round (more: picked up by the next round)
+// k_entsync is latency-bound (a few serial re-decodes per image): one wave per image keeps more
+// images in flight per CU than a 4-wave workgroup would (the LDS tables bound both)
+constexpr int kSyncThreads = 64;
 constexpr int kMaxSlots = 2 * kMaxComp;  // a DC and an AC table per component at most
 
 // ------------------------------------------------------------------------------------------
@@ -53,7 +56,9 @@ struct EntTables {
   int32_t slot_src[kMaxSlots];  // (kind << 2) | id of the table in each slot (kind 0 = DC, 1 = AC)
   int32_t nslots;
   uint32_t pk_dc[2], pk_ac[2], pk_c;  // per MCU block: DC slot, AC slot (4 bits each), component (2)
+  uint32_t pad[4];
 };
+static_assert(sizeof(EntTables) % 16 == 0, "EntTables is copied in 16-byte units");
 
 // Is this image decoded by the LB variant?  (LB = 11 when its tables fit 4 slots, else LB = 10.)
 template <int LB>
@@ -61,8 +66,16 @@ __device__ __forceinline__ bool variant_owns(int ns) {
   return LB == 11 ? (ns << 11) <= kLutEntries : (ns << 11) > kLutEntries && (ns << 10) <= kLutEntries;
 }
 
-template <int LB>
-__device__ int load_tables(EntTables& T, const ImgDesc* d, const ImgTables* tb) {
+// k_enttab: one workgroup per image builds its decode tables once into HBM; every entropy kernel
+// then copies the image's EntTables into LDS with 16-byte loads (one round trip) instead of
+// rebuilding them.
+__global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restrict__ descs,
+                                                       const ImgTables* __restrict__ tables, EntTables* __restrict__ out) {
+  const ImgDesc* d = &descs[blockIdx.x];
+  if (d->status != SDSJ_OK) return;
+  const ImgTables* tb = &tables[blockIdx.x];
+  __shared__ EntTables T;
+  __shared__ int32_t lim[kMaxSlots][12];
   const int t = threadIdx.x;
   if (t == 0) {
     int ns = 0;
@@ -91,12 +104,15 @@ __device__ int load_tables(EntTables& T, const ImgDesc* d, const ImgTables* tb) 
     T.pk_ac[0] = (uint32_t)pac;
     T.pk_ac[1] = (uint32_t)(pac >> 32);
     T.pk_c = pc;
+    T.pad[0] = T.pad[1] = T.pad[2] = T.pad[3] = 0;
   }
-  if (t < 80) T.nat[t] = (uint8_t)natural_order(t);
+  for (int i = t; i < 80; i += kEntThreads) T.nat[i] = (uint8_t)natural_order(i);
   __syncthreads();
   const int ns = T.nslots;
-  if (!variant_owns<LB>(ns)) return ns;
-  // canonical code bounds per slot (jdhuff.c jpeg_make_d_derived_tbl: maxcode / valoffset)
+  const int lb = (ns << 11) <= kLutEntries ? 11 : 10;  // the variant that will decode this image
+  // canonical code bounds per slot (jdhuff.c jpeg_make_d_derived_tbl: maxcode / valoffset), and
+  // lim[l] = (end of the length-l codes) << (lb - l): the lookahead indices below lim[l] and at or
+  // above lim[l-1] hold length-l codes (canonical codes make lim non-decreasing in l)
   if (t < ns) {
     const int key = T.slot_src[t];
     const HuffSpec& h = (key & 4) ? tb->ac_spec[key & 3] : tb->dc_spec[key & 3];
@@ -105,6 +121,7 @@ __device__ int load_tables(EntTables& T, const ImgDesc* d, const ImgTables* tb) 
       const int cnt = h.bits[l];
       T.maxcode[t][l] = cnt ? code + cnt - 1 : -1;
       T.valoff[t][l] = cnt ? p - code : 0;
+      if (l <= lb) lim[t][l] = (code + cnt) << (lb - l);
       p += cnt;
       code = (code + cnt) << 1;
     }
@@ -112,30 +129,46 @@ __device__ int load_tables(EntTables& T, const ImgDesc* d, const ImgTables* tb) 
     T.valoff[t][0] = 0;
     T.maxcode[t][17] = 0xFFFFF;  // sentinel: the search stops at length 17 (bad code)
     T.valoff[t][17] = 0;
+    if (lb == 10) lim[t][11] = 1 << 30;
   }
-  for (int i = t; i < ns * 256; i += blockDim.x) {
+  for (int i = t; i < ns * 256; i += kEntThreads) {
     const int q = i >> 8, k = i & 255;
     const int key = T.slot_src[q];
     T.vals[q][k] = (key & 4) ? tb->ac_spec[key & 3].vals[k] : tb->dc_spec[key & 3].vals[k];
   }
   __syncthreads();
-  // 2^LB lookahead entries: the shortest length whose code prefix is <= maxcode (len | size << 4 |
-  // run << 8); codes longer than LB bits (entry 0) take the canonical search in decode_sym
-  for (int i = t; i < (ns << LB); i += blockDim.x) {
-    const int q = i >> LB, k = i & ((1 << LB) - 1);
-    const bool dc = (T.slot_src[q] & 4) == 0;
+  // 2^lb lookahead entries (len | size << 4 | run << 8); codes longer than lb bits (entry 0) take
+  // the canonical search in decode_sym
+  for (int i = t; i < (ns << lb); i += kEntThreads) {
+    const int q = i >> lb, k = i & ((1 << lb) - 1);
+    int l = 1;
+#pragma unroll
+    for (int m = 1; m <= 11; m++) l += k >= lim[q][m] ? 1 : 0;
     uint16_t e = 0;
-    for (int l = 1; l <= LB; l++) {
-      const int code = k >> (LB - l);
-      if (code <= T.maxcode[q][l]) {
-        const int sym = T.vals[q][(code + T.valoff[q][l]) & 0xFF];
-        const int sz = dc ? sym : (sym & 15), run = dc ? 0 : (sym >> 4);
-        e = sz > 15 ? (uint16_t)0 : (uint16_t)(l | (sz << 4) | (run << 8));
-        break;
-      }
+    if (l <= lb) {
+      const bool dc = (T.slot_src[q] & 4) == 0;
+      const int sym = T.vals[q][((k >> (lb - l)) + T.valoff[q][l]) & 0xFF];
+      const int sz = dc ? sym : (sym & 15), run = dc ? 0 : (sym >> 4);
+      e = sz > 15 ? (uint16_t)0 : (uint16_t)(l | (sz << 4) | (run << 8));
     }
     T.lut[i] = e;
   }
+  __syncthreads();
+  const uint4* src = reinterpret_cast<const uint4*>(&T);
+  uint4* dst = reinterpret_cast<uint4*>(&out[blockIdx.x]);
+  for (int i = t; i < (int)(sizeof(EntTables) / 16); i += kEntThreads) dst[i] = src[i];
+}
+
+// The image's tables into LDS (the LUT part the variant uses, and everything after it).
+template <int LB>
+__device__ __forceinline__ int load_tables(EntTables& T, const EntTables* g) {
+  const uint4* src = reinterpret_cast<const uint4*>(g);
+  uint4* dst = reinterpret_cast<uint4*>(&T);
+  constexpr int kLut16 = (int)(sizeof(T.lut) / 16), kAll16 = (int)(sizeof(EntTables) / 16);
+  const int ns = g->nslots;
+  const int used16 = variant_owns<LB>(ns) ? ((ns << LB) * 2 + 15) / 16 : 0;
+  for (int i = threadIdx.x; i < kAll16; i += blockDim.x)
+    if (i < used16 || i >= kLut16) dst[i] = src[i];
   __syncthreads();
   return ns;
 }
@@ -288,18 +321,19 @@ __device__ __forceinline__ void add_dc(int c, int v, int& d0, int& d1, int& d2) 
   d2 += c == 2 ? v : 0;
 }
 
+template <int NT = kEntThreads>
 __device__ inline int block_excl_scan(int v, int* tmp, int* total) {
   const int t = threadIdx.x;
   tmp[t] = v;
   __syncthreads();
-  for (int off = 1; off < kEntThreads; off <<= 1) {
+  for (int off = 1; off < NT; off <<= 1) {
     int a = t >= off ? tmp[t - off] : 0;
     __syncthreads();
     tmp[t] += a;
     __syncthreads();
   }
   const int incl = tmp[t];
-  *total = tmp[kEntThreads - 1];
+  *total = tmp[NT - 1];
   __syncthreads();
   return incl - v;
 }
@@ -307,22 +341,24 @@ __device__ inline int block_excl_scan(int v, int* tmp, int* total) {
 // ------------------------------------------------------------------------------------------
 // k_entsync
 // ------------------------------------------------------------------------------------------
-struct LdsSync {
+template <int NT>
+struct LdsSyncT {
   EntTables T;
-  int32_t tmp[kEntThreads];  // block_excl_scan scratch
+  int32_t tmp[NT];  // block_excl_scan scratch
   union {                    // sync rounds | final segmented scan (never live together)
     int32_t task[2][kMaxTasks];
     struct {
-      int32_t scan[4][kEntThreads];
-      int32_t flag[kEntThreads];
+      int32_t scan[4][NT];
+      int32_t flag[NT];
     } fs;
   } u;
   int32_t nsub, rounds, stages;
   unsigned long long sym[2];
   unsigned long long t0, t1, t2;
   unsigned long long it[2];
-  int32_t wmax[kEntThreads / 64];
+  int32_t wmax[NT / 64];
 };
+using LdsSync = LdsSyncT<kEntThreads>;
 
 // Speculative decode of subsequence S.  Warm-up: decode from `warm` bits before start_bit (not
 // before the segment start) assuming (block 0, DC), and take the first block boundary at or after
@@ -552,19 +588,17 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
 }
 
 template <int LB>
-__device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
+__device__ void entspec_image(int img, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                               uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
   __shared__ LdsSync L;
   const int t = threadIdx.x;
-  const int ns = load_tables<LB>(L.T, d, &tables[img]);
+  const int ns = load_tables<LB>(L.T, &tables[img]);
   if (!variant_owns<LB>(ns)) return;
   if (t == 0) {
-    L.rounds = 0;
-    L.stages = 0;
-    L.sym[0] = L.sym[1] = 0;
-    L.it[0] = L.it[1] = 0;
+    L.sym[0] = 0;
+    L.it[0] = 0;
   }
   const BlkCtx K = make_ctx(L.T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
@@ -608,7 +642,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const ImgTab
   }
   __syncthreads();
   const int nsub = L.nsub;
-  unsigned long long nsym_spec = 0, nsym_sync = 0;
+  unsigned long long nsym_spec = 0;
 
   // --- 1. speculative pass ---
   if (t == 0) L.t0 = __builtin_amdgcn_s_memtime();
@@ -625,97 +659,136 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const ImgTab
     L.t1 = __builtin_amdgcn_s_memtime();
     for (int w = 0; w < kEntThreads / 64; w++) L.it[0] += 64ull * L.wmax[w];
   }
-
-  // --- 2. sync rounds until every entry equals its predecessor's exit ---
-  for (;;) {
-    // tasks of this round: j with entry != exit(j-1); new entry = exit(j-1) (previous values)
-    int ntask = 0;
-    for (int base = 0; base < nsub; base += kEntThreads) {
-      const int j = base + t;
-      bool need = false;
-      uint32_t ep = 0;
-      uint16_t ebz = 0;
-      if (j < nsub && !sub[j].first) {
-        ep = sub[j - 1].cur_exit_p;
-        ebz = sub[j - 1].cur_exit_bz;
-        need = ep != sub[j].entry_p || ebz != sub[j].entry_bz;
-      }
-      int tot;
-      const int off = block_excl_scan(need ? 1 : 0, L.tmp, &tot);
-      if (need && ntask + off < kMaxTasks) {
-        L.u.task[0][ntask + off] = j;
-        SubState& S = sub[j];
-        S.new_entry_p = ep;
-        S.new_entry_bz = ebz;
-        S.res_p = ep;
-        S.res_bz = ebz;
-        S.res_nblk = 0;
-        S.res_ri = 0;
-        S.res_dc[0] = S.res_dc[1] = S.res_dc[2] = 0;
-        S.res_q[0] = S.res_q[1] = S.res_q[2] = 0;
-      }
-      ntask += tot;
-    }
-    if (ntask > kMaxTasks) ntask = kMaxTasks;  // the rest are picked up by the next round
-    __syncthreads();
-    if (ntask == 0) break;
-    if (t == 0) L.rounds++;
-    // work stages with doubling budgets; unfinished tasks are compacted to the front
-    int cur = 0, nt = ntask, budget = kBudget0;
-    while (nt > 0) {
-      if ((t & 63) == 0) L.wmax[t >> 6] = 0;
-      __syncthreads();
-      bool pending = false;
-      int my_task = -1;
-      if (t < nt) {
-        my_task = L.u.task[cur][t];
-        int k = 0;
-        pending = !sync_step<LB>(L.T, K, src, sub[my_task], recs + (int64_t)my_task * kRec, budget, &k);
-        nsym_sync += k;
-        atomicMax(&L.wmax[t >> 6], k);
-      }
-      for (int i = t + kEntThreads; i < nt; i += kEntThreads) {  // beyond one task per thread: no budget
-        int k = 0;
-        const int j = L.u.task[cur][i];
-        sync_step<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, 1 << 30, &k);
-        nsym_sync += k;
-      }
-      int tot;
-      const int off = block_excl_scan(pending ? 1 : 0, L.tmp, &tot);
-      if (pending) L.u.task[cur ^ 1][off] = my_task;
-      if (t == 0) {
-        L.stages++;
-        for (int w = 0; w < kEntThreads / 64; w++) L.it[1] += 64ull * L.wmax[w];
-      }
-      __syncthreads();
-      cur ^= 1;
-      nt = tot;
-      budget *= 2;
-    }
-    // commit every task of the round (entries first: they were read from cur_exit of j-1)
-    for (int i = t; i < ntask; i += kEntThreads) {
-      SubState& S = sub[L.u.task[0][i]];
-      S.entry_p = S.new_entry_p;
-      S.entry_bz = S.new_entry_bz;
-    }
-    __syncthreads();
-    for (int i = t; i < ntask; i += kEntThreads) {
-      SubState& S = sub[L.u.task[0][i]];
-      S.cur_exit_p = S.new_exit_p;
-      S.cur_exit_bz = S.new_exit_bz;
-      S.cur_nblk = S.new_nblk;
-      S.cur_dc[0] = S.new_dc[0];
-      S.cur_dc[1] = S.new_dc[1];
-      S.cur_dc[2] = S.new_dc[2];
-    }
-    __syncthreads();
+  atomicAdd(&L.sym[0], nsym_spec);
+  __syncthreads();
+  if (t == 0) {
+    d->nsub = nsub;
+    d->sym_spec = (int64_t)L.sym[0];
+    d->t_spec = (int64_t)(L.t1 - L.t0);
+    d->it_spec = (int64_t)L.it[0];
   }
+}
 
+template <int LB, int NT>
+__device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+                              uint8_t* __restrict__ scratch) {
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK) return;
+  __shared__ LdsSyncT<NT> L;
+  const int t = threadIdx.x;
+  const int nsub = d->nsub;
+  SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
+  SyncRec* recs = reinterpret_cast<SyncRec*>(scratch + d->off_rec);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
+  unsigned long long nsym_sync = 0;
+  if (t == 0) {
+    L.rounds = 0;
+    L.stages = 0;
+    L.sym[0] = L.sym[1] = 0;
+    L.it[0] = L.it[1] = 0;
+    L.t1 = __builtin_amdgcn_s_memtime();
+  }
+  // any subsequence whose entry differs from its predecessor's exit?  Only then are the decode
+  // tables built (most images: none after the warm-up)
+  bool need_any = false;
+  for (int j = t; j < nsub; j += NT)
+    if (!sub[j].first && (sub[j - 1].cur_exit_p != sub[j].entry_p || sub[j - 1].cur_exit_bz != sub[j].entry_bz))
+      need_any = true;
+  BlkCtx K{};
+  if (__syncthreads_or(need_any)) {
+    load_tables<LB>(L.T, &tables[img]);
+    K = make_ctx(L.T, d->bpm);
+    // --- 2. sync rounds until every entry equals its predecessor's exit ---
+    for (;;) {
+      // tasks of this round: j with entry != exit(j-1); new entry = exit(j-1) (previous values)
+      int ntask = 0;
+      for (int base = 0; base < nsub; base += NT) {
+        const int j = base + t;
+        bool need = false;
+        uint32_t ep = 0;
+        uint16_t ebz = 0;
+        if (j < nsub && !sub[j].first) {
+          ep = sub[j - 1].cur_exit_p;
+          ebz = sub[j - 1].cur_exit_bz;
+          need = ep != sub[j].entry_p || ebz != sub[j].entry_bz;
+        }
+        int tot;
+        const int off = block_excl_scan<NT>(need ? 1 : 0, L.tmp, &tot);
+        if (need && ntask + off < kMaxTasks) {
+          L.u.task[0][ntask + off] = j;
+          SubState& S = sub[j];
+          S.new_entry_p = ep;
+          S.new_entry_bz = ebz;
+          S.res_p = ep;
+          S.res_bz = ebz;
+          S.res_nblk = 0;
+          S.res_ri = 0;
+          S.res_dc[0] = S.res_dc[1] = S.res_dc[2] = 0;
+          S.res_q[0] = S.res_q[1] = S.res_q[2] = 0;
+        }
+        ntask += tot;
+      }
+      if (ntask > kMaxTasks) ntask = kMaxTasks;  // the rest are picked up by the next round
+      __syncthreads();
+      if (ntask == 0) break;
+      if (t == 0) L.rounds++;
+      // work stages with doubling budgets; unfinished tasks are compacted to the front
+      // budgets (and the compaction between stages) only pay when the tasks span several waves
+      int cur = 0, nt = ntask, budget = ntask <= NT ? (1 << 30) : kBudget0;
+      while (nt > 0) {
+        if ((t & 63) == 0) L.wmax[t >> 6] = 0;
+        __syncthreads();
+        bool pending = false;
+        int my_task = -1;
+        if (t < nt) {
+          my_task = L.u.task[cur][t];
+          int k = 0;
+          pending = !sync_step<LB>(L.T, K, src, sub[my_task], recs + (int64_t)my_task * kRec, budget, &k);
+          nsym_sync += k;
+          atomicMax(&L.wmax[t >> 6], k);
+        }
+        for (int i = t + NT; i < nt; i += NT) {  // beyond one task per thread: no budget
+          int k = 0;
+          const int j = L.u.task[cur][i];
+          sync_step<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, 1 << 30, &k);
+          nsym_sync += k;
+        }
+        int tot;
+        const int off = block_excl_scan<NT>(pending ? 1 : 0, L.tmp, &tot);
+        if (pending) L.u.task[cur ^ 1][off] = my_task;
+        if (t == 0) {
+          L.stages++;
+          for (int w = 0; w < NT / 64; w++) L.it[1] += 64ull * L.wmax[w];
+        }
+        __syncthreads();
+        cur ^= 1;
+        nt = tot;
+        budget *= 2;
+      }
+      // commit every task of the round (entries first: they were read from cur_exit of j-1)
+      for (int i = t; i < ntask; i += NT) {
+        SubState& S = sub[L.u.task[0][i]];
+        S.entry_p = S.new_entry_p;
+        S.entry_bz = S.new_entry_bz;
+      }
+      __syncthreads();
+      for (int i = t; i < ntask; i += NT) {
+        SubState& S = sub[L.u.task[0][i]];
+        S.cur_exit_p = S.new_exit_p;
+        S.cur_exit_bz = S.new_exit_bz;
+        S.cur_nblk = S.new_nblk;
+        S.cur_dc[0] = S.new_dc[0];
+        S.cur_dc[1] = S.new_dc[1];
+        S.cur_dc[2] = S.new_dc[2];
+      }
+      __syncthreads();
+    }
+  }
   // --- 3. segmented exclusive scan of (blocks, dc0, dc1, dc2) ---
   if (t == 0) L.t2 = __builtin_amdgcn_s_memtime();
   {
     int carry[4] = {0, 0, 0, 0};
-    for (int base = 0; base < nsub; base += kEntThreads) {
+    for (int base = 0; base < nsub; base += NT) {
       const int j = base + t;
       int v[4] = {0, 0, 0, 0};
       int f = 1;
@@ -730,7 +803,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const ImgTab
       for (int q = 0; q < 4; q++) L.u.fs.scan[q][t] = v[q];
       L.u.fs.flag[t] = f;
       __syncthreads();
-      for (int off = 1; off < kEntThreads; off <<= 1) {
+      for (int off = 1; off < NT; off <<= 1) {
         int a[4] = {0, 0, 0, 0}, af = 0;
         const bool take = t >= off;
         if (take) {
@@ -754,24 +827,19 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const ImgTab
         S.dc_ex[2] = ex[3];
       }
       __syncthreads();
-      const int any = L.u.fs.flag[kEntThreads - 1];
-      for (int q = 0; q < 4; q++) carry[q] = L.u.fs.scan[q][kEntThreads - 1] + (any ? 0 : carry[q]);
+      const int any = L.u.fs.flag[NT - 1];
+      for (int q = 0; q < 4; q++) carry[q] = L.u.fs.scan[q][NT - 1] + (any ? 0 : carry[q]);
       __syncthreads();
     }
   }
-  atomicAdd(&L.sym[0], nsym_spec);
   atomicAdd(&L.sym[1], nsym_sync);
   __syncthreads();
   if (t == 0) {
-    d->nsub = nsub;
     d->sync_rounds = L.rounds;
     d->pad0 = L.stages;
-    d->sym_spec = (int64_t)L.sym[0];
     d->sym_sync = (int64_t)L.sym[1];
-    d->t_spec = (int64_t)(L.t1 - L.t0);
     d->t_sync = (int64_t)(L.t2 - L.t1);
     d->t_scan = (int64_t)(__builtin_amdgcn_s_memtime() - L.t2);
-    d->it_spec = (int64_t)L.it[0];
     d->it_sync = (int64_t)L.it[1];
   }
 }
@@ -789,13 +857,13 @@ struct LdsWrite {
 };
 
 template <int LB>
-__device__ void entwrite_image(int img, ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
+__device__ void entwrite_image(int img, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                                uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
   __shared__ LdsWrite L;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int ns = load_tables<LB>(L.T, d, &tables[img]);
+  const int ns = load_tables<LB>(L.T, &tables[img]);
   if (!variant_owns<LB>(ns)) return;
   {
     uint4* z4 = reinterpret_cast<uint4*>(L.stage);
@@ -933,53 +1001,74 @@ __device__ void entwrite_image(int img, ImgDesc* __restrict__ descs, const ImgTa
   }
 }
 
+template <int LB, int PHASE>
+__device__ __forceinline__ void ent_phase(int img, ImgDesc* descs, const EntTables* tables, uint8_t* scratch) {
+  if (PHASE == 0) entspec_image<LB>(img, descs, tables, scratch);
+  else if (PHASE == 1) entsync_image<LB, kSyncThreads>(img, descs, tables, scratch);
+  else entwrite_image<LB>(img, descs, tables, scratch);
+}
+
 // The entropy kernels take images from their route's list.  The main route (LB = 11) runs one
 // workgroup per list entry (grid = batch size, surplus workgroups exit at once); the rare LB = 10
 // route strides a small grid over its list.
-template <int LB, bool WRITE>
-__device__ __forceinline__ void ent_feed(ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes,
+template <int LB, int PHASE>  // 0 spec, 1 sync + scan, 2 write
+__device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables, uint8_t* scratch, int32_t* routes,
                                          int cap) {
   const int r = LB == 11 ? kRtEnt11 : kRtEnt10;
   const int cnt = routes[r];
   const int32_t* list = route_list(routes, cap, r);
   if (LB == 11) {
     if ((int)blockIdx.x >= cnt) return;
-    if (WRITE) entwrite_image<LB>(list[blockIdx.x], descs, tables, scratch);
-    else entsync_image<LB>(list[blockIdx.x], descs, tables, scratch);
+    ent_phase<LB, PHASE>(list[blockIdx.x], descs, tables, scratch);
     return;
   }
   for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
-    if (WRITE) entwrite_image<LB>(list[li], descs, tables, scratch);
-    else entsync_image<LB>(list[li], descs, tables, scratch);
+    ent_phase<LB, PHASE>(list[li], descs, tables, scratch);
     __syncthreads();  // LDS reuse by the next image
   }
 }
 
+// k_entspec: subsequence layout + speculative pass (warm-up, records); k_entsync: sync rounds +
+// segmented scan, decode tables built only when some entry disagrees with its predecessor's exit.
 template <int LB>
 __global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(5)))
-k_entsync(ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables, uint8_t* __restrict__ scratch,
+k_entspec(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, uint8_t* __restrict__ scratch,
           int32_t* __restrict__ routes, int cap) {
-  ent_feed<LB, false>(descs, tables, scratch, routes, cap);
+  ent_feed<LB, 0>(descs, tables, scratch, routes, cap);
 }
 
 template <int LB>
-__global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
-                                                          uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
-                                                          int cap) {
-  ent_feed<LB, true>(descs, tables, scratch, routes, cap);
+__global__ void __launch_bounds__(kSyncThreads) k_entsync(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+                                                         uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
+                                                         int cap) {
+  ent_feed<LB, 1>(descs, tables, scratch, routes, cap);
 }
 
-hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes, int cap,
-                          hipStream_t s) {
+template <int LB>
+__global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+                                                          uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
+                                                          int cap) {
+  ent_feed<LB, 2>(descs, tables, scratch, routes, cap);
+}
+
+size_t enttab_bytes() { return sizeof(EntTables); }
+
+hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
+                          int cap, hipStream_t s) {
   const int g = n;  // one workgroup per image on the main route
-  hipLaunchKernelGGL(k_entsync<11>, dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL(k_entsync<10>, dim3(g < 256 ? g : 256), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  EntTables* tables = static_cast<EntTables*>(etab);
+  hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
+  hipLaunchKernelGGL(k_entspec<11>, dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL(k_entspec<10>, dim3(g < 256 ? g : 256), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL(k_entsync<11>, dim3(g), dim3(kSyncThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL(k_entsync<10>, dim3(g < 256 ? g : 256), dim3(kSyncThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 
-hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes, int cap,
+hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
                            hipStream_t s) {
   const int g = n;  // one workgroup per image on the main route
+  const EntTables* tables = static_cast<const EntTables*>(etab);
   hipLaunchKernelGGL(k_entwrite<11>, dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   hipLaunchKernelGGL(k_entwrite<10>, dim3(g < 256 ? g : 256), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();

@@ -12,9 +12,10 @@ hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, Im
                           hipStream_t s);
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
-hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes, int cap,
-                          hipStream_t s);
-hipError_t launch_entwrite(int n, ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, int32_t* routes, int cap,
+size_t enttab_bytes();  // per-image decode tables (k_enttab) held in HBM between the entropy kernels
+hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
+                          int cap, hipStream_t s);
+hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
                            hipStream_t s);
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
 hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s);
