@@ -23,7 +23,7 @@ constexpr int kMaxBlocksPerMcu = 10;  // D_MAX_BLOCKS_IN_MCU
 constexpr int kRec = 64;              // block-boundary records kept per subsequence by k_entsync
 constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
-constexpr int kWarmBits = 4000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
+constexpr int kWarmBits = 2000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
 constexpr int kUPad = 128;            // zero bytes after each unstuffed stream (bit-reader prefetch)
 constexpr int kMaxSpan = 960;         // source columns per fused-resample tile (LDS row width)
 constexpr int kRingDW = 3072;         // fused-resample ring (dwords): ring_rows x (3072 / ring_rows) columns

@@ -173,6 +173,44 @@ __device__ __forceinline__ int load_tables(EntTables& T, const EntTables* g) {
   return ns;
 }
 
+// k_entsync's tables: a 2^9-entry lookahead per slot (codes of at most 9 bits; longer ones take the
+// canonical search) so that about 10 KB of LDS per image lets ~15 images share a CU -- its few
+// lanes per image are latency-bound, and more images in flight hide that latency.
+constexpr int kSyncLB = 9;
+struct SyncTables {
+  uint16_t lut[kMaxSlots << kSyncLB];
+  int32_t maxcode[kMaxSlots][18];
+  int32_t valoff[kMaxSlots][18];
+  uint8_t vals[kMaxSlots][256];
+  uint32_t pk_dc[2], pk_ac[2], pk_c;
+};
+
+// The 9-bit lookahead from the image's LB-bit one: entry k << (LB - 9) when its code fits 9 bits.
+template <int LB>
+__device__ void load_sync_tables(SyncTables& T, const EntTables* g) {
+  const int ns = g->nslots;
+  for (int i = threadIdx.x; i < (ns << kSyncLB); i += blockDim.x) {
+    const int q = i >> kSyncLB, k = i & ((1 << kSyncLB) - 1);
+    const uint16_t e = g->lut[(q << LB) + (k << (LB - kSyncLB))];
+    T.lut[i] = (e & 15) <= kSyncLB ? e : (uint16_t)0;
+  }
+  for (int i = threadIdx.x; i < ns * 18; i += blockDim.x) {
+    T.maxcode[i / 18][i % 18] = g->maxcode[i / 18][i % 18];
+    T.valoff[i / 18][i % 18] = g->valoff[i / 18][i % 18];
+  }
+  const uint32_t* gv = reinterpret_cast<const uint32_t*>(g->vals);
+  uint32_t* tv = reinterpret_cast<uint32_t*>(T.vals);
+  for (int i = threadIdx.x; i < ns * 64; i += blockDim.x) tv[i] = gv[i];
+  if (threadIdx.x == 0) {
+    T.pk_dc[0] = g->pk_dc[0];
+    T.pk_dc[1] = g->pk_dc[1];
+    T.pk_ac[0] = g->pk_ac[0];
+    T.pk_ac[1] = g->pk_ac[1];
+    T.pk_c = g->pk_c;
+  }
+  __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------
 // Bit reader: 64-bit MSB-first window fed from a queue of kQ byte-swapped words held in
 // registers.  The queue is refilled for every lane of a wave at once (bits_fill) when any lane
@@ -185,7 +223,8 @@ constexpr int kSpecGroup = 4;   // symbols decoded between two wave-uniform refi
 constexpr int kWriteGroup = 4;  // (write pass)
 static_assert(kSpecGroup < kQ && kWriteGroup < kQ, "a fresh refill must pass the group check");
 
-struct Bits {
+template <int Q>
+struct BitsQ {
   const uint32_t* src;
   uint64_t buf;
   int nb;
@@ -193,8 +232,9 @@ struct Bits {
   uint32_t wi;   // word index of q[0]
   uint32_t pos;  // absolute bit position of the next unconsumed bit
   uint32_t lim;  // bits at or beyond lim read as zeros (the data ran into a marker)
-  uint32_t q[kQ];
+  uint32_t q[Q];
 };
+using Bits = BitsQ<kQ>;
 
 // Word w of the stream (MSB-first bits [32w, 32w + 32)), zeroed from bit `lim` on.
 __device__ __forceinline__ uint32_t load_word(const uint32_t* src, uint32_t w, uint32_t lim) {
@@ -204,7 +244,8 @@ __device__ __forceinline__ uint32_t load_word(const uint32_t* src, uint32_t w, u
   return keep >= 32u ? v : (v & ~(0xFFFFFFFFu >> keep));
 }
 
-__device__ __forceinline__ void bits_init(Bits& b, const uint32_t* src, uint32_t p, uint32_t lim) {
+template <int Q>
+__device__ __forceinline__ void bits_init(BitsQ<Q>& b, const uint32_t* src, uint32_t p, uint32_t lim) {
   b.src = src;
   b.lim = lim;
   const uint32_t w = p >> 5;
@@ -216,30 +257,33 @@ __device__ __forceinline__ void bits_init(Bits& b, const uint32_t* src, uint32_t
   b.wi = w + 2;
   b.pos = p;
 #pragma unroll
-  for (int k = 0; k < kQ; k++) b.q[k] = 0;
+  for (int k = 0; k < Q; k++) b.q[k] = 0;
 }
 
 // Wave-synchronous refill: re-reads kQ words from wi (the ustream carries kUPad bytes of slack).
-__device__ __forceinline__ void bits_fill(Bits& b) {
-  if ((b.wi + kQ) * 32u <= b.lim) {  // the common case: all kQ words lie before the limit
+template <int Q>
+__device__ __forceinline__ void bits_fill(BitsQ<Q>& b) {
+  if ((b.wi + Q) * 32u <= b.lim) {  // the common case: all kQ words lie before the limit
 #pragma unroll
-    for (int k = 0; k < kQ; k++) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+    for (int k = 0; k < Q; k++) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
   } else {
 #pragma unroll
-    for (int k = 0; k < kQ; k++) b.q[k] = load_word(b.src, b.wi + k, b.lim);
+    for (int k = 0; k < Q; k++) b.q[k] = load_word(b.src, b.wi + k, b.lim);
   }
-  b.nq = kQ;
+  b.nq = Q;
 }
 
 // Can the next symbol (at most 32 bits) be decoded without a refill?
-__device__ __forceinline__ bool bits_can(const Bits& b) { return b.nb > 32 || b.nq > 0; }
+template <int Q>
+__device__ __forceinline__ bool bits_can(const BitsQ<Q>& b) { return b.nb > 32 || b.nq > 0; }
 
-__device__ __forceinline__ void bits_pull(Bits& b) {
+template <int Q>
+__device__ __forceinline__ void bits_pull(BitsQ<Q>& b) {
   if (b.nb <= 32) {
     b.buf |= (uint64_t)b.q[0] << (32 - b.nb);
     b.nb += 32;
 #pragma unroll
-    for (int k = 0; k + 1 < kQ; k++) b.q[k] = b.q[k + 1];
+    for (int k = 0; k + 1 < Q; k++) b.q[k] = b.q[k + 1];
     b.nq--;
     b.wi++;
   }
@@ -256,7 +300,8 @@ __device__ __forceinline__ int ctx_dc(const BlkCtx& k, int blk) { return (int)(k
 __device__ __forceinline__ int ctx_ac(const BlkCtx& k, int blk) { return (int)(k.pac >> (4 * blk)) & 15; }
 __device__ __forceinline__ int ctx_c(const BlkCtx& k, int blk) { return (int)(k.pc >> (2 * blk)) & 3; }
 
-__device__ __forceinline__ BlkCtx make_ctx(const EntTables& T, int bpm) {
+template <class TT>
+__device__ __forceinline__ BlkCtx make_ctx(const TT& T, int bpm) {
   BlkCtx k;
   k.pdc = ((uint64_t)T.pk_dc[1] << 32) | T.pk_dc[0];
   k.pac = ((uint64_t)T.pk_ac[1] << 32) | T.pk_ac[0];
@@ -267,8 +312,8 @@ __device__ __forceinline__ BlkCtx make_ctx(const EntTables& T, int bpm) {
 
 // One symbol (jdhuff.c HUFF_DECODE + get_bits + HUFF_EXTEND): DC -> category s, r = 0;
 // AC -> (r, s).  val = the extended value (0 when s = 0).
-template <int LB>
-__device__ __forceinline__ void decode_sym(const EntTables& T, Bits& b, int slot, bool isdc, int& s, int& r, int& val,
+template <int LB, class TT, int Q>
+__device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, bool isdc, int& s, int& r, int& val,
                                            int& bad) {
   bits_pull(b);
   const uint32_t hi = (uint32_t)(b.buf >> 32);
@@ -341,12 +386,12 @@ __device__ inline int block_excl_scan(int v, int* tmp, int* total) {
 // ------------------------------------------------------------------------------------------
 // k_entsync
 // ------------------------------------------------------------------------------------------
-template <int NT>
+template <int NT, class TT = EntTables>
 struct LdsSyncT {
-  EntTables T;
+  TT T;
   int32_t tmp[NT];  // block_excl_scan scratch
   union {                    // sync rounds | final segmented scan (never live together)
-    int32_t task[2][kMaxTasks];
+    int32_t task[1][kMaxTasks];
     struct {
       int32_t scan[4][NT];
       int32_t flag[NT];
@@ -464,6 +509,57 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
   S.spec_dc[1] = S.cur_dc[1] = d1;
   S.spec_dc[2] = S.cur_dc[2] = d2;
   S.nrec = nrec < kRec ? nrec : kRec;
+  return nsym;
+}
+
+// Re-decode of subsequence S from its corrected entry (new_entry_*) to its end -- the first block
+// boundary at or after end_bit, as in the speculative pass -- giving the exact exit state, block
+// count and DC sums in new_*.  A lean loop like the speculative pass's: the few lanes running such
+// tasks are bound by per-symbol latency, so a full re-decode beats stopping early at a merge point
+// with the speculative path (which needs per-block record bookkeeping).
+constexpr int kSyncQ = kQ;  // (a deeper queue measured slower: the pull shifts it)
+
+template <int LB, class TT>
+__device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S) {
+  const uint32_t end = S.end_bit;
+  BitsQ<kSyncQ> b;
+  bits_init(b, src, S.new_entry_p, S.lim_bit);
+  int blk = S.new_entry_bz >> 8, z = S.new_entry_bz & 0xFF;
+  int nblk = 0, bad = 0, nsym = 0, d0 = 0, d1 = 0, d2 = 0;
+  int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
+  bool run = b.pos < end || z != 0;
+  while (__builtin_amdgcn_ballot_w64(run)) {
+    if (run) bits_fill(b);
+    for (;;) {
+#pragma unroll
+      for (int u = 0; u < kSpecGroup; u++) {
+        if (run) {
+          int sy, r, val;
+          const bool isdc = z == 0;
+          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, sy, r, val, bad);
+          nsym++;
+          add_dc(c, isdc ? val : 0, d0, d1, d2);
+          if (next_z(z, sy, r)) {
+            nblk++;
+            blk = blk + 1 == K.bpm ? 0 : blk + 1;
+            c = ctx_c(K, blk);
+            sdc = ctx_dc(K, blk);
+            sac = ctx_ac(K, blk);
+          }
+          run = b.pos < end || z != 0;
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kSpecGroup + 1)) ||
+          !__builtin_amdgcn_ballot_w64(run))
+        break;
+    }
+  }
+  S.new_exit_p = b.pos;
+  S.new_exit_bz = (uint16_t)((blk << 8) | z);
+  S.new_nblk = nblk;
+  S.new_dc[0] = d0;
+  S.new_dc[1] = d1;
+  S.new_dc[2] = d2;
   return nsym;
 }
 
@@ -674,7 +770,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
                               uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
-  __shared__ LdsSyncT<NT> L;
+  __shared__ LdsSyncT<NT, SyncTables> L;
   const int t = threadIdx.x;
   const int nsub = d->nsub;
   SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
@@ -696,7 +792,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       need_any = true;
   BlkCtx K{};
   if (__syncthreads_or(need_any)) {
-    load_tables<LB>(L.T, &tables[img]);
+    load_sync_tables<LB>(L.T, &tables[img]);
     K = make_ctx(L.T, d->bpm);
     // --- 2. sync rounds until every entry equals its predecessor's exit ---
     for (;;) {
@@ -732,39 +828,8 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       __syncthreads();
       if (ntask == 0) break;
       if (t == 0) L.rounds++;
-      // work stages with doubling budgets; unfinished tasks are compacted to the front
-      // budgets (and the compaction between stages) only pay when the tasks span several waves
-      int cur = 0, nt = ntask, budget = ntask <= NT ? (1 << 30) : kBudget0;
-      while (nt > 0) {
-        if ((t & 63) == 0) L.wmax[t >> 6] = 0;
-        __syncthreads();
-        bool pending = false;
-        int my_task = -1;
-        if (t < nt) {
-          my_task = L.u.task[cur][t];
-          int k = 0;
-          pending = !sync_step<LB>(L.T, K, src, sub[my_task], recs + (int64_t)my_task * kRec, budget, &k);
-          nsym_sync += k;
-          atomicMax(&L.wmax[t >> 6], k);
-        }
-        for (int i = t + NT; i < nt; i += NT) {  // beyond one task per thread: no budget
-          int k = 0;
-          const int j = L.u.task[cur][i];
-          sync_step<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, 1 << 30, &k);
-          nsym_sync += k;
-        }
-        int tot;
-        const int off = block_excl_scan<NT>(pending ? 1 : 0, L.tmp, &tot);
-        if (pending) L.u.task[cur ^ 1][off] = my_task;
-        if (t == 0) {
-          L.stages++;
-          for (int w = 0; w < NT / 64; w++) L.it[1] += 64ull * L.wmax[w];
-        }
-        __syncthreads();
-        cur ^= 1;
-        nt = tot;
-        budget *= 2;
-      }
+      for (int i = t; i < ntask; i += NT) nsym_sync += sync_full<kSyncLB>(L.T, K, src, sub[L.u.task[0][i]]);
+      __syncthreads();
       // commit every task of the round (entries first: they were read from cur_exit of j-1)
       for (int i = t; i < ntask; i += NT) {
         SubState& S = sub[L.u.task[0][i]];
