@@ -21,6 +21,7 @@ using namespace sdsj;
 
 namespace {
 constexpr int kStages = 11;
+constexpr int kMaxLanes = 4;
 const char* kStageNames[kStages] = {"parse", "plan",  "unstuff", "entsync", "entwrite", "idct",
                                     "color", "coeffs", "hpass",   "vpass",   "resample"};
 }  // namespace
@@ -37,6 +38,13 @@ struct sdsj_engine {
   int64_t* d_total = nullptr;
   void* d_etab = nullptr;       // per-image decode tables built by k_enttab
   int32_t* d_routes = nullptr;  // per-variant image lists built by k_plan (sdsj_common.h Route)
+  // lanes 2.. of a chunk (run_chunk): route lists and scratch totals, streams and events
+  int lanes = 4;     // SDSJ_LANES (experiments)
+  int lane_mid = 3;  // lane k + 1 starts after lane k's stage lane_mid (>= 2: k_plan done; -1: its spec pass)
+  int64_t* d_totals_x = nullptr;
+  int32_t* d_routes_x = nullptr;
+  hipStream_t aux[kMaxLanes - 1] = {};
+  hipEvent_t ev_mid[kMaxLanes - 1] = {}, ev_join[kMaxLanes - 1] = {};
   // frames path: host-planned descriptors and route list, staged through pinned memory
   ImgDesc* h_fdescs = nullptr;
   int32_t* h_froutes = nullptr;
@@ -132,9 +140,26 @@ bool valid_op(const sdsj_op* op) {
          (op->layout == SDSJ_LAYOUT_CHW || op->layout == SDSJ_LAYOUT_HWC);
 }
 
-// Runs the kernel sequence for one chunk (n <= max_batch) of device-resident inputs.
-int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_offsets, const int32_t* d_lengths,
-              const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status, hipStream_t s) {
+int64_t out_bytes_per_image(const sdsj_op& op) {
+  return (int64_t)op.out_h * op.out_w * 3 * (op.out_dtype == SDSJ_DTYPE_F32 ? 4 : 1);
+}
+
+// One lane of a chunk: a contiguous range of its images with their own route lists and scratch
+// total.  `base`: the scratch bytes the previous lane took (device), or null for the first lane.
+struct Lane {
+  ImgDesc* descs;
+  ImgTables* tables;
+  void* etab;
+  int32_t* routes;
+  int64_t* total;
+  const int64_t* base;
+};
+
+// Runs the kernel sequence for one lane (n <= max_batch images) of device-resident inputs.
+// after_spec (optional) is recorded once the lane's speculative entropy pass is queued.
+int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const int64_t* d_offsets,
+             const int32_t* d_lengths, const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status,
+             hipStream_t s, hipEvent_t after_spec) {
   std::vector<hipEvent_t>* evs = nullptr;
   if (e->timing) {
     if (e->ev_used == e->ev_sets.size()) {
@@ -146,38 +171,80 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
   }
   auto mark = [&](int k) {
     if (evs) (void)hipEventRecord((*evs)[k], s);
+    if (after_spec && e->lane_mid == k) (void)hipEventRecord(after_spec, s);
   };
   mark(0);
-  SDSJ_HIP(e, launch_parse(n, d_blob, d_offsets, d_lengths, op, e->warm_bits, e->descs, e->tables, s));
+  SDSJ_HIP(e, launch_parse(n, d_blob, d_offsets, d_lengths, op, e->warm_bits, ln.descs, ln.tables, s));
   mark(1);
   const int cap = e->max_batch;
-  SDSJ_HIP(e, launch_plan(n, e->descs, e->capacity, e->d_total, e->d_routes, cap, s));
+  SDSJ_HIP(e, launch_plan(n, ln.descs, e->capacity, ln.base, ln.total, ln.routes, cap, s));
   mark(2);
-  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, e->descs, e->scratch, s));
-  SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, e->descs, e->scratch, s));
+  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, s));
+  SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, ln.descs, e->scratch, s));
   mark(3);
-  SDSJ_HIP(e, launch_entsync(n, e->descs, e->tables, e->d_etab, e->scratch, e->d_routes, cap, s));
+  SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s,
+                             e->lane_mid < 0 ? after_spec : nullptr));
   mark(4);
-  SDSJ_HIP(e, launch_entwrite(n, e->descs, e->d_etab, e->scratch, e->d_routes, cap, s));
+  SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
   mark(5);
-  SDSJ_HIP(e, launch_idct(n, e->descs, e->tables, e->scratch, s));
+  SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
   mark(6);
-  SDSJ_HIP(e, launch_color(n, e->descs, e->scratch, e->d_routes, cap, s));
+  SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s));
   mark(7);
-  SDSJ_HIP(e, launch_coeffs(n, e->descs, op, e->scratch, s));
+  SDSJ_HIP(e, launch_coeffs(n, ln.descs, op, e->scratch, s));
   mark(8);
-  SDSJ_HIP(e, launch_hpass(n, e->descs, op, e->scratch, e->d_routes, cap, s));
+  SDSJ_HIP(e, launch_hpass(n, ln.descs, op, e->scratch, ln.routes, cap, s));
   mark(9);
-  SDSJ_HIP(e, launch_vpass(n, e->descs, op, e->scratch, d_flip, d_out, e->d_routes, cap, e->d_lut, s));
+  SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s));
   mark(10);
-  SDSJ_HIP(e, launch_resample(n, e->descs, op, e->scratch, d_flip, d_out, d_status, e->d_routes, cap, e->d_lut, s));
-  SDSJ_HIP(e, launch_finish(n, e->descs, op, d_out, d_status, e->d_lut, s));
+  SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s));
+  SDSJ_HIP(e, launch_finish(n, ln.descs, op, d_out, d_status, e->d_lut, s));
   mark(11);
   return SDSJ_OK;
 }
 
-int64_t out_bytes_per_image(const sdsj_op& op) {
-  return (int64_t)op.out_h * op.out_w * 3 * (op.out_dtype == SDSJ_DTYPE_F32 ? 4 : 1);
+// Runs one chunk (n <= max_batch).  A chunk of at least L x kLaneMin images runs as L lanes
+// (contiguous image ranges) on L streams, lane k + 1 starting once lane k has planned its scratch:
+// the lanes' kernel sequences overlap, so the latency-bound kernels of one lane (the entropy sync
+// pass, every kernel's tail) run beside the throughput-bound kernels of another.  The caller's
+// stream waits for every lane at the end.  Scratch is taken by the lanes in image order (lane k + 1's
+// k_plan starts from lane k's total), so per-image results and capacity failures are those of a
+// single lane.
+constexpr int kLaneMin = 256;
+
+int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_offsets, const int32_t* d_lengths,
+              const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status, hipStream_t s) {
+  int nl = std::min(std::max(e->lanes, 1), kMaxLanes);
+  while (nl > 1 && n < nl * kLaneMin) nl--;
+  const Lane first{e->descs, e->tables, e->d_etab, e->d_routes, e->d_total, nullptr};
+  if (nl == 1) return run_lane(e, first, n, d_blob, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr);
+  for (int k = 0; k + 1 < nl; k++)
+    if (!e->aux[k]) {
+      SDSJ_HIP(e, hipStreamCreateWithFlags(&e->aux[k], hipStreamNonBlocking));
+      SDSJ_HIP(e, hipEventCreateWithFlags(&e->ev_mid[k], hipEventDisableTiming));
+      SDSJ_HIP(e, hipEventCreateWithFlags(&e->ev_join[k], hipEventDisableTiming));
+    }
+  const int64_t ob = out_bytes_per_image(op);
+  const size_t rsz = kRouteSlots + (size_t)kNumRoutes * e->max_batch;
+  for (int k = 0; k < nl; k++) {
+    const int i0 = (int)((int64_t)n * k / nl), i1 = (int)((int64_t)n * (k + 1) / nl);
+    const Lane ln = k == 0 ? first
+                           : Lane{e->descs + i0, e->tables + i0,
+                                  static_cast<uint8_t*>(e->d_etab) + (size_t)i0 * enttab_bytes(),
+                                  e->d_routes_x + (k - 1) * rsz, e->d_totals_x + (k - 1),
+                                  k == 1 ? e->d_total : e->d_totals_x + (k - 2)};
+    hipStream_t ls = k == 0 ? s : e->aux[k - 1];
+    if (k > 0) SDSJ_HIP(e, hipStreamWaitEvent(ls, e->ev_mid[k - 1], 0));
+    int st = run_lane(e, ln, i1 - i0, d_blob, d_offsets + i0, d_lengths + i0, op, d_flip ? d_flip + i0 : nullptr,
+                      static_cast<uint8_t*>(d_out) + i0 * ob, d_status + i0, ls,
+                      k + 1 < nl ? e->ev_mid[k] : nullptr);
+    if (st != SDSJ_OK) return st;
+  }
+  for (int k = 0; k + 1 < nl; k++) {
+    SDSJ_HIP(e, hipEventRecord(e->ev_join[k], e->aux[k]));
+    SDSJ_HIP(e, hipStreamWaitEvent(s, e->ev_join[k], 0));
+  }
+  return SDSJ_OK;
 }
 
 }  // namespace
@@ -232,7 +299,14 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   };
   if (hipMalloc(&e->descs, sizeof(ImgDesc) * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->tables, sizeof(ImgTables) * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (const char* l = getenv("SDSJ_LANES")) e->lanes = atoi(l);
+  if (const char* l = getenv("SDSJ_LANE_MID")) e->lane_mid = atoi(l);
+  if (e->lane_mid >= 0 && e->lane_mid < 2) e->lane_mid = 2;  // a lane's k_plan reads the previous lane's total
   if (hipMalloc(&e->d_total, sizeof(int64_t)) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMalloc(&e->d_totals_x, sizeof(int64_t) * (kMaxLanes - 1)) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMalloc(&e->d_routes_x, sizeof(int32_t) * (kMaxLanes - 1) * (kRouteSlots + (size_t)kNumRoutes * e->max_batch)) !=
+      hipSuccess)
+    return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_etab, enttab_bytes() * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_routes, sizeof(int32_t) * (kRouteSlots + (size_t)kNumRoutes * e->max_batch)) != hipSuccess)
     return cleanup(SDSJ_ENOMEM);
@@ -266,6 +340,13 @@ int sdsj_engine_destroy(sdsj_engine* e) {
   (void)hipFree(e->d_total);
   (void)hipFree(e->d_routes);
   (void)hipFree(e->d_etab);
+  (void)hipFree(e->d_totals_x);
+  (void)hipFree(e->d_routes_x);
+  for (int k = 0; k + 1 < kMaxLanes; k++) {
+    if (e->aux[k]) (void)hipStreamDestroy(e->aux[k]);
+    if (e->ev_mid[k]) (void)hipEventDestroy(e->ev_mid[k]);
+    if (e->ev_join[k]) (void)hipEventDestroy(e->ev_join[k]);
+  }
   (void)hipHostFree(e->h_fdescs);
   (void)hipHostFree(e->h_froutes);
   (void)hipFree(e->d_lut);
@@ -445,7 +526,8 @@ int sdsj_engine_stage_times(const sdsj_engine* e, float* ms, int cap, int* n_sta
   for (int k = 0; k < cap && k < kStages; k++) ms[k] = 0.f;
   if (!e->timing || e->ev_used == 0) return SDSJ_OK;
   DeviceGuard g(e->device);
-  if (hipEventSynchronize(e->ev_sets[e->ev_used - 1][kStages]) != hipSuccess) return SDSJ_EHIP;
+  for (size_t c = 0; c < e->ev_used; c++)  // lanes run on two streams: wait for every set
+    if (hipEventSynchronize(e->ev_sets[c][kStages]) != hipSuccess) return SDSJ_EHIP;
   for (size_t c = 0; c < e->ev_used; c++) {
     for (int k = 0; k < cap && k < kStages; k++) {
       float v = 0.f;

@@ -1119,12 +1119,13 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ 
 size_t enttab_bytes() { return sizeof(EntTables); }
 
 hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s) {
+                          int cap, hipStream_t s, hipEvent_t after_spec) {
   const int g = n;  // one workgroup per image on the main route
   EntTables* tables = static_cast<EntTables*>(etab);
   hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
   hipLaunchKernelGGL(k_entspec<11>, dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   hipLaunchKernelGGL(k_entspec<10>, dim3(g < 256 ? g : 256), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  if (after_spec) (void)hipEventRecord(after_spec, s);
   hipLaunchKernelGGL(k_entsync<11>, dim3(g), dim3(kSyncThreads), 0, s, descs, tables, scratch, routes, cap);
   hipLaunchKernelGGL(k_entsync<10>, dim3(g < 256 ? g : 256), dim3(kSyncThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();

@@ -7,14 +7,16 @@
 namespace sdsj {
 hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, const int32_t* lengths, const sdsj_op& op,
                         int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s);
-hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, int32_t* routes, int cap, hipStream_t s);
+// base: scratch bytes a previous lane of the batch already took (device), or null
+hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* base, int64_t* total, int32_t* routes,
+                       int cap, hipStream_t s);
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
 size_t enttab_bytes();  // per-image decode tables (k_enttab) held in HBM between the entropy kernels
 hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s);
+                          int cap, hipStream_t s, hipEvent_t after_spec);  // recorded between the two passes
 hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
                            hipStream_t s);
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);

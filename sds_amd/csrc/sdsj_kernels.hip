@@ -250,11 +250,12 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
 // k_plan: one workgroup; exclusive scan of per-image scratch needs -> absolute offsets.
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ descs, int64_t capacity,
-                                               int64_t* __restrict__ total_out, int32_t* __restrict__ routes, int cap) {
+                                               const int64_t* __restrict__ base, int64_t* __restrict__ total_out,
+                                               int32_t* __restrict__ routes, int cap) {
   __shared__ int64_t part[1024];
   __shared__ int64_t carry;
   __shared__ int rcnt[kNumRoutes];
-  if (threadIdx.x == 0) carry = 0;
+  if (threadIdx.x == 0) carry = base ? *base : 0;  // a second lane allocates after the first
   if (threadIdx.x < kNumRoutes) rcnt[threadIdx.x] = 0;
   __syncthreads();
   for (int base = 0; base < n; base += 1024) {
@@ -1168,8 +1169,9 @@ hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, cons
   hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, offsets, lengths, op, warm_bits, descs, tables);
   return hipGetLastError();
 }
-hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, int64_t* total, int32_t* routes, int cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, n, descs, capacity, total, routes, cap);
+hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* base, int64_t* total, int32_t* routes,
+                       int cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, n, descs, capacity, base, total, routes, cap);
   return hipGetLastError();
 }
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,

@@ -154,46 +154,92 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
         tm = now;
       }
     };
-    for (int ra = r_lo; ra < r_hi; ra += kFRows) {
-      const int nr = r_hi - ra < kFRows ? r_hi - ra : kFRows;
-      const int ya = cy0 + ra;
-      int ilo = (ya >> 1) - 1, ihi = ((ya + nr - 1) >> 1) + 1;
+    // Plane rows of a step (4 source rows): luma rows ya.., chroma rows ilo..ihi -- the rows the
+    // h2v2 fancy upsampling reads (row i = y >> 1 and its neighbour f = i -/+ 1 for even/odd y),
+    // clamped to the plane: at most 4 chroma rows per plane.
+    struct Step {
+      int ra, nr, ya, ilo, nrc;
+    };
+    auto plan_step = [&](int ra) {
+      Step p;
+      p.ra = ra;
+      p.nr = r_hi - ra < kFRows ? r_hi - ra : kFRows;
+      p.ya = cy0 + ra;
+      int ilo = ((p.ya + 1) >> 1) - 1, ihi = (p.ya + p.nr) >> 1;
       ilo = ilo < 0 ? 0 : ilo;
       ihi = ihi > dhc - 1 ? dhc - 1 : ihi;
-      const int nrc = ihi - ilo + 1;
-      // A. stage: luma rows ya.., chroma rows ilo..ihi (one global_load_lds_dword per 64 dwords)
-      for (int row = wv; row < nr + 2 * nrc; row += 4) {
-        const uint8_t* g;
-        int nd, o;
-        if (row < nr) {
-          g = pY + (int64_t)(ya + row) * pitchY + jalY;
-          nd = ndY;
-          o = row * kFYDW;
-        } else if (row < nr + nrc) {
-          g = pCb + (int64_t)(ilo + row - nr) * pitchC + jalC;
-          nd = ndC;
-          o = kFRows * kFYDW + (row - nr) * kFCDW;
-        } else {
-          g = pCr + (int64_t)(ilo + row - nr - nrc) * pitchC + jalC;
-          nd = ndC;
-          o = kFRows * kFYDW + kFRows * kFCDW + (row - nr - nrc) * kFCDW;
-        }
-        for (int h = 0; h < nd; h += 64)
-          if (h + lane < nd)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 4 * (h + lane)),
-                                             (__attribute__((address_space(3))) void*)(L.st + o + h), 4, 0, 0);
+      p.ilo = ilo;
+      p.nrc = ihi - ilo + 1;
+      return p;
+    };
+    // The next step's rows travel through registers (global loads issued before this step's
+    // conversion, written to LDS after its H/V work), so their latency hides behind a whole step.
+    // Wave wv holds staged rows wv, wv + 4, wv + 8 (<= 12 rows), 64 dwords per load.
+    constexpr int kPR = 3, kPC = (kMaxSpan / 4 + 2 + 63) / 64;
+    uint32_t pre[kPR][kPC];
+    auto row_src = [&](const Step& p, int row, const uint8_t*& g, int& nd, int& o) {
+      if (row < p.nr) {
+        g = pY + (int64_t)(p.ya + row) * pitchY + jalY;
+        nd = ndY;
+        o = row * kFYDW;
+      } else if (row < p.nr + p.nrc) {
+        g = pCb + (int64_t)(p.ilo + row - p.nr) * pitchC + jalC;
+        nd = ndC;
+        o = kFRows * kFYDW + (row - p.nr) * kFCDW;
+      } else {
+        g = pCr + (int64_t)(p.ilo + row - p.nr - p.nrc) * pitchC + jalC;
+        nd = ndC;
+        o = kFRows * kFYDW + kFRows * kFCDW + (row - p.nr - p.nrc) * kFCDW;
       }
-      if (t < nr) {
-        const int y = ya + t, i = y >> 1;
+    };
+    auto issue = [&](const Step& p) {
+#pragma unroll
+      for (int i = 0; i < kPR; i++) {
+        const int row = wv + 4 * i;
+        if (row < p.nr + 2 * p.nrc) {
+          const uint8_t* g;
+          int nd, o;
+          row_src(p, row, g, nd, o);
+          const uint32_t* g4 = reinterpret_cast<const uint32_t*>(g);
+#pragma unroll
+          for (int h = 0; h < kPC; h++)
+            if (64 * h + lane < nd) pre[i][h] = __builtin_nontemporal_load(g4 + 64 * h + lane);
+        }
+      }
+    };
+    auto commit = [&](const Step& p) {
+#pragma unroll
+      for (int i = 0; i < kPR; i++) {
+        const int row = wv + 4 * i;
+        if (row < p.nr + 2 * p.nrc) {
+          const uint8_t* g;
+          int nd, o;
+          row_src(p, row, g, nd, o);
+#pragma unroll
+          for (int h = 0; h < kPC; h++)
+            if (64 * h + lane < nd) L.st[o + 64 * h + lane] = pre[i][h];
+        }
+      }
+      if (t < p.nr) {
+        const int y = p.ya + t, i = y >> 1;
         int f = (y & 1) ? i + 1 : i - 1;
         f = f < 0 ? 0 : (f > dhc - 1 ? dhc - 1 : f);
         L.rinfo[t][0] = 4 * (t * kFYDW) - jalY;
-        L.rinfo[t][1] = 4 * (kFRows * kFYDW + (i - ilo) * kFCDW) - jalC;
-        L.rinfo[t][2] = 4 * (kFRows * kFYDW + (f - ilo) * kFCDW) - jalC;
-        L.rinfo[t][3] = 4 * (kFRows * kFYDW + kFRows * kFCDW + (i - ilo) * kFCDW) - jalC;
-        L.rinfo[t][4] = 4 * (kFRows * kFYDW + kFRows * kFCDW + (f - ilo) * kFCDW) - jalC;
+        L.rinfo[t][1] = 4 * (kFRows * kFYDW + (i - p.ilo) * kFCDW) - jalC;
+        L.rinfo[t][2] = 4 * (kFRows * kFYDW + (f - p.ilo) * kFCDW) - jalC;
+        L.rinfo[t][3] = 4 * (kFRows * kFYDW + kFRows * kFCDW + (i - p.ilo) * kFCDW) - jalC;
+        L.rinfo[t][4] = 4 * (kFRows * kFYDW + kFRows * kFCDW + (f - p.ilo) * kFCDW) - jalC;
       }
-      __syncthreads();  // DMA landed; previous step's H reads of rgb are done
+    };
+    Step cur = plan_step(r_lo);
+    issue(cur);
+    commit(cur);
+    __syncthreads();
+    for (int ra = r_lo; ra < r_hi; ra += kFRows) {
+      const int nr = cur.nr;
+      const bool more = ra + kFRows < r_hi;
+      const Step nxt = more ? plan_step(ra + kFRows) : cur;
+      if (more) issue(nxt);
       mark(0);
       // B. h2v2 fancy upsampling + ycc->rgb on 4 pixel pairs (8 pixels) per item: chroma columns
       // jg - 4 .. jg + 7 and luma x .. x + 7 come in as aligned dwords (jg = jb + 4g)
@@ -288,6 +334,11 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
           }
         }
       }
+      if (more) {
+        commit(nxt);
+        cur = nxt;
+      }
+      __syncthreads();  // next step's rows staged; this step's H reads of rgb are done
       mark(2);
     }
     if (SDSJ_RS_TIMING && lane == 0)
