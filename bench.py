@@ -37,15 +37,25 @@ STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_unstuf
                  "hpass": ["k_hpass"], "vpass": ["k_vpass"], "resample": ["k_resample", "k_rs420"]}
 
 
-def pmc_traffic(stage: str, batch: int):
-    """HBM bytes per launch of `stage` from the committed PMC summary (FETCH_SIZE + WRITE_SIZE, KB as
-    rocprofv3 reports them, summed over the stage's kernels), if it was collected at this batch size."""
+def engine_lanes(batch: int) -> int:
+    """Lanes the engine splits a batch into (sdsj_engine.hip run_chunk: SDSJ_LANES, default 4, at most 4,
+    at least 256 images per lane).  Each lane dispatches every kernel once per batch."""
+    n = max(1, min(int(os.environ.get("SDSJ_LANES", "4")), 4))
+    while n > 1 and batch < 256 * n:
+        n -= 1
+    return n
+
+
+def pmc_traffic(stage: str, batch: int, lanes: int):
+    """HBM bytes per launch (one lane's dispatch) of `stage` from the committed PMC summary
+    (FETCH_SIZE + WRITE_SIZE, KB as rocprofv3 reports them, summed over the stage's kernels), if it
+    was collected at this batch size and lane count."""
     try:
         with open(PMC_JSON) as f:
             pmc = json.load(f)
     except (OSError, ValueError):
         return None
-    if pmc.get("batch") != batch:
+    if pmc.get("batch") != batch or pmc.get("lanes", 1) != lanes:
         return None
     tot, hit = 0.0, False
     for name, ctr in pmc.get("kernels", {}).items():
@@ -260,11 +270,15 @@ def main():
     mean_in = float(np.mean(t_lens))
     out_bytes = 3 * args.res * args.res * (4 if mixed else 1)
     alg_bytes_per_img = mean_in + out_bytes
+    # Each lane (B / lanes images) launches every stage once per step on its own stream; the stage
+    # times are HIP events around each lane's launches, summed over lanes and steps.  A "launch" below
+    # is one lane's dispatch of the dominant stage: B / lanes images in dom_ms / lanes on average.
+    lanes = engine_lanes(B)
     dom = max(stages, key=stages.get)
-    dom_ms = stages[dom] / args.steps  # mean duration of the dominant kernel per launch (1 launch / step)
-    achieved = B * alg_bytes_per_img / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-    pipeline_ms = sum(stages.values()) / args.steps
-    traffic = pmc_traffic(dom, B)
+    launch_ms = stages[dom] / (args.steps * lanes)
+    launch_bytes = B * alg_bytes_per_img / lanes
+    achieved = launch_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    traffic = pmc_traffic(dom, B, lanes)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -302,10 +316,10 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": (traffic or {}).get("bytes_per_launch"),
                          "traffic_detail": traffic,
-                         "algorithmic_bytes_per_launch": round(B * alg_bytes_per_img),
+                         "algorithmic_bytes_per_launch": round(launch_bytes),
                          "algorithmic_bytes_per_image": round(alg_bytes_per_img, 1),
-                         "pipeline_achieved": round(B * alg_bytes_per_img / (pipeline_ms * 1e-3) / 1e9, 2)
-                         if pipeline_ms > 0 else None},
+                         "launch_ms": round(launch_ms, 4), "images_per_launch": B / lanes, "lanes": lanes,
+                         "pipeline_achieved": round(value * alg_bytes_per_img / 1e9, 2)},
             "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
             "cpu_baseline": cpu,
         }

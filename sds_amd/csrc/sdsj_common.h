@@ -24,6 +24,11 @@ constexpr int kRec = 64;              // block-boundary records kept per subsequ
 constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
 constexpr int kWarmBits = 2000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
+constexpr int kWarmDiv = 3;           // ... or sub_bits / kWarmDiv when that is larger
+// large images: ent_groups = ceil(bits / (kDecodeThreads x kGroupBits)) workgroups (<= kMaxEntGroups)
+// share the subsequences, so one lane's serial decode stays near kGroupBits
+constexpr int kGroupBits = 8192;
+constexpr int kMaxEntGroups = 8;
 constexpr int kUPad = 128;            // zero bytes after each unstuffed stream (bit-reader prefetch)
 constexpr int kMaxSpan = 960;         // source columns per fused-resample tile (LDS row width)
 constexpr int kRingDW = 3072;         // fused-resample ring (dwords): ring_rows x (3072 / ring_rows) columns
@@ -133,8 +138,8 @@ struct ImgDesc {
   // entropy-relative index of its last FF byte
   int32_t scan_end_code;
   int64_t scan_end_raw;
-  int32_t rgb_pitch;  // pixels per row of the RGB rows the unfused passes read (frames: the frame width)
-  int32_t pad2;
+  int32_t rgb_pitch;   // pixels per row of the RGB rows the unfused passes read (frames: the frame width)
+  int32_t ent_groups;  // workgroups sharing the image's subsequences in the spec / write passes
 };
 
 // Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).
@@ -201,6 +206,7 @@ enum Route : int32_t {
   kRtGeneric,      // k_resample
   kRt3, kRt5, kRt7, kRt9, kRt11,  // k_rs420<KT>
   kRtEnt10, kRtEnt11,             // entropy kernels by lookahead width
+  kRtEnt11M,                      // LB = 11 images decoded by several workgroups (ent_groups > 1)
   kNumRoutes
 };
 constexpr int kRouteSlots = 16;  // counts [0, kNumRoutes), the rest zero

@@ -514,18 +514,23 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
 
 // Re-decode of subsequence S from its corrected entry (new_entry_*) to its end -- the first block
 // boundary at or after end_bit, as in the speculative pass -- giving the exact exit state, block
-// count and DC sums in new_*.  A lean loop like the speculative pass's: the few lanes running such
-// tasks are bound by per-symbol latency, so a full re-decode beats stopping early at a merge point
-// with the speculative path (which needs per-block record bookkeeping).
+// count and DC sums in new_*.  A lean loop like the speculative pass's; every kMergeBits of progress
+// a lane that sits on a block boundary looks it up among the speculative pass's records (binary
+// search): the same position and MCU block means the two paths have merged, and the rest of the
+// speculative result is exact (large subsequences stop there instead of decoding to their end).
+constexpr uint32_t kMergeBits = 768;
 constexpr int kSyncQ = kQ;  // (a deeper queue measured slower: the pull shifts it)
 
 template <int LB, class TT>
-__device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S) {
+__device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const SyncRec* rec) {
   const uint32_t end = S.end_bit;
+  const int nrec = S.nrec;
   BitsQ<kSyncQ> b;
   bits_init(b, src, S.new_entry_p, S.lim_bit);
   int blk = S.new_entry_bz >> 8, z = S.new_entry_bz & 0xFF;
   int nblk = 0, bad = 0, nsym = 0, d0 = 0, d1 = 0, d2 = 0;
+  uint32_t next_chk = nrec > 0 ? b.pos + kMergeBits : 0xFFFFFFFFu;
+  bool merged = false;
   int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
   bool run = b.pos < end || z != 0;
   while (__builtin_amdgcn_ballot_w64(run)) {
@@ -549,17 +554,43 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           run = b.pos < end || z != 0;
         }
       }
+      if (run && z == 0 && b.pos >= next_chk) {
+        // first record at or after b.pos; a record there for the block just completed = merged
+        int lo = 0, hi = nrec;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (rec[mid].p < b.pos) lo = mid + 1;
+          else hi = mid;
+        }
+        const int done_blk = blk == 0 ? K.bpm - 1 : blk - 1;
+        if (lo < nrec && rec[lo].p == b.pos && rec[lo].blk == done_blk) {
+          int q0 = 0, q1 = 0, q2 = 0;  // speculative DC sums up to and including that block
+          for (int k = 0; k <= lo; k++) add_dc(ctx_c(K, rec[k].blk), rec[k].dc, q0, q1, q2);
+          S.new_exit_p = S.spec_exit_p;
+          S.new_exit_bz = S.spec_exit_bz;
+          S.new_nblk = nblk + S.spec_nblk - (lo + 1);
+          S.new_dc[0] = d0 + S.spec_dc[0] - q0;
+          S.new_dc[1] = d1 + S.spec_dc[1] - q1;
+          S.new_dc[2] = d2 + S.spec_dc[2] - q2;
+          merged = true;
+          run = false;
+        } else {
+          next_chk = lo < nrec ? b.pos + kMergeBits : 0xFFFFFFFFu;
+        }
+      }
       if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kSpecGroup + 1)) ||
           !__builtin_amdgcn_ballot_w64(run))
         break;
     }
   }
-  S.new_exit_p = b.pos;
-  S.new_exit_bz = (uint16_t)((blk << 8) | z);
-  S.new_nblk = nblk;
-  S.new_dc[0] = d0;
-  S.new_dc[1] = d1;
-  S.new_dc[2] = d2;
+  if (!merged) {
+    S.new_exit_p = b.pos;
+    S.new_exit_bz = (uint16_t)((blk << 8) | z);
+    S.new_nblk = nblk;
+    S.new_dc[0] = d0;
+    S.new_dc[1] = d1;
+    S.new_dc[2] = d2;
+  }
   return nsym;
 }
 
@@ -684,7 +715,7 @@ __device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* s
 }
 
 template <int LB>
-__device__ void entspec_image(int img, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+__device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                               uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
@@ -744,7 +775,9 @@ __device__ void entspec_image(int img, ImgDesc* __restrict__ descs, const EntTab
   if (t == 0) L.t0 = __builtin_amdgcn_s_memtime();
   if ((t & 63) == 0) L.wmax[t >> 6] = 0;
   __syncthreads();
-  for (int j = t; j < nsub; j += kEntThreads) {
+  // this workgroup's share of the subsequences (every group computes the same layout above)
+  const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
+  for (int j = j0 + t; j < j1; j += kEntThreads) {
     const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, (uint32_t)sv.lo[sub[j].seg] * 8u,
                                 (uint32_t)d->warm_bits);
     nsym_spec += k;
@@ -757,8 +790,8 @@ __device__ void entspec_image(int img, ImgDesc* __restrict__ descs, const EntTab
   }
   atomicAdd(&L.sym[0], nsym_spec);
   __syncthreads();
-  if (t == 0) {
-    d->nsub = nsub;
+  if (t == 0) d->nsub = nsub;
+  if (t == 0 && grp == 0) {  // statistics: the first group's share
     d->sym_spec = (int64_t)L.sym[0];
     d->t_spec = (int64_t)(L.t1 - L.t0);
     d->it_spec = (int64_t)L.it[0];
@@ -827,8 +860,14 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       if (ntask > kMaxTasks) ntask = kMaxTasks;  // the rest are picked up by the next round
       __syncthreads();
       if (ntask == 0) break;
-      if (t == 0) L.rounds++;
-      for (int i = t; i < ntask; i += NT) nsym_sync += sync_full<kSyncLB>(L.T, K, src, sub[L.u.task[0][i]]);
+      if (t == 0) {
+        L.rounds++;
+        L.stages += ntask;  // (statistics: tasks over all rounds)
+      }
+      for (int i = t; i < ntask; i += NT) {
+        const int j = L.u.task[0][i];
+        nsym_sync += sync_full<kSyncLB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec);
+      }
       __syncthreads();
       // commit every task of the round (entries first: they were read from cur_exit of j-1)
       for (int i = t; i < ntask; i += NT) {
@@ -922,7 +961,7 @@ struct LdsWrite {
 };
 
 template <int LB>
-__device__ void entwrite_image(int img, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+__device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                                uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
@@ -953,9 +992,10 @@ __device__ void entwrite_image(int img, ImgDesc* __restrict__ descs, const EntTa
   int bad = 0;
   unsigned long long nsym = 0, witers = 0;
 
-  for (int jb = 0; jb < nsub; jb += kEntThreads) {  // uniform trip count for the whole workgroup
+  const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
+  for (int jb = j0; jb < j1; jb += kEntThreads) {  // uniform trip count for the whole workgroup
     const int j = jb + t;
-    const bool active = j < nsub;
+    const bool active = j < j1;
     Bits b;
     int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, sdc = 0, sac = 0;
     int64_t g = 0, gend = 0;
@@ -1059,61 +1099,71 @@ __device__ void entwrite_image(int img, ImgDesc* __restrict__ descs, const EntTa
   atomicAdd(&L.sym, nsym);
   if (lane == 0) atomicAdd(&L.it, 64ull * witers);
   __syncthreads();
-  if (t == 0) {
+  if (t == 0 && grp == 0) {  // statistics: the first group's share
     d->sym_write = (int64_t)L.sym;
     d->it_write = (int64_t)L.it;
     d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - L.t0);
   }
 }
 
-template <int LB, int PHASE>
-__device__ __forceinline__ void ent_phase(int img, ImgDesc* descs, const EntTables* tables, uint8_t* scratch) {
-  if (PHASE == 0) entspec_image<LB>(img, descs, tables, scratch);
-  else if (PHASE == 1) entsync_image<LB, kSyncThreads>(img, descs, tables, scratch);
-  else entwrite_image<LB>(img, descs, tables, scratch);
+template <int LB, int PHASE, int NTS = kSyncThreads>
+__device__ __forceinline__ void ent_phase(int img, int grp, ImgDesc* descs, const EntTables* tables, uint8_t* scratch) {
+  if (PHASE == 0) entspec_image<LB>(img, grp, descs, tables, scratch);
+  else if (PHASE == 1) entsync_image<LB, NTS>(img, descs, tables, scratch);
+  else entwrite_image<LB>(img, grp, descs, tables, scratch);
 }
 
-// The entropy kernels take images from their route's list.  The main route (LB = 11) runs one
-// workgroup per list entry (grid = batch size, surplus workgroups exit at once); the rare LB = 10
-// route strides a small grid over its list.
-template <int LB, int PHASE>  // 0 spec, 1 sync + scan, 2 write
+// The entropy kernels take images from a route list.  MODE 0: one workgroup per list entry (grid =
+// batch size, surplus workgroups exit at once) -- the main route (LB = 11, one group per image).
+// MODE 1: a small grid strides over the list and runs each image's groups in turn (LB = 10, and the
+// sync pass of multi-group images).  MODE 2: grid.y = kMaxEntGroups, workgroup y takes group y of
+// each image it strides over (LB = 11 images with ent_groups > 1).  The sync pass is per image.
+template <int LB, int PHASE, int RT, int MODE, int NTS = kSyncThreads>
 __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables, uint8_t* scratch, int32_t* routes,
                                          int cap) {
-  const int r = LB == 11 ? kRtEnt11 : kRtEnt10;
-  const int cnt = routes[r];
-  const int32_t* list = route_list(routes, cap, r);
-  if (LB == 11) {
+  const int cnt = routes[RT];
+  const int32_t* list = route_list(routes, cap, RT);
+  if (MODE == 0) {
     if ((int)blockIdx.x >= cnt) return;
-    ent_phase<LB, PHASE>(list[blockIdx.x], descs, tables, scratch);
+    ent_phase<LB, PHASE, NTS>(list[blockIdx.x], 0, descs, tables, scratch);
     return;
   }
   for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
-    ent_phase<LB, PHASE>(list[li], descs, tables, scratch);
+    const int img = list[li];
+    const int G = PHASE == 1 ? 1 : descs[img].ent_groups;
+    if (MODE == 2) {
+      if ((int)blockIdx.y < G) ent_phase<LB, PHASE, NTS>(img, blockIdx.y, descs, tables, scratch);
+    } else {
+      for (int grp = 0; grp < G; grp++) {
+        ent_phase<LB, PHASE, NTS>(img, grp, descs, tables, scratch);
+        __syncthreads();  // LDS reuse by the next group
+      }
+    }
     __syncthreads();  // LDS reuse by the next image
   }
 }
 
 // k_entspec: subsequence layout + speculative pass (warm-up, records); k_entsync: sync rounds +
 // segmented scan, decode tables built only when some entry disagrees with its predecessor's exit.
-template <int LB>
+template <int LB, int RT, int MODE>
 __global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(5)))
 k_entspec(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, uint8_t* __restrict__ scratch,
           int32_t* __restrict__ routes, int cap) {
-  ent_feed<LB, 0>(descs, tables, scratch, routes, cap);
+  ent_feed<LB, 0, RT, MODE>(descs, tables, scratch, routes, cap);
 }
 
-template <int LB>
-__global__ void __launch_bounds__(kSyncThreads) k_entsync(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
-                                                         uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
-                                                         int cap) {
-  ent_feed<LB, 1>(descs, tables, scratch, routes, cap);
+// (multi-group images have several times the sync tasks: a 4-wave workgroup runs them)
+template <int LB, int RT, int MODE, int NTS>
+__global__ void __launch_bounds__(NTS) k_entsync(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+                                                 uint8_t* __restrict__ scratch, int32_t* __restrict__ routes, int cap) {
+  ent_feed<LB, 1, RT, MODE, NTS>(descs, tables, scratch, routes, cap);
 }
 
-template <int LB>
+template <int LB, int RT, int MODE>
 __global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                                                           uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
                                                           int cap) {
-  ent_feed<LB, 2>(descs, tables, scratch, routes, cap);
+  ent_feed<LB, 2, RT, MODE>(descs, tables, scratch, routes, cap);
 }
 
 size_t enttab_bytes() { return sizeof(EntTables); }
@@ -1123,11 +1173,18 @@ hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* e
   const int g = n;  // one workgroup per image on the main route
   EntTables* tables = static_cast<EntTables*>(etab);
   hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
-  hipLaunchKernelGGL(k_entspec<11>, dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL(k_entspec<10>, dim3(g < 256 ? g : 256), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  const int gs = g < 256 ? g : 256, gm = g < 192 ? g : 192;
+  hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 2>), dim3(gm, kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables, scratch,
+                     routes, cap);
+  hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   if (after_spec) (void)hipEventRecord(after_spec, s);
-  hipLaunchKernelGGL(k_entsync<11>, dim3(g), dim3(kSyncThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL(k_entsync<10>, dim3(g < 256 ? g : 256), dim3(kSyncThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL((k_entsync<11, kRtEnt11, 0, kSyncThreads>), dim3(g), dim3(kSyncThreads), 0, s, descs, tables, scratch,
+                     routes, cap);
+  hipLaunchKernelGGL((k_entsync<11, kRtEnt11M, 1, kEntThreads>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch,
+                     routes, cap);
+  hipLaunchKernelGGL((k_entsync<10, kRtEnt10, 1, kSyncThreads>), dim3(gs), dim3(kSyncThreads), 0, s, descs, tables, scratch,
+                     routes, cap);
   return hipGetLastError();
 }
 
@@ -1135,8 +1192,11 @@ hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scr
                            hipStream_t s) {
   const int g = n;  // one workgroup per image on the main route
   const EntTables* tables = static_cast<const EntTables*>(etab);
-  hipLaunchKernelGGL(k_entwrite<11>, dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL(k_entwrite<10>, dim3(g < 256 ? g : 256), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  const int gs = g < 256 ? g : 256, gm = g < 192 ? g : 192;
+  hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 2>), dim3(gm, kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables, scratch,
+                     routes, cap);
+  hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 

@@ -124,9 +124,21 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
       d->comp[1].rv == 2 && d->comp[2].rh == 2 && d->comp[2].rv == 2 && d->comp[1].dw > 2 &&
       d->comp[2].dw == d->comp[1].dw && d->comp[2].dh == d->comp[1].dh)
     d->rs_fast = d->ksh;
-  d->sub_bits = (int32_t)align_up((d->entropy_len * 8 + kDecodeThreads - 1) / kDecodeThreads, 32);
+  {
+    const int64_t bits = d->entropy_len * 8, per_group = (int64_t)kDecodeThreads * kGroupBits;
+    int64_t g = (bits + per_group - 1) / per_group;
+    g = g < 1 ? 1 : (g > kMaxEntGroups ? kMaxEntGroups : g);
+    d->ent_groups = frames ? 1 : (int32_t)g;
+    const int64_t lanes = (int64_t)kDecodeThreads * d->ent_groups;
+    d->sub_bits = (int32_t)align_up((bits + lanes - 1) / lanes, 32);
+  }
   if (d->sub_bits < kMinSubBits) d->sub_bits = kMinSubBits;
-  d->warm_bits = d->sub_bits * 3 / 2 < kWarmBits ? d->sub_bits * 3 / 2 : kWarmBits;
+  // warm-up: kWarmBits, or sub_bits / kWarmDiv for long subsequences (large images: a few percent
+  // more speculative work removes nearly every sync task, each of which is a serial re-decode)
+  {
+    const int64_t w = d->sub_bits / kWarmDiv > kWarmBits ? d->sub_bits / kWarmDiv : kWarmBits;
+    d->warm_bits = (int)(d->sub_bits * 3 / 2 < w ? d->sub_bits * 3 / 2 : w);
+  }
   d->nsub_cap = (int32_t)((d->entropy_len * 8 + d->sub_bits - 1) / d->sub_bits) + d->nseg + 1;
   // scratch layout (relative offsets; k_plan adds the image base)
   int64_t o = 0;
@@ -296,7 +308,7 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
             for (int q = 0; q < ns; q++) seen |= keys[q] == key;
             if (!seen) keys[ns++] = key;
           }
-        const int re = ns <= 4 ? kRtEnt11 : kRtEnt10;
+        const int re = ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
         int32_t* lst = routes + kRouteSlots + re * cap;
         lst[atomicAdd(&rcnt[re], 1)] = i;
         if (d.geo != kGeoZeros) {

@@ -21,7 +21,7 @@ wr = np.array([d.sym_write for d in descs])
 ns = np.array([d.nsub for d in descs])
 print(f"images={n} status_ok={(st == 0).all()} nsub mean={ns.mean():.1f} bits/sub={descs[0].sub_bits}")
 st = np.array([d.pad0 for d in descs])
-print(f"sync rounds: mean={r.mean():.2f} max={r.max()} hist={np.bincount(r).tolist()}; stages mean={st.mean():.2f}")
+print(f"sync rounds: mean={r.mean():.2f} max={r.max()} hist={np.bincount(r).tolist()}; tasks mean={st.mean():.2f}")
 print(f"symbols/image: spec={sp.mean():.0f} sync={sy.mean():.0f} write={wr.mean():.0f} "
       f"-> {(sp + sy + wr).mean() / wr.mean():.2f}x the write pass")
 ts = np.array([d.t_spec for d in descs]); ty = np.array([d.t_sync for d in descs]); tc = np.array([d.t_scan for d in descs])

@@ -14,4 +14,4 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   rm -rf gpurun_out/pmc_$i
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_$i -o p -- $B > gpurun_out/pmc_$i.log 2>&1
 done
-python3 tools/pmc_summary.py gpurun_out 4096 > gpurun_out/pmc.json
+python3 tools/pmc_summary.py gpurun_out 4096 "$(python3 -c 'import bench; print(bench.engine_lanes(4096))')" > gpurun_out/pmc.json
