@@ -480,9 +480,9 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           const bool isdc = z == 0;
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
           nsym++;
-          dcd = isdc ? val : dcd;
-          add_dc(c, isdc ? val : 0, d0, d1, d2);
+          dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           if (next_z(z, s, r)) {
+            add_dc(c, dcd, d0, d1, d2);
             if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
             nrec++;
             nblk++;
@@ -528,7 +528,7 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   BitsQ<kSyncQ> b;
   bits_init(b, src, S.new_entry_p, S.lim_bit);
   int blk = S.new_entry_bz >> 8, z = S.new_entry_bz & 0xFF;
-  int nblk = 0, bad = 0, nsym = 0, d0 = 0, d1 = 0, d2 = 0;
+  int nblk = 0, bad = 0, nsym = 0, d0 = 0, d1 = 0, d2 = 0, dcd = 0;
   uint32_t next_chk = nrec > 0 ? b.pos + kMergeBits : 0xFFFFFFFFu;
   bool merged = false;
   int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
@@ -543,8 +543,9 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           const bool isdc = z == 0;
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, sy, r, val, bad);
           nsym++;
-          add_dc(c, isdc ? val : 0, d0, d1, d2);
+          dcd = isdc ? val : dcd;
           if (next_z(z, sy, r)) {
+            add_dc(c, dcd, d0, d1, d2);
             nblk++;
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
             c = ctx_c(K, blk);
@@ -997,7 +998,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     const int j = jb + t;
     const bool active = j < j1;
     Bits b;
-    int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, sdc = 0, sac = 0;
+    int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, pc = 0, sdc = 0, sac = 0;
     int64_t g = 0, gend = 0;
     uint32_t end_bit = 0, lim = 0;
     int s_int = 0;
@@ -1015,6 +1016,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       blk = S.entry_bz >> 8;
       z = S.entry_bz & 0xFF;
       c = ctx_c(K, blk);
+      pc = c == 0 ? p0 : (c == 1 ? p1 : p2);  // the current block's component predictor
       sdc = ctx_dc(K, blk);
       sac = ctx_ac(K, blk);
       writing = z == 0;
@@ -1042,18 +1044,18 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           nsym++;
           bad |= sb;
           // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
-          const int add = isdc ? val : 0;
-          p0 += c == 0 ? add : 0;
-          p1 += c == 1 ? add : 0;
-          p2 += c == 2 ? add : 0;
-          const int pv = c == 0 ? p0 : (c == 1 ? p1 : p2);
+          pc += isdc ? val : 0;
           const int wpos = isdc ? 0 : (int)T.nat[z + r];
-          L.stage[((writing && (isdc || s)) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pv : val);
+          L.stage[((writing && (isdc || s)) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
           if (next_z(z, s, r)) {
             ready = writing;
             gdone = (uint32_t)g;
+            p0 = c == 0 ? pc : p0;  // the component's predictor back, the next block's out
+            p1 = c == 1 ? pc : p1;
+            p2 = c == 2 ? pc : p2;
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
             c = ctx_c(K, blk);
+            pc = c == 0 ? p0 : (c == 1 ? p1 : p2);
             sdc = ctx_dc(K, blk);
             sac = ctx_ac(K, blk);
             g++;
