@@ -766,6 +766,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   __shared__ int32_t qt[kMaxComp][64];
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
   __shared__ int32_t gstart[kMaxComp + 1], ngx[kMaxComp], cbw[kMaxComp], ch_[kMaxComp], cv_[kMaxComp], cpitch[kMaxComp];
+  __shared__ int32_t cgx0[kMaxComp], cby0[kMaxComp];  // first 8-block group column / block row needed
   __shared__ float rngx[kMaxComp], rch[kMaxComp], rcv[kMaxComp];  // reciprocals for the exact quotients below
   __shared__ int64_t cplane[kMaxComp];
   const int t = threadIdx.x;
@@ -773,11 +774,23 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   for (int i = t; i < ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][i % 64];
   if (t < bpm) binv[d->blk_comp[t]][d->blk_dy[t] * 4 + d->blk_dx[t]] = t;
   if (t == 0) {
+    // only the blocks whose pixels the colour/resample passes read: the source rectangle
+    // [src_x0, src_x0 + src_w) x [src_y0, src_y1) in each component's sampling, widened by one
+    // sample for the fancy upsampling's neighbours (the crop drops the rest of the image)
+    const int x0 = d->src_x0, x1 = d->src_x0 + d->src_w, y0 = d->src_y0, y1 = d->src_y1;
     int acc = 0;
     for (int c = 0; c < ncomp; c++) {
       const CompDesc& cd = d->comp[c];
+      const int rh = ncomp == 1 ? 1 : d->hmax / cd.h, rv = ncomp == 1 ? 1 : d->vmax / cd.v;
+      int cx0 = x0 / rh - 1, cx1 = (x1 - 1) / rh + 1, cy0 = y0 / rv - 1, cy1 = (y1 - 1) / rv + 1;
+      cx0 = cx0 < 0 ? 0 : cx0;
+      cy0 = cy0 < 0 ? 0 : cy0;
+      cx1 = cx1 > cd.bw * 8 - 1 ? cd.bw * 8 - 1 : cx1;
+      cy1 = cy1 > cd.bh * 8 - 1 ? cd.bh * 8 - 1 : cy1;
       gstart[c] = acc;
-      ngx[c] = (cd.bw + 7) >> 3;
+      cgx0[c] = cx0 >> 6;
+      ngx[c] = (cx1 >> 6) - cgx0[c] + 1;
+      cby0[c] = cy0 >> 3;
       cbw[c] = cd.bw;
       ch_[c] = ncomp == 1 ? 1 : cd.h;
       cv_[c] = ncomp == 1 ? 1 : cd.v;
@@ -786,7 +799,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
       rngx[c] = 1.0f / (float)ngx[c];
       rch[c] = 1.0f / (float)ch_[c];
       rcv[c] = 1.0f / (float)cv_[c];
-      acc += ngx[c] * cd.bh;
+      acc += x1 > x0 && y1 > y0 ? ngx[c] * ((cy1 >> 3) - cby0[c] + 1) : 0;
     }
     gstart[ncomp] = acc;
   }
@@ -818,8 +831,9 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   auto locate = [&](int grp, int& c, int& by, int& bx, int& g) {
     c = ncomp > 1 && grp >= gstart[1] ? (ncomp > 2 && grp >= gstart[2] ? 2 : 1) : 0;
     const int local = grp - gstart[c];
-    by = qdiv(local, ngx[c], rngx[c]);
-    bx = (local - by * ngx[c]) * 8 + lb;
+    const int byl = qdiv(local, ngx[c], rngx[c]);
+    by = cby0[c] + byl;
+    bx = (cgx0[c] + local - byl * ngx[c]) * 8 + lb;
     g = -1;
     if (grp < ngroups && bx < cbw[c]) {
       const int h = ch_[c], v = cv_[c];
