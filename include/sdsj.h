@@ -111,6 +111,27 @@ int sdsj_decode_resize_batch_device(sdsj_engine* eng, int n, const uint8_t* d_bl
                                     const int32_t* d_lengths, const sdsj_op* op, const uint8_t* d_flip,
                                     void* d_out, int32_t* d_status, void* hip_stream);
 
+/* Asynchronous host path with double-buffered pinned staging (downloader /
+ * host cache -> pinned staging -> H2D -> decode, overlapped; config 5).  Up to SDSJ_SLOTS batches are
+ * in flight.  A submit stages its batch into the slot's pinned buffer -- while the GPU still decodes
+ * the previous batch --, copies it H2D on an engine-owned copy stream and enqueues the decode on
+ * `hip_stream` behind that copy, then returns.  sdsj_wait_batch blocks until the slot's batch is done
+ * and fills its per-sample status.  `out` (device, as in sdsj_decode_resize_batch) must stay untouched
+ * until then.  n <= the engine's max_batch.  Submitting to a slot still in flight waits for it first
+ * (its statuses are then dropped).
+ *   sdsj_submit_batch : encoded bytes in host memory, borrowed for the call only
+ *                       (same samples as sdsj_decode_resize_batch)
+ *   sdsj_submit_files : n file paths read straight into the slot's pinned buffer -- what
+ *                       LoadFromDiskTransform (presets.py:613-626) does with the local cache that
+ *                       run_downloading_task (downloader.py:117-131) fills.  A file that cannot be
+ *                       read is reported per sample as SDSJ_EINVAL. */
+#define SDSJ_SLOTS 2
+int sdsj_submit_batch(sdsj_engine* eng, int slot, int n, const uint8_t* const* jpg, const size_t* len,
+                      const sdsj_op* op, const uint8_t* flip, void* out, void* hip_stream);
+int sdsj_submit_files(sdsj_engine* eng, int slot, int n, const char* const* paths, const sdsj_op* op,
+                      const uint8_t* flip, void* out, void* hip_stream);
+int sdsj_wait_batch(sdsj_engine* eng, int slot, int32_t* status);
+
 /* Crop + resize (+flip, +normalise) of n raw RGB frames already in DEVICE memory -- the video path
  * (sds/transforms/presets.py:121-135 ResizeVideoTransform + ConvertVideoToByteTensorTransform ->
  * functional.py:42-86 lean_resize_frames on the frames PyAV decoded).  Frame i is uint8 HWC

@@ -31,8 +31,10 @@ LAYOUT_CHW, LAYOUT_HWC = 0, 1
 EXPORTS = [
     "sdsj_abi_version", "sdsj_probe", "sdsj_engine_create", "sdsj_engine_destroy", "sdsj_decode_resize_batch",
     "sdsj_decode_resize_batch_device", "sdsj_engine_set_timing", "sdsj_engine_stage_times", "sdsj_last_error",
-    "sdsj_stage_name", "sdsj_engine_debug_buffers", "sdsj_resize_frames_device",
+    "sdsj_stage_name", "sdsj_engine_debug_buffers", "sdsj_resize_frames_device", "sdsj_submit_batch",
+    "sdsj_submit_files", "sdsj_wait_batch",
 ]
+SLOTS = 2  # SDSJ_SLOTS: batches in flight on the asynchronous host path
 
 
 class NativeLibraryError(RuntimeError):
@@ -87,6 +89,11 @@ def load() -> ctypes.CDLL:
                                                         vp, vp]
         lib.sdsj_resize_frames_device.argtypes = [vp, ctypes.c_int, vp, i32, i32, i64, ctypes.POINTER(SdsjOp), vp, vp,
                                                   vp, vp]
+        lib.sdsj_submit_batch.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                          ctypes.POINTER(sz), ctypes.POINTER(SdsjOp), vp, vp, vp]
+        lib.sdsj_submit_files.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                          ctypes.POINTER(SdsjOp), vp, vp, vp]
+        lib.sdsj_wait_batch.argtypes = [vp, ctypes.c_int, ctypes.POINTER(i32)]
         lib.sdsj_engine_set_timing.argtypes = [vp, ctypes.c_int]
         lib.sdsj_engine_stage_times.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_int)]

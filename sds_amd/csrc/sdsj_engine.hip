@@ -10,8 +10,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sdsj_common.h"
@@ -63,6 +69,21 @@ struct sdsj_engine {
   int32_t* d_status = nullptr;
   int32_t* h_status = nullptr;
   int io_cap = 0;
+  // asynchronous host path (sdsj_submit_*): per-slot pinned staging, device inputs and events
+  struct Slot {
+    uint8_t* h_stage = nullptr;
+    uint8_t* d_blob = nullptr;
+    size_t bytes_cap = 0;
+    int64_t *h_offsets = nullptr, *d_offsets = nullptr;
+    int32_t *h_lengths = nullptr, *d_lengths = nullptr;
+    uint8_t *h_flip = nullptr, *d_flip = nullptr;
+    int32_t *h_status = nullptr, *d_status = nullptr;
+    int32_t* h_pre = nullptr;  // host-side per-sample status (unreadable files)
+    int cap = 0, n = 0;
+    bool pending = false;
+    hipEvent_t ev_h2d = nullptr, ev_done = nullptr;
+  } slots[SDSJ_SLOTS];
+  hipStream_t copy_stream = nullptr;
   // timing: one event set per chunk launched since the last sdsj_engine_set_timing(e, 1)
   bool timing = false;
   std::vector<std::vector<hipEvent_t>> ev_sets;
@@ -247,11 +268,245 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
   return SDSJ_OK;
 }
 
+// -- asynchronous host path (sdsj_submit_*) ---------------------------------------------------
+using Slot = sdsj_engine::Slot;
+
+// Host staging (copies / file reads into pinned memory, header planning) is split over threads:
+// a single core's memcpy bandwidth would otherwise bound the pipelined host path.
+int stage_threads() {
+  static const int k = [] {
+    const char* v = getenv("SDSJ_STAGE_THREADS");
+    const int hw = (int)std::thread::hardware_concurrency();
+    const int d = std::max(1, std::min(8, hw > 0 ? hw : 1));
+    return v ? std::max(1, atoi(v)) : d;
+  }();
+  return k;
+}
+
+template <class F>
+void parallel_for(int n, F fn) {
+  const int nt = std::min(stage_threads(), std::max(1, n / 16));
+  if (nt <= 1) {
+    fn(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (int k = 1; k < nt; k++) th.emplace_back(fn, (int)((int64_t)n * k / nt), (int)((int64_t)n * (k + 1) / nt));
+  fn(0, (int)((int64_t)n / nt));
+  for (auto& t : th) t.join();
+}
+
+void slot_free(Slot& sl) {
+  (void)hipHostFree(sl.h_stage);
+  (void)hipFree(sl.d_blob);
+  (void)hipHostFree(sl.h_offsets);
+  (void)hipFree(sl.d_offsets);
+  (void)hipHostFree(sl.h_lengths);
+  (void)hipFree(sl.d_lengths);
+  (void)hipHostFree(sl.h_flip);
+  (void)hipFree(sl.d_flip);
+  (void)hipHostFree(sl.h_status);
+  (void)hipFree(sl.d_status);
+  free(sl.h_pre);
+  if (sl.ev_h2d) (void)hipEventDestroy(sl.ev_h2d);
+  if (sl.ev_done) (void)hipEventDestroy(sl.ev_done);
+  sl = Slot();
+}
+
+// Waits for the slot's previous batch (its pinned and device buffers are then free) and sizes the
+// buffers for n samples / `bytes` staged bytes.
+int slot_reserve(sdsj_engine* e, Slot& sl, int n, size_t bytes) {
+  if (sl.pending) {
+    SDSJ_HIP(e, hipEventSynchronize(sl.ev_done));
+    sl.pending = false;
+  }
+  if (!e->copy_stream) SDSJ_HIP(e, hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+  if (!sl.ev_done) {
+    SDSJ_HIP(e, hipEventCreateWithFlags(&sl.ev_h2d, hipEventDisableTiming));
+    SDSJ_HIP(e, hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
+  }
+  if (n > sl.cap) {
+    const int cap = std::max(n, 64);
+    (void)hipHostFree(sl.h_offsets), (void)hipFree(sl.d_offsets), (void)hipHostFree(sl.h_lengths);
+    (void)hipFree(sl.d_lengths), (void)hipHostFree(sl.h_flip), (void)hipFree(sl.d_flip);
+    (void)hipHostFree(sl.h_status), (void)hipFree(sl.d_status), free(sl.h_pre);
+    sl.h_pre = nullptr;
+    sl.cap = 0;
+    SDSJ_HIP(e, hipHostMalloc(&sl.h_offsets, sizeof(int64_t) * cap));
+    SDSJ_HIP(e, hipMalloc(&sl.d_offsets, sizeof(int64_t) * cap));
+    SDSJ_HIP(e, hipHostMalloc(&sl.h_lengths, sizeof(int32_t) * cap));
+    SDSJ_HIP(e, hipMalloc(&sl.d_lengths, sizeof(int32_t) * cap));
+    SDSJ_HIP(e, hipHostMalloc(&sl.h_flip, cap));
+    SDSJ_HIP(e, hipMalloc(&sl.d_flip, cap));
+    SDSJ_HIP(e, hipHostMalloc(&sl.h_status, sizeof(int32_t) * cap));
+    SDSJ_HIP(e, hipMalloc(&sl.d_status, sizeof(int32_t) * cap));
+    sl.h_pre = static_cast<int32_t*>(malloc(sizeof(int32_t) * cap));
+    if (!sl.h_pre) return fail(e, SDSJ_ENOMEM, "host allocation failed");
+    sl.cap = cap;
+  }
+  if (bytes > sl.bytes_cap) {
+    (void)hipHostFree(sl.h_stage);
+    (void)hipFree(sl.d_blob);
+    sl.h_stage = nullptr;
+    sl.d_blob = nullptr;
+    sl.bytes_cap = 0;
+    const size_t cap = std::max<size_t>(bytes * 3 / 2, 1 << 20);
+    SDSJ_HIP(e, hipHostMalloc(&sl.h_stage, cap));
+    SDSJ_HIP(e, hipMalloc(&sl.d_blob, cap));
+    sl.bytes_cap = cap;
+  }
+  return SDSJ_OK;
+}
+
+// The staged batch: scratch sized from host planning, H2D on the copy stream, the decode on `s`
+// behind that copy, status D2H into pinned memory, completion event.
+int slot_launch(sdsj_engine* e, Slot& sl, int n, size_t bytes, const sdsj_op& op, void* out, hipStream_t s) {
+  std::vector<int64_t> needs(n, 0);
+  parallel_for(n, [&](int i0, int i1) {
+    for (int i = i0; i < i1; i++) {
+      if (sl.h_pre[i] != SDSJ_OK) continue;
+      int st = SDSJ_OK;
+      const int64_t ni = host_plan_need(sl.h_stage + sl.h_offsets[i], sl.h_lengths[i], op, &st);
+      if (st == SDSJ_OK) needs[i] = align_up(ni, 256);
+    }
+  });
+  int64_t need = 0;
+  for (int i = 0; i < n; i++) need += needs[i];
+  if (need > e->capacity || !e->scratch) {
+    if (e->scratch && !e->grow) return fail(e, SDSJ_ECAPACITY, "batch exceeds the configured scratch capacity");
+    SDSJ_HIP(e, hipStreamSynchronize(s));
+    const int st = ensure_scratch(e, need);
+    if (st != SDSJ_OK) return st;
+  }
+  hipStream_t cs = e->copy_stream;
+  SDSJ_HIP(e, hipMemcpyAsync(sl.d_blob, sl.h_stage, bytes, hipMemcpyHostToDevice, cs));
+  SDSJ_HIP(e, hipMemcpyAsync(sl.d_offsets, sl.h_offsets, sizeof(int64_t) * n, hipMemcpyHostToDevice, cs));
+  SDSJ_HIP(e, hipMemcpyAsync(sl.d_lengths, sl.h_lengths, sizeof(int32_t) * n, hipMemcpyHostToDevice, cs));
+  SDSJ_HIP(e, hipMemcpyAsync(sl.d_flip, sl.h_flip, n, hipMemcpyHostToDevice, cs));
+  SDSJ_HIP(e, hipEventRecord(sl.ev_h2d, cs));
+  SDSJ_HIP(e, hipStreamWaitEvent(s, sl.ev_h2d, 0));
+  const int rc = run_chunk(e, n, sl.d_blob, sl.d_offsets, sl.d_lengths, op, sl.d_flip, out, sl.d_status, s);
+  if (rc != SDSJ_OK) return rc;
+  SDSJ_HIP(e, hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
+  SDSJ_HIP(e, hipEventRecord(sl.ev_done, s));
+  sl.n = n;
+  sl.pending = true;
+  return SDSJ_OK;
+}
+
+int64_t file_size(const char* path) {
+  struct stat sb;
+  if (!path || stat(path, &sb) != 0 || !S_ISREG(sb.st_mode)) return -1;
+  return (int64_t)sb.st_size;
+}
+
+// Reads exactly `size` bytes of `path` into dst; false on any error or a short file.
+bool read_file(const char* path, uint8_t* dst, int64_t size) {
+  const int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  int64_t got = 0;
+  while (got < size) {
+    const ssize_t r = read(fd, dst + got, (size_t)std::min<int64_t>(size - got, 1 << 30));
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) break;
+    got += r;
+  }
+  close(fd);
+  return got == size;
+}
+
 }  // namespace
 
 extern "C" {
 
 int sdsj_abi_version(void) { return SDSJ_ABI_VERSION; }
+
+int sdsj_submit_batch(sdsj_engine* e, int slot, int n, const uint8_t* const* jpg, const size_t* len, const sdsj_op* op,
+                      const uint8_t* flip, void* out, void* hip_stream) {
+  if (!e) return SDSJ_EINVAL;
+  if (slot < 0 || slot >= SDSJ_SLOTS || n < 0 || n > e->max_batch || (n > 0 && (!jpg || !len || !out)) ||
+      !valid_op(op))
+    return fail(e, SDSJ_EINVAL, "invalid argument");
+  DeviceGuard g(e->device);
+  Slot& sl = e->slots[slot];
+  size_t bytes = 0;
+  for (int i = 0; i < n; i++) {
+    if (len[i] > (size_t)INT32_MAX) return fail(e, SDSJ_EINVAL, "sample larger than 2 GiB");
+    bytes += align_up((int64_t)len[i], 16);
+  }
+  int rc = slot_reserve(e, sl, std::max(n, 1), std::max<size_t>(bytes, 16));
+  if (rc != SDSJ_OK) return rc;
+  int64_t off = 0;
+  for (int i = 0; i < n; i++) {
+    sl.h_offsets[i] = off;
+    sl.h_lengths[i] = (int32_t)len[i];
+    sl.h_flip[i] = flip ? flip[i] : 0;
+    sl.h_pre[i] = SDSJ_OK;
+    off += align_up((int64_t)len[i], 16);
+  }
+  parallel_for(n, [&](int i0, int i1) {
+    for (int i = i0; i < i1; i++) memcpy(sl.h_stage + sl.h_offsets[i], jpg[i], len[i]);
+  });
+  if (n == 0) {
+    sl.n = 0;
+    sl.pending = true;
+    return hipEventRecord(sl.ev_done, reinterpret_cast<hipStream_t>(hip_stream)) == hipSuccess ? SDSJ_OK : SDSJ_EHIP;
+  }
+  return slot_launch(e, sl, n, (size_t)off, *op, out, reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+int sdsj_submit_files(sdsj_engine* e, int slot, int n, const char* const* paths, const sdsj_op* op,
+                      const uint8_t* flip, void* out, void* hip_stream) {
+  if (!e) return SDSJ_EINVAL;
+  if (slot < 0 || slot >= SDSJ_SLOTS || n < 0 || n > e->max_batch || (n > 0 && (!paths || !out)) || !valid_op(op))
+    return fail(e, SDSJ_EINVAL, "invalid argument");
+  DeviceGuard g(e->device);
+  Slot& sl = e->slots[slot];
+  std::vector<int64_t> sizes(n);
+  parallel_for(n, [&](int i0, int i1) {
+    for (int i = i0; i < i1; i++) {
+      sizes[i] = file_size(paths[i]);
+      if (sizes[i] > INT32_MAX) sizes[i] = -1;
+    }
+  });
+  size_t bytes = 0;
+  for (int i = 0; i < n; i++)
+    if (sizes[i] > 0) bytes += align_up(sizes[i], 16);
+  int rc = slot_reserve(e, sl, std::max(n, 1), std::max<size_t>(bytes, 16));
+  if (rc != SDSJ_OK) return rc;
+  int64_t off = 0;
+  for (int i = 0; i < n; i++) {
+    sl.h_offsets[i] = off;
+    sl.h_flip[i] = flip ? flip[i] : 0;
+    if (sizes[i] > 0) off += align_up(sizes[i], 16);
+  }
+  parallel_for(n, [&](int i0, int i1) {
+    for (int i = i0; i < i1; i++) {
+      const bool ok = sizes[i] >= 0 && read_file(paths[i], sl.h_stage + sl.h_offsets[i], sizes[i]);
+      sl.h_lengths[i] = ok ? (int32_t)sizes[i] : 0;
+      sl.h_pre[i] = ok ? SDSJ_OK : SDSJ_EINVAL;
+    }
+  });
+  if (n == 0) {
+    sl.n = 0;
+    sl.pending = true;
+    return hipEventRecord(sl.ev_done, reinterpret_cast<hipStream_t>(hip_stream)) == hipSuccess ? SDSJ_OK : SDSJ_EHIP;
+  }
+  return slot_launch(e, sl, n, (size_t)std::max<int64_t>(off, 16), *op, out, reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+int sdsj_wait_batch(sdsj_engine* e, int slot, int32_t* status) {
+  if (!e) return SDSJ_EINVAL;
+  if (slot < 0 || slot >= SDSJ_SLOTS || !e->slots[slot].pending) return fail(e, SDSJ_EINVAL, "no batch in flight on slot");
+  DeviceGuard g(e->device);
+  Slot& sl = e->slots[slot];
+  SDSJ_HIP(e, hipEventSynchronize(sl.ev_done));
+  sl.pending = false;
+  for (int i = 0; i < sl.n; i++)
+    if (status) status[i] = sl.h_pre[i] != SDSJ_OK ? sl.h_pre[i] : sl.h_status[i];
+  return SDSJ_OK;
+}
 
 int sdsj_probe(const uint8_t* jpg, size_t n, sdsj_info* out) {
   if (!jpg || !out) return SDSJ_EINVAL;
@@ -342,6 +597,8 @@ int sdsj_engine_destroy(sdsj_engine* e) {
   (void)hipFree(e->d_etab);
   (void)hipFree(e->d_totals_x);
   (void)hipFree(e->d_routes_x);
+  for (auto& sl : e->slots) slot_free(sl);
+  if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
   for (int k = 0; k + 1 < kMaxLanes; k++) {
     if (e->aux[k]) (void)hipStreamDestroy(e->aux[k]);
     if (e->ev_mid[k]) (void)hipEventDestroy(e->ev_mid[k]);

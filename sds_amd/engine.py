@@ -67,6 +67,7 @@ class JpegEngine:
             raise RuntimeError(f"sdsj_engine_create failed: {_lib.STATUS_NAMES.get(st, st)}")
         self._h = h
         self._pid = os.getpid()
+        self._inflight: dict[int, tuple[torch.Tensor, int]] = {}
 
     # -- lifetime --------------------------------------------------------------------------
     def close(self) -> None:
@@ -128,6 +129,62 @@ class JpegEngine:
                                                    ctypes.c_void_p(out.data_ptr()), status, ctypes.c_void_p(stream))
         self._check(rc, "sdsj_decode_resize_batch")
         return out, np.frombuffer(status, dtype=np.int32, count=n).copy()
+
+    # -- asynchronous host path ----------------------------------------
+    def submit(self, slot: int, samples: Sequence, resolution, *, files: bool = False, crop_before_resize: bool = True,
+               filter: str = "bilinear", normalize: bool = False, flip: Optional[Sequence[bool]] = None,
+               layout: str = "chw", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Stages a batch into pinned slot ``slot`` (0 or 1) and enqueues H2D + decode without waiting.
+
+        ``samples``: encoded bytes, or file paths with ``files=True`` (read straight into the pinned
+        slot, as LoadFromDiskTransform presets.py:613-626 reads the downloader's local cache).  Returns
+        the output tensor, valid after ``wait(slot)``; submitting batch k + 1 to the other slot before
+        waiting for batch k overlaps its host staging and H2D copy with batch k's decode."""
+        op = self.make_op(resolution, crop_before_resize, filter, normalize, layout)
+        n = len(samples)
+        if n > self.max_batch:
+            raise ValueError(f"a slot holds at most max_batch={self.max_batch} samples, got {n}")
+        if out is None:
+            out = self._alloc_out(n, op)
+        flip_arr = (ctypes.c_uint8 * max(n, 1))(*[1 if f else 0 for f in flip]) if flip is not None else None
+        with torch.cuda.device(self.device):
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+            fl = ctypes.cast(flip_arr, ctypes.c_void_p) if flip_arr else None
+            if files:
+                paths = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in samples])
+                rc = self.lib.sdsj_submit_files(self._h, slot, n, paths, ctypes.byref(op), fl,
+                                                ctypes.c_void_p(out.data_ptr()), stream)
+            else:
+                ptrs = (ctypes.c_char_p * max(n, 1))(*samples)
+                lens = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in samples])
+                rc = self.lib.sdsj_submit_batch(self._h, slot, n, ptrs, lens, ctypes.byref(op), fl,
+                                                ctypes.c_void_p(out.data_ptr()), stream)
+        self._check(rc, "sdsj_submit_files" if files else "sdsj_submit_batch")
+        self._inflight[slot] = (out, n)
+        return out
+
+    def wait(self, slot: int) -> tuple[torch.Tensor, np.ndarray]:
+        """Blocks until the batch in ``slot`` is decoded; returns (output tensor, per-sample status)."""
+        if slot not in self._inflight:
+            raise RuntimeError(f"no batch in flight on slot {slot}")
+        out, n = self._inflight.pop(slot)
+        status = (ctypes.c_int32 * max(n, 1))()
+        self._check(self.lib.sdsj_wait_batch(self._h, slot, status), "sdsj_wait_batch")
+        return out, np.frombuffer(status, dtype=np.int32, count=n).copy()
+
+    def decode_stream(self, batches, resolution, *, files: bool = False, **kw):
+        """Yields (out, status) per batch of ``batches`` (each a list of bytes, or of paths with
+        ``files=True``), keeping one batch in flight: batch k + 1 is staged and copied while batch k
+        decodes (double-buffered pinned slots)."""
+        k, prev = 0, None
+        for batch in batches:
+            slot = k % _lib.SLOTS
+            self.submit(slot, batch, resolution, files=files, **kw)
+            if prev is not None:
+                yield self.wait(prev)
+            prev, k = slot, k + 1
+        if prev is not None:
+            yield self.wait(prev)
 
     # -- device-resident batch -------------------------------------------------------------
     def decode_resize_device(self, blob: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor, resolution, *,
