@@ -322,12 +322,14 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   s = (e >> 4) & 15;
   r = (e >> 8) & 15;
   if (l == 0) {
-    // jpeg_huff_decode: canonical search (longer codes, or a DC category > 15) -- the first
-    // length whose code is <= maxcode; all 16 compares issue together
+    // jpeg_huff_decode: canonical search for codes longer than LB bits -- the first length whose
+    // code is <= maxcode.  Only lengths LB + 1 .. 16 can match: every code of at most LB bits has
+    // its lookahead entry (a zero entry for a short code would need a DC category > 15, and such
+    // tables are rejected at parse time, huff_table_ok).  The compares issue together.
     const uint32_t peek = hi >> 16;
     int ll = 17;
 #pragma unroll
-    for (int k = 16; k >= 1; k--) ll = (int32_t)(peek >> (16 - k)) <= T.maxcode[slot][k] ? k : ll;
+    for (int k = 16; k > LB; k--) ll = (int32_t)(peek >> (16 - k)) <= T.maxcode[slot][k] ? k : ll;
     if (ll > 16) {
       bad = 1;  // JWRN_HUFF_BAD_CODE: 17 bits consumed, symbol 0 (libjpeg warns and goes on)
       l = 17;
