@@ -310,6 +310,31 @@ __device__ __forceinline__ BlkCtx make_ctx(const TT& T, int bpm) {
   return k;
 }
 
+// jpeg_huff_decode for a code longer than LB bits (lookahead entry 0): the canonical search --
+// the first length whose code is <= maxcode.  Only lengths LB + 1 .. 16 can match: every code of at
+// most LB bits has its lookahead entry (a zero entry for a short code would need a DC category > 15,
+// and such tables are rejected at parse time, huff_table_ok).  The compares issue together.
+// hi = the next 32 bits; gives the code length l (17 = bad code), category s and run r.
+template <int LB, class TT>
+__device__ __forceinline__ void long_code(const TT& T, int slot, bool isdc, uint32_t hi, int& l, int& s, int& r,
+                                          int& bad) {
+  const uint32_t peek = hi >> 16;
+  int ll = 17;
+#pragma unroll
+  for (int k = 16; k > LB; k--) ll = (int32_t)(peek >> (16 - k)) <= T.maxcode[slot][k] ? k : ll;
+  if (ll > 16) {
+    bad = 1;  // JWRN_HUFF_BAD_CODE: 17 bits consumed, symbol 0 (libjpeg warns and goes on)
+    l = 17;
+    s = 0;
+    r = 0;
+  } else {
+    const int sym = T.vals[slot][((int32_t)(peek >> (16 - ll)) + T.valoff[slot][ll]) & 0xFF];
+    l = ll;
+    s = isdc ? sym : (sym & 15);
+    r = isdc ? 0 : (sym >> 4);
+  }
+}
+
 // One symbol (jdhuff.c HUFF_DECODE + get_bits + HUFF_EXTEND): DC -> category s, r = 0;
 // AC -> (r, s).  val = the extended value (0 when s = 0).
 template <int LB, class TT, int Q>
@@ -321,31 +346,7 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   int l = e & 15;
   s = (e >> 4) & 15;
   r = (e >> 8) & 15;
-  if (l == 0) {
-    // jpeg_huff_decode: canonical search for codes longer than LB bits -- the first length whose
-    // code is <= maxcode.  Only lengths LB + 1 .. 16 can match: every code of at most LB bits has
-    // its lookahead entry (a zero entry for a short code would need a DC category > 15, and such
-    // tables are rejected at parse time, huff_table_ok).  The compares issue together.
-    const uint32_t peek = hi >> 16;
-    int ll = 17;
-#pragma unroll
-    for (int k = 16; k > LB; k--) ll = (int32_t)(peek >> (16 - k)) <= T.maxcode[slot][k] ? k : ll;
-    if (ll > 16) {
-      bad = 1;  // JWRN_HUFF_BAD_CODE: 17 bits consumed, symbol 0 (libjpeg warns and goes on)
-      l = 17;
-      s = 0;
-      r = 0;
-    } else {
-      const int sym = T.vals[slot][((int32_t)(peek >> (16 - ll)) + T.valoff[slot][ll]) & 0xFF];
-      l = ll;
-      s = isdc ? sym : (sym & 15);
-      r = isdc ? 0 : (sym >> 4);
-      if (s > 16) {
-        bad = 1;
-        s = 16;
-      }
-    }
-  }
+  if (l == 0) long_code<LB>(T, slot, isdc, hi, l, s, r, bad);
   const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - s) & 31);
   val = s == 0 ? 0 : (x < (1u << (s - 1)) ? (int)x - (1 << s) + 1 : (int)x);
   const int tot = l + s;
@@ -440,17 +441,11 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           const uint32_t hi = (uint32_t)(b.buf >> 32);
           const uint32_t e = T.lut[(slot << LB) + (hi >> (32 - LB))];
           int l = e & 15, sz = (e >> 4) & 15, r = (e >> 8) & 15;
-          if (l == 0) {
-            int s2, r2, v2;
-            decode_sym<LB>(T, b, slot, isdc, s2, r2, v2, bad);  // long code: the canonical search
-            sz = s2;
-            r = r2;
-          } else {
-            const int tot = l + sz;
-            b.buf <<= tot;
-            b.nb -= tot;
-            b.pos += tot;
-          }
+          if (l == 0) long_code<LB>(T, slot, isdc, hi, l, sz, r, bad);
+          const int tot = l + sz;
+          b.buf <<= tot;
+          b.nb -= tot;
+          b.pos += tot;
           nsym++;
           if (next_z(z, sz, r)) {
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
