@@ -140,6 +140,12 @@ struct ImgDesc {
   int64_t scan_end_raw;
   int32_t rgb_pitch;   // pixels per row of the RGB rows the unfused passes read (frames: the frame width)
   int32_t ent_groups;  // workgroups sharing the image's subsequences in the spec / write passes
+  // progressive JPEG (SOF2): every scan is decoded by k_prog from sos_pos (the first SOS segment's
+  // length field) into the zeroed coefficient array; ProgTables at off_ptab hold its table state
+  int32_t progressive;
+  int32_t pad3;
+  int64_t sos_pos;
+  int64_t off_ptab;
 };
 
 // Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).
@@ -160,6 +166,20 @@ struct SubState {
   int32_t first, seg;
   uint32_t lim_bit;  // end of the interval's data: bits at or beyond it read as zeros (jpeg_fill_bit_buffer)
   int32_t pad;
+};
+
+// Table state of the progressive decoder (k_prog), one per progressive image in scratch: derived
+// Huffman tables (jpeg_make_d_derived_tbl) of the 4 DC and 4 AC slots, the current DQT tables and
+// the per-component latched quant tables (jdinput.c latch_quant_tables).
+struct ProgTables {
+  int32_t maxcode[8][18];
+  int32_t valoff[8][18];
+  uint8_t vals[8][256];
+  uint8_t bits[8][17];
+  uint8_t defined[8];
+  uint16_t qt[4][64];
+  int32_t qt_defined[4];
+  int32_t latched[kMaxComp];
 };
 
 // One block boundary met by the speculative decode (for early sync detection).
@@ -207,6 +227,7 @@ enum Route : int32_t {
   kRt3, kRt5, kRt7, kRt9, kRt11,  // k_rs420<KT>
   kRtEnt10, kRtEnt11,             // entropy kernels by lookahead width
   kRtEnt11M,                      // LB = 11 images decoded by several workgroups (ent_groups > 1)
+  kRtProg,                        // progressive images (k_prog)
   kNumRoutes
 };
 constexpr int kRouteSlots = 16;  // counts [0, kNumRoutes), the rest zero
@@ -249,6 +270,8 @@ template <class Reader, class Sink>
 SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t, const Sink& sink) {
   d->status = SDSJ_OK;
   d->width = d->height = d->ncomp = 0;
+  d->progressive = 0;
+  d->sos_pos = 0;
   d->restart_interval = 0;
   d->saw_jfif = d->saw_adobe = d->adobe_transform = 0;
   for (int q = 0; q < 4; q++) {
@@ -273,17 +296,19 @@ SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t,
     int sl = len - 2;
     switch (m) {
       case 0xC0:
-      case 0xC1: {
+      case 0xC1:
+      case 0xC2: {  // baseline, extended sequential, progressive (Huffman)
         if (saw_sof) return SDSJ_CORRUPT;
         saw_sof = true;
+        d->progressive = m == 0xC2;
         if (sl < 6) return SDSJ_CORRUPT;
         if (rd(s) != 8) return SDSJ_UNSUPPORTED;
         d->height = (rd(s + 1) << 8) | rd(s + 2);
         d->width = (rd(s + 3) << 8) | rd(s + 4);
         d->ncomp = rd(s + 5);
         if (d->height == 0 || d->width == 0) return SDSJ_UNSUPPORTED;  // DNL
+        if (sl != 6 + 3 * d->ncomp) return SDSJ_CORRUPT;                // get_sof: JERR_BAD_LENGTH
         if (d->ncomp != 1 && d->ncomp != 3) return SDSJ_UNSUPPORTED;
-        if (sl < 6 + 3 * d->ncomp) return SDSJ_CORRUPT;
         d->hmax = d->vmax = 1;
         for (int c = 0; c < d->ncomp; c++) {
           CompDesc& cp = d->comp[c];
@@ -298,7 +323,7 @@ SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t,
         }
         break;
       }
-      case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9:
+      case 0xC3: case 0xC5: case 0xC6: case 0xC7: case 0xC9:
       case 0xCA: case 0xCB: case 0xCD: case 0xCE: case 0xCF:
         return SDSJ_UNSUPPORTED;
       case 0xC4: {  // DHT
@@ -354,7 +379,13 @@ SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t,
       case 0xDA: {  // SOS
         if (!saw_sof || sl < 1) return SDSJ_CORRUPT;
         int ns = rd(s);
-        if (sl < 1 + 2 * ns + 3) return SDSJ_CORRUPT;
+        if (ns < 1 || ns > 4 || sl != 2 * ns + 4) return SDSJ_CORRUPT;  // get_sos: JERR_BAD_LENGTH
+        if (d->progressive) {  // every scan is parsed by k_prog
+          d->sos_pos = i;
+          d->entropy_off = i + len;
+          d->entropy_len = n - d->entropy_off;
+          return SDSJ_OK;
+        }
         if (ns != d->ncomp) return SDSJ_UNSUPPORTED;  // multi-scan sequential
         for (int q = 0; q < ns; q++) {
           int cid = rd(s + 1 + 2 * q);
@@ -399,6 +430,7 @@ SDSJ_HD inline int setup_geometry(ImgDesc* d, const ImgTables* t) {
     if (cp.rh > 2 || cp.rv > 2) return SDSJ_UNSUPPORTED;
     cp.dw = ceil_div(d->width * cp.h, d->hmax);
     cp.dh = ceil_div(d->height * cp.v, d->vmax);
+    if (d->progressive) continue;  // tables are checked per scan (k_prog)
     if (!t->qt_defined[cp.tq]) return SDSJ_CORRUPT;
     if (!t->dc_spec[cp.td].defined || !t->ac_spec[cp.ta].defined) return SDSJ_CORRUPT;
   }

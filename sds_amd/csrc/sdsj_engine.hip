@@ -202,6 +202,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   mark(2);
   SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, s));
   SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, ln.descs, e->scratch, s));
+  SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s));
   mark(3);
   SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s,
                              e->lane_mid < 0 ? after_spec : nullptr));
@@ -522,7 +523,7 @@ int sdsj_probe(const uint8_t* jpg, size_t n, sdsj_info* out) {
   out->height = d.height;
   out->ncomp = d.ncomp;
   if (st == SDSJ_OK) st = setup_geometry(&d, &t);
-  for (int c = 0; st == SDSJ_OK && c < d.ncomp; c++)
+  for (int c = 0; st == SDSJ_OK && !d.progressive && c < d.ncomp; c++)  // (progressive: checked per scan)
     if (!huff_table_ok(t.dc_spec[d.comp[c].td], true) || !huff_table_ok(t.ac_spec[d.comp[c].ta], false))
       st = SDSJ_CORRUPT;
   for (int c = 0; c < d.ncomp && c < 3; c++) {
@@ -745,6 +746,7 @@ int sdsj_resize_frames_device(sdsj_engine* e, int n, const uint8_t* d_frames, in
       d.off_seg += o;
       d.off_sub += o;
       d.off_rec += o;
+      d.off_ptab += o;
       d.off_coef += o;
       d.off_planes += o;
       d.off_tmp += o;

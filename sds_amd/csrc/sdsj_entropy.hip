@@ -72,7 +72,7 @@ __device__ __forceinline__ bool variant_owns(int ns) {
 __global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restrict__ descs,
                                                        const ImgTables* __restrict__ tables, EntTables* __restrict__ out) {
   const ImgDesc* d = &descs[blockIdx.x];
-  if (d->status != SDSJ_OK) return;
+  if (d->status != SDSJ_OK || d->progressive) return;
   const ImgTables* tb = &tables[blockIdx.x];
   __shared__ EntTables T;
   __shared__ int32_t lim[kMaxSlots][12];

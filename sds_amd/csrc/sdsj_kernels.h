@@ -14,6 +14,9 @@ hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, Im
                           hipStream_t s);
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
+// progressive images (route kRtProg): zero their coefficients, then one lane per image decodes all scans
+hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* blob, const int64_t* offsets,
+                       const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s);
 size_t enttab_bytes();  // per-image decode tables (k_enttab) held in HBM between the entropy kernels
 hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
                           int cap, hipStream_t s, hipEvent_t after_spec);  // recorded between the two passes

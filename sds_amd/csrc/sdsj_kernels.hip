@@ -140,6 +140,11 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
     d->warm_bits = (int)(d->sub_bits * 3 / 2 < w ? d->sub_bits * 3 / 2 : w);
   }
   d->nsub_cap = (int32_t)((d->entropy_len * 8 + d->sub_bits - 1) / d->sub_bits) + d->nseg + 1;
+  const bool prog = d->progressive && !frames;  // k_prog decodes it: no unstuffed stream, no subsequences
+  if (prog) {
+    d->ent_groups = 1;
+    d->nsub_cap = 1;
+  }
   // scratch layout (relative offsets; k_plan adds the image base)
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -147,11 +152,12 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
     o += align_up(bytes, 256);
     return r;
   };
-  d->off_ustream = take(d->entropy_len + kUPad + 32);  // + the 16-byte granule of the final pad store
-  d->ustream_cap = d->entropy_len + kUPad;
+  d->off_ustream = take(prog ? 32 : d->entropy_len + kUPad + 32);  // + the 16-byte granule of the final pad store
+  d->ustream_cap = prog ? 0 : d->entropy_len + kUPad;
   d->off_seg = take(seg_bytes(d->nseg));
   d->off_sub = take((int64_t)d->nsub_cap * sizeof(SubState));
   d->off_rec = take((int64_t)d->nsub_cap * kRec * sizeof(SyncRec));
+  d->off_ptab = take(prog ? (int64_t)sizeof(ProgTables) : 0);
   d->off_coef = take(d->total_blocks * 128);
   int64_t planes = 0;
   for (int c = 0; c < d->ncomp; c++) planes += align_up((int64_t)d->comp[c].pitch * d->comp[c].bh * 8, 256);
@@ -240,7 +246,7 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
   }
   __syncthreads();
   // validation of the tables the scan uses (jdhuff.c jpeg_make_d_derived_tbl), one lane per table
-  if (s_status == SDSJ_OK && lane < 2 * sd.ncomp) {
+  if (s_status == SDSJ_OK && !sd.progressive && lane < 2 * sd.ncomp) {
     const int c = lane >> 1;
     const bool dc = (lane & 1) == 0;
     const HuffSpec& h = dc ? st.dc_spec[sd.comp[c].td] : st.ac_spec[sd.comp[c].ta];
@@ -292,6 +298,7 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         d.off_seg += start;
         d.off_sub += start;
         d.off_rec += start;
+        d.off_ptab += start;
         d.off_coef += start;
         d.off_planes += start;
         d.off_rgb += start;
@@ -308,7 +315,7 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
             for (int q = 0; q < ns; q++) seen |= keys[q] == key;
             if (!seen) keys[ns++] = key;
           }
-        const int re = ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
+        const int re = d.progressive ? kRtProg : ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
         int32_t* lst = routes + kRouteSlots + re * cap;
         lst[atomicAdd(&rcnt[re], 1)] = i;
         if (d.geo != kGeoZeros) {
@@ -492,7 +499,7 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_
   const int img = blockIdx.x;
   if (img >= n) return;
   ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK) return;
+  if (d->status != SDSJ_OK || d->progressive) return;  // progressive: k_prog reads the raw stream
   __shared__ alignas(16) uint8_t buf[kUsTile + 32];  // [carried tail][this tile's output]
   __shared__ int wsum[kUnstuffThreads / 64];
   __shared__ int s_end, s_end_code, s_overflow;
@@ -667,7 +674,7 @@ __global__ void __launch_bounds__(64) k_scanmap(int n, const uint8_t* __restrict
   const int img = blockIdx.x * 64 + threadIdx.x;
   if (img >= n) return;
   ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK) return;
+  if (d->status != SDSJ_OK || d->progressive) return;  // progressive: k_prog reads the raw stream
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
   finish_scan(d, sv, blob + offsets[img], d->entropy_len, d->useg_found - 1, d->scan_end_code, d->scan_end_raw, d->ulen, 0);
 }
@@ -814,8 +821,10 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
   const int nseg = d->nseg;
   const int bps = d->restart_interval ? d->restart_interval * bpm : (int)d->total_blocks;
-  const int vend0 = sv.vend[0];
+  const int vend0 = d->progressive ? 0 : sv.vend[0];
+  const bool prog = d->progressive != 0;  // (k_prog decodes every block; no cut intervals)
   auto zero_block = [&](int g) {
+    if (prog) return false;
     if (nseg == 1) return g >= vend0;
     const int k = g / bps;
     return g >= sv.vend[k] || (k > 0 && (sv.flag[k] & kSegEmpty) && (sv.flag[k - 1] & kSegIns));

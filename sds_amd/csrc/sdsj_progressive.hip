@@ -1,0 +1,467 @@
+// sdsj_progressive.hip -- progressive JPEG (SOF2, Huffman) for the MI355X path.
+//
+// Restates libjpeg-turbo's progressive decoder as Pillow runs it: jdphuff.c decode_mcu_DC_first /
+// _AC_first / _DC_refine / _AC_refine with EOB runs and start_pass_phuff_decoder's progression
+// checks, jdinput.c per-scan MCU geometry and latch_quant_tables, jdmarker.c read_markers between
+// scans (DHT / DQT / DRI may change from one scan to the next) up to EOI, and the bit reader /
+// restart / resynchronisation rules the baseline path shares (jdhuff.c jpeg_fill_bit_buffer,
+// read_restart_marker + jpeg_resync_to_restart).  Each image's scans depend on one another, so one
+// lane walks an image's whole file; the coefficients land in the same MCU-ordered array the
+// baseline entropy kernels write, and k_idct / the resample kernels take it from there.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sdsj_common.h"
+#include "sdsj_kernels.h"
+
+namespace sdsj {
+
+namespace {
+
+// Bit reader over the stuffed stream (jdhuff.c jpeg_fill_bit_buffer semantics): FF00 -> FF, FF fill
+// bytes skipped; a marker stops the data (zeros are fed from there); the input ending first is eof.
+struct PBits {
+  const uint8_t* d;
+  int64_t n, pos;
+  uint64_t buf;
+  int nbits, hit_marker, marker, pad_bits, insufficient, eof;
+};
+
+__device__ void pfill(PBits& b) {
+  while (b.nbits <= 56) {
+    int c;
+    if (b.hit_marker || b.pos >= b.n) {
+      if (!b.hit_marker) b.eof = 1;
+      c = 0;
+      b.pad_bits += 8;
+    } else {
+      c = b.d[b.pos++];
+      if (c == 0xFF) {
+        int c2;
+        do {
+          c2 = b.pos < b.n ? b.d[b.pos++] : -1;
+        } while (c2 == 0xFF);
+        if (c2 == 0) {
+          c = 0xFF;
+        } else if (c2 < 0) {
+          b.pos = b.n;
+          continue;
+        } else {
+          b.hit_marker = 1;
+          b.marker = c2;
+          b.pos -= 2;  // the marker stays for process_restart / read_markers
+          continue;
+        }
+      }
+    }
+    b.buf |= (uint64_t)c << (56 - b.nbits);
+    b.nbits += 8;
+  }
+}
+
+__device__ int pgetbits(PBits& b, int n) {
+  if (n == 0) return 0;
+  if (b.nbits < n) pfill(b);
+  const int v = (int)(b.buf >> (64 - n));
+  b.buf <<= n;
+  b.nbits -= n;
+  if (b.nbits < b.pad_bits) b.insufficient = 1;  // consumed inserted zeros (JWRN_HIT_MARKER)
+  return v;
+}
+
+// jdhuff.c jpeg_huff_decode (bit-serial canonical decode; > 16 bits: bad code, symbol 0)
+__device__ int phuff(PBits& b, const ProgTables* P, int slot) {
+  int l = 1, code = pgetbits(b, 1);
+  while (l <= 16 && code > P->maxcode[slot][l]) {
+    code = (code << 1) | pgetbits(b, 1);
+    l++;
+  }
+  if (l > 16) return 0;
+  return P->vals[slot][(code + P->valoff[slot][l]) & 0xFF];
+}
+
+__device__ int pextend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)((~0u << s) + 1) : x; }
+
+// jdmarker.c next_marker from the byte cursor: pos ends on the marker's last FF; -1 at the end
+__device__ int pnext_marker(PBits& b) {
+  for (;;) {
+    while (b.pos < b.n && b.d[b.pos] != 0xFF) b.pos++;
+    if (b.pos >= b.n) return -1;
+    int64_t p = b.pos + 1;
+    while (p < b.n && b.d[p] == 0xFF) p++;
+    if (p >= b.n) return -1;
+    if (b.d[p] != 0) {
+      b.pos = p - 1;
+      return b.d[p];
+    }
+    b.pos = p + 1;
+  }
+}
+
+__device__ void pconsume_marker(PBits& b) {
+  b.pos += 2;
+  b.hit_marker = 0;
+  b.marker = 0;
+}
+
+// read_restart_marker + jpeg_resync_to_restart (actions 1 / 2 / 3); -1 when the input ends first
+__device__ int pread_restart(PBits& b, int desired) {
+  if (!b.hit_marker) {
+    const int m = pnext_marker(b);
+    if (m < 0) return -1;
+    b.hit_marker = 1;
+    b.marker = m;
+  }
+  if (b.marker == 0xD0 + desired) {
+    pconsume_marker(b);
+    return 0;
+  }
+  for (;;) {
+    const int m = b.marker;
+    int action;
+    if (m < 0xC0) action = 2;
+    else if (m < 0xD0 || m > 0xD7) action = 3;
+    else if (m == 0xD0 + ((desired + 1) & 7) || m == 0xD0 + ((desired + 2) & 7)) action = 3;
+    else if (m == 0xD0 + ((desired - 1) & 7) || m == 0xD0 + ((desired - 2) & 7)) action = 2;
+    else action = 1;
+    if (action == 1) {
+      pconsume_marker(b);
+      return 0;
+    }
+    if (action == 3) return 0;
+    pconsume_marker(b);
+    const int m2 = pnext_marker(b);
+    if (m2 < 0) return -1;
+    b.hit_marker = 1;
+    b.marker = m2;
+  }
+}
+
+__device__ int pprocess_restart(PBits& b, int* next_num) {
+  b.buf = 0;
+  b.nbits = 0;
+  b.pad_bits = 0;
+  if (pread_restart(b, *next_num)) return -1;
+  *next_num = (*next_num + 1) & 7;
+  if (!b.hit_marker) b.insufficient = 0;
+  return 0;
+}
+
+__device__ int rd16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+
+// jdhuff.c jpeg_make_d_derived_tbl for slot (0..3 DC, 4..7 AC): canonical bounds; false when the
+// code assignment overflows (JERR_BAD_HUFF_TABLE), or a DC table holds a symbol > 15
+__device__ bool pderive(ProgTables* P, int slot) {
+  if (!P->defined[slot]) return false;
+  int code = 0, p = 0;
+  for (int l = 1; l <= 16; l++) {
+    const int cnt = P->bits[slot][l];
+    P->maxcode[slot][l] = cnt ? code + cnt - 1 : -1;
+    P->valoff[slot][l] = cnt ? p - code : 0;
+    p += cnt;
+    code += cnt;
+    if (cnt && code >= (1 << l)) return false;  // (the all-ones code is reserved)
+    code <<= 1;
+  }
+  if (p > 256) return false;
+  if (slot < 4)
+    for (int i = 0; i < p; i++)
+      if (P->vals[slot][i] > 15) return false;
+  P->maxcode[slot][17] = 0xFFFFF;
+  P->valoff[slot][17] = 0;
+  return true;
+}
+
+// get_dht / get_dqt bodies
+__device__ int pread_dht(ProgTables* P, const uint8_t* s, int sl) {
+  int k = 0;
+  while (k < sl) {
+    if (k + 17 > sl) return SDSJ_CORRUPT;
+    const int tc = s[k] >> 4, th = s[k] & 15;
+    if (tc > 1 || th > 3) return SDSJ_CORRUPT;
+    const int slot = tc * 4 + th;
+    int cnt = 0;
+    P->bits[slot][0] = 0;
+    for (int l = 1; l <= 16; l++) {
+      P->bits[slot][l] = s[k + l];
+      cnt += s[k + l];
+    }
+    if (cnt > 256 || k + 17 + cnt > sl) return SDSJ_CORRUPT;
+    for (int i = 0; i < 256; i++) P->vals[slot][i] = i < cnt ? s[k + 17 + i] : 0;
+    P->defined[slot] = 1;
+    k += 17 + cnt;
+  }
+  return SDSJ_OK;
+}
+
+__device__ int pread_dqt(ProgTables* P, const uint8_t* s, int sl) {
+  int k = 0;
+  while (k < sl) {
+    const int pq = s[k] >> 4, tq = s[k] & 15;
+    if (tq > 3 || pq > 1) return SDSJ_CORRUPT;
+    const int need = 1 + 64 * (pq ? 2 : 1);
+    if (k + need > sl) return SDSJ_CORRUPT;
+    for (int q = 0; q < 64; q++)
+      P->qt[tq][natural_order(q)] = (uint16_t)(pq ? rd16(s + k + 1 + 2 * q) : s[k + 1 + q]);
+    P->qt_defined[tq] = 1;
+    k += need;
+  }
+  return SDSJ_OK;
+}
+
+// One block of one scan (jdphuff.c decode_mcu_DC_first / _DC_refine / _AC_first / _AC_refine).
+__device__ void pblock(PBits& b, const ProgTables* P, int dslot, int aslot, int16_t* blk, int ss, int se, int ah,
+                       int al, int* last_dc, int* eobrun) {
+  if (ss == 0) {
+    if (ah == 0) {  // decode_mcu_DC_first
+      int s = phuff(b, P, dslot);
+      if (s) s = pextend(pgetbits(b, s), s);
+      s += *last_dc;
+      *last_dc = s;
+      blk[0] = (int16_t)((unsigned)s << al);
+    } else if (pgetbits(b, 1)) {  // decode_mcu_DC_refine
+      blk[0] = (int16_t)(blk[0] | (1 << al));
+    }
+    return;
+  }
+  if (ah == 0) {  // decode_mcu_AC_first
+    if (*eobrun > 0) {
+      (*eobrun)--;
+      return;
+    }
+    for (int k = ss; k <= se; k++) {
+      const int sym = phuff(b, P, aslot);
+      const int r = sym >> 4, s = sym & 15;
+      if (s) {
+        k += r;
+        const int x = pgetbits(b, s);
+        blk[natural_order(k)] = (int16_t)((unsigned)pextend(x, s) << al);
+      } else if (r == 15) {
+        k += 15;
+      } else {
+        *eobrun = 1 << r;
+        if (r) *eobrun += pgetbits(b, r);
+        (*eobrun)--;
+        break;
+      }
+    }
+    return;
+  }
+  // decode_mcu_AC_refine
+  const int p1 = 1 << al, m1 = -(1 << al);
+  int k = ss;
+  if (*eobrun == 0) {
+    for (; k <= se; k++) {
+      const int sym = phuff(b, P, aslot);
+      int r = sym >> 4, s = sym & 15;
+      if (s) {
+        s = pgetbits(b, 1) ? p1 : m1;  // (s != 1: JWRN_HUFF_BAD_CODE, decoding goes on)
+      } else if (r != 15) {
+        *eobrun = 1 << r;
+        if (r) *eobrun += pgetbits(b, r);
+        break;
+      }
+      do {
+        int16_t* c = blk + natural_order(k);
+        if (*c != 0) {
+          if (pgetbits(b, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
+        } else if (--r < 0) {
+          break;
+        }
+        k++;
+      } while (k <= se);
+      if (s) blk[natural_order(k)] = (int16_t)s;
+    }
+  }
+  if (*eobrun > 0) {
+    for (; k <= se; k++) {
+      int16_t* c = blk + natural_order(k);
+      if (*c != 0 && pgetbits(b, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
+    }
+    (*eobrun)--;
+  }
+}
+
+// Every scan of image d, then the markers up to EOI.  Returns an SDSJ status.
+__device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, int64_t n, int16_t* coef,
+                                  ProgTables* P) {
+  // table state as k_parse left it (the DHT / DQT segments before the first SOS)
+  for (int q = 0; q < 4; q++) {
+    P->qt_defined[q] = t->qt_defined[q];
+    for (int i = 0; i < 64; i++) P->qt[q][i] = t->qt[q][i];
+    for (int k = 0; k < 2; k++) {
+      const HuffSpec& h = k ? t->ac_spec[q] : t->dc_spec[q];
+      const int slot = k * 4 + q;
+      P->defined[slot] = h.defined;
+      for (int l = 0; l <= 16; l++) P->bits[slot][l] = h.bits[l];
+      for (int i = 0; i < 256; i++) P->vals[slot][i] = h.vals[i];
+    }
+  }
+  for (int c = 0; c < kMaxComp; c++) P->latched[c] = 0;
+  int restart_interval = d->restart_interval;
+  int boff[kMaxComp] = {0, 0, 0};
+  for (int c = 1; c < d->ncomp; c++) boff[c] = boff[c - 1] + d->comp[c - 1].h * d->comp[c - 1].v;
+  int64_t pos = d->sos_pos;
+  for (;;) {
+    if (pos + 2 > n) return SDSJ_CORRUPT;
+    const int len = rd16(raw + pos), sl = len - 2;
+    if (len < 2 || pos + len > n) return SDSJ_CORRUPT;
+    const uint8_t* s = raw + pos + 2;
+    if (sl < 1) return SDSJ_CORRUPT;
+    const int ns = s[0];
+    if (ns < 1 || ns > 4 || sl != 2 * ns + 4) return SDSJ_CORRUPT;  // get_sos: JERR_BAD_LENGTH
+    int comps[4], td[4], ta[4];
+    for (int q = 0; q < ns; q++) {
+      const int cid = s[1 + 2 * q];
+      int c = 0;
+      while (c < d->ncomp && d->comp_id[c] != cid) c++;
+      if (c == d->ncomp) return SDSJ_CORRUPT;
+      comps[q] = c;
+      td[q] = s[2 + 2 * q] >> 4;  // checked only where the table is used (jpeg_make_d_derived_tbl)
+      ta[q] = s[2 + 2 * q] & 15;
+    }
+    const int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ah = s[3 + 2 * ns] >> 4, al = s[3 + 2 * ns] & 15;
+    bool bad = false;
+    if (ss == 0) bad = se != 0;
+    else bad = se < ss || se > 63 || ns != 1;
+    if (ah != 0 && al != ah - 1) bad = true;
+    if (al > 13) bad = true;
+    if (bad) return SDSJ_CORRUPT;  // JERR_BAD_PROGRESSION
+    for (int q = 0; q < ns; q++) {
+      const int c = comps[q], tq = d->comp[c].tq;
+      if (!P->latched[c]) {  // latch_quant_tables: the component's table at its first scan
+        if (!P->qt_defined[tq]) return SDSJ_CORRUPT;
+        for (int i = 0; i < 64; i++) t->qt[c][i] = P->qt[tq][i];  // (k_idct reads slot c: see below)
+        P->latched[c] = 1;
+      }
+      if (ss == 0 && ah == 0) {
+        if (td[q] > 3 || !pderive(P, td[q])) return SDSJ_CORRUPT;
+      } else if (ss != 0) {
+        if (ta[q] > 3 || !pderive(P, 4 + ta[q])) return SDSJ_CORRUPT;
+      }
+    }
+    // jdinput.c per_scan_setup: a single-component scan walks that component's own block grid
+    int nmcu, cwb = 0;
+    if (ns == 1) {
+      const CompDesc& cp = d->comp[comps[0]];
+      cwb = (cp.dw + 7) / 8;
+      nmcu = cwb * ((cp.dh + 7) / 8);
+    } else {
+      nmcu = d->mcux * d->mcuy;
+    }
+    PBits b;
+    b.d = raw;
+    b.n = n;
+    b.pos = pos + len;
+    b.buf = 0;
+    b.nbits = b.hit_marker = b.marker = b.pad_bits = b.insufficient = b.eof = 0;
+    int last_dc[4] = {0, 0, 0, 0}, eobrun = 0;
+    int restarts_left = restart_interval, next_num = 0;
+    for (int m = 0; m < nmcu; m++) {
+      if (restart_interval) {
+        if (restarts_left == 0) {
+          if (pprocess_restart(b, &next_num)) return SDSJ_CORRUPT;
+          last_dc[0] = last_dc[1] = last_dc[2] = last_dc[3] = 0;
+          eobrun = 0;
+          restarts_left = restart_interval;
+        }
+        restarts_left--;
+      }
+      if (b.insufficient) continue;  // the MCU's coefficients stay as they are
+      for (int q = 0; q < ns; q++) {
+        const int c = comps[q];
+        const CompDesc& cp = d->comp[c];
+        const int hh = ns == 1 ? 1 : cp.h, vv = ns == 1 ? 1 : cp.v;
+        for (int v = 0; v < vv; v++)
+          for (int h = 0; h < hh; h++) {
+            const int bx = ns == 1 ? m % cwb : (m % d->mcux) * cp.h + h;
+            const int by = ns == 1 ? m / cwb : (m / d->mcux) * cp.v + v;
+            // block (bx, by) of component c in the MCU-ordered coefficient array
+            const int64_t g = d->ncomp == 1
+                                  ? (int64_t)by * cp.bw + bx
+                                  : ((int64_t)(by / cp.v) * d->mcux + bx / cp.h) * d->bpm + boff[c] +
+                                        (by % cp.v) * cp.h + (bx % cp.h);
+            pblock(b, P, td[q] & 3, 4 + (ta[q] & 3), coef + g * 64, ss, se, ah, al, &last_dc[q], &eobrun);
+          }
+      }
+    }
+    if (b.eof) return SDSJ_CORRUPT;  // the input ended inside the scan (Pillow: truncated)
+    if (!b.hit_marker && pnext_marker(b) < 0) return SDSJ_CORRUPT;
+    // jdmarker.c read_markers until the next SOS or EOI
+    for (;;) {
+      if (b.pos + 1 >= n) return SDSJ_CORRUPT;
+      const int m = b.d[b.pos + 1];
+      const int64_t body = b.pos + 2;
+      if (m == 0xD9) {
+        // k_idct reads each component's latched table from slot c
+        for (int c = 0; c < d->ncomp; c++) d->comp[c].tq = c;
+        return SDSJ_OK;
+      }
+      if ((m >= 0xD0 && m <= 0xD7) || m == 0x01) {
+        b.pos = body;
+      } else {
+        const bool seg = (m >= 0xE0 && m <= 0xEF) || m == 0xFE || m == 0xDC || m == 0xCC || m == 0xDD ||
+                         m == 0xC4 || m == 0xDB || m == 0xDA;
+        if (!seg) return SDSJ_CORRUPT;  // a second SOI / SOF, or an unknown marker
+        if (m == 0xDC || m == 0xCC) return SDSJ_UNSUPPORTED;
+        if (body + 2 > n) return SDSJ_CORRUPT;
+        const int l2 = rd16(raw + body);
+        if (l2 < 2 || body + l2 > n) return SDSJ_CORRUPT;
+        if (m == 0xDA) {
+          pos = body;
+          break;
+        }
+        int st = SDSJ_OK;
+        if (m == 0xC4) st = pread_dht(P, raw + body + 2, l2 - 2);
+        if (m == 0xDB) st = pread_dqt(P, raw + body + 2, l2 - 2);
+        if (m == 0xDD) {
+          if (l2 != 4) return SDSJ_CORRUPT;
+          restart_interval = rd16(raw + body + 2);
+        }
+        if (st != SDSJ_OK) return st;
+        b.pos = body + l2;
+      }
+      if (pnext_marker(b) < 0) return SDSJ_CORRUPT;
+    }
+  }
+}
+
+}  // namespace
+
+// Zeroes the coefficient arrays of the progressive images (scans accumulate into them).
+__global__ void __launch_bounds__(256) k_prog_zero(const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                                   const int32_t* __restrict__ routes, int cap) {
+  if ((int)blockIdx.x >= routes[kRtProg]) return;
+  const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[blockIdx.x]];
+  if (d->status != SDSJ_OK) return;
+  uint4* p = reinterpret_cast<uint4*>(scratch + d->off_coef);
+  const int64_t n16 = d->total_blocks * 8;
+  for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.y * 256)
+    p[i] = make_uint4(0, 0, 0, 0);
+}
+
+// One lane per progressive image: all its scans (see the header).
+__global__ void __launch_bounds__(64) k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables,
+                                             const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
+                                             const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
+                                             const int32_t* __restrict__ routes, int cap) {
+  const int li = blockIdx.x * 64 + threadIdx.x;
+  if (li >= routes[kRtProg]) return;
+  const int img = route_list(routes, cap, kRtProg)[li];
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK) return;
+  const int st = decode_progressive(d, &tables[img], blob + offsets[img], lengths[img],
+                                    reinterpret_cast<int16_t*>(scratch + d->off_coef),
+                                    reinterpret_cast<ProgTables*>(scratch + d->off_ptab));
+  if (st != SDSJ_OK) d->status = st;
+}
+
+hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* blob, const int64_t* offsets,
+                       const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_prog_zero, dim3(n, 16), dim3(256), 0, s, descs, scratch, routes, cap);
+  hipLaunchKernelGGL(k_prog, dim3((n + 63) / 64), dim3(64), 0, s, descs, tables, blob, offsets, lengths, scratch,
+                     routes, cap);
+  return hipGetLastError();
+}
+
+}  // namespace sdsj

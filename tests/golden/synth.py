@@ -78,3 +78,25 @@ def mutated_jpegs(seed: int, n: int) -> list[bytes]:
             jpg[p:p] = b"\xff\xd3"                          # an unexpected RSTn
         out.append(bytes(jpg))
     return out
+
+
+def progressive_jpegs(seed: int, n: int, max_w: int = 400, max_h: int = 300) -> list[bytes]:
+    """Progressive JPEGs (PIL/libjpeg-turbo's default scan script) of random sizes, sampling,
+    quality, optimized tables and restart intervals, grayscale every fifth."""
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        w, h = int(rng.integers(1, max_w)), int(rng.integers(1, max_h))
+        rgb = rng.integers(0, 256, (h, w, 3), dtype=np.uint8) if i % 3 == 0 else synth_rgb(rng, w, h)
+        kw = dict(progressive=True)
+        if i % 5 == 0:
+            rgb = np.array(Image.fromarray(rgb).convert("L"))
+        else:
+            kw["subsampling"] = int(rng.integers(0, 3))
+        if i % 4 == 1:
+            kw["optimize"] = True
+        if i % 7 == 2:
+            kw["restart_marker_blocks"] = int(rng.integers(1, 5))
+        out.append(encode_jpeg(rgb, int(rng.integers(5, 101)), **kw))
+    return out

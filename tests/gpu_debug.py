@@ -36,7 +36,8 @@ class ImgDescC(ctypes.Structure):
                 ("t_spec", i64), ("t_sync", i64), ("t_scan", i64), ("t_write", i64), ("it_spec", i64), ("it_sync", i64),
                 ("it_write", i64), ("fused", i32), ("tile_w", i32), ("ring_rows", i32), ("rs_fast", i32), ("t_rs", i64 * 4),
                 ("warm_bits", i32), ("scan_end_code", i32), ("scan_end_raw", i64),
-                ("rgb_pitch", i32), ("ent_groups", i32)]
+                ("rgb_pitch", i32), ("ent_groups", i32),
+                ("progressive", i32), ("pad3", i32), ("sos_pos", i64), ("off_ptab", i64)]
 
 
 def _memcpy_d2h(ptr: int, nbytes: int) -> np.ndarray:

@@ -40,9 +40,6 @@ def test_g1_golden(engine, case, jpg, arrs):
     if case["decode"] != "ok":
         assert _status(engine, jpg) == _lib.CORRUPT
         return
-    if name.startswith("progressive"):
-        assert _status(engine, jpg) == _lib.UNSUPPORTED
-        return
     w, h = case["size"]
     # full-resolution decode = same-size shortcut (functional.py:78-80)
     full, st = engine.decode_resize([jpg], (h, w), layout="hwc")
@@ -59,7 +56,7 @@ def test_g1_golden(engine, case, jpg, arrs):
 
 def test_g1_as_one_batch(engine):
     """All decodable G1 cases in one launch at 48x64 (mixed sizes/samplings/restarts in a batch)."""
-    cases = [(c, j, a) for c, j, a in G1 if c["decode"] == "ok" and not c["name"].startswith("progressive")]
+    cases = [(c, j, a) for c, j, a in G1 if c["decode"] == "ok"]
     got, st = engine.decode_resize([j for _, j, _ in cases], (48, 64))
     assert (st == 0).all()
     for k, (c, j, a) in enumerate(cases):
@@ -207,3 +204,45 @@ def test_g5_edge_cases(engine):
         full, st = engine.decode_resize([jpg], (h, w), layout="hwc")
         assert st[0] == 0, c["name"]
         assert G.sha(full[0].cpu().numpy()) == c["rgb_sha256"], c["name"]
+
+
+def test_progressive_batch_vs_oracle(engine):
+    """Progressive JPEGs (k_prog) mixed with baseline ones in one batch."""
+    from tests.golden.synth import progressive_jpegs
+    jpgs = progressive_jpegs(5, 40) + _random_jpegs(3, 24)
+    res = (56, 72)
+    got, st = engine.decode_resize(jpgs, res, flip=[k % 2 == 0 for k in range(len(jpgs))])
+    assert (st == 0).all()
+    for k, j in enumerate(jpgs):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res, flip=k % 2 == 0), err_msg=f"image {k}")
+
+
+def test_progressive_full_resolution_and_damaged_streams(engine):
+    from tests.golden.synth import progressive_jpegs
+    jpgs = progressive_jpegs(6, 6)
+    for j in jpgs:  # full-resolution decode = the same-size shortcut
+        ref = O.decode(j)
+        got, st = engine.decode_resize([j], ref.shape[:2], layout="hwc")
+        assert st[0] == 0
+        np.testing.assert_array_equal(got[0].cpu().numpy(), ref)
+    rng = np.random.default_rng(17)
+    bad = []
+    for j in progressive_jpegs(7, 8):
+        for _ in range(6):
+            jb = bytearray(j)
+            kind = int(rng.integers(0, 3))
+            if kind == 0:
+                jb = jb[:int(rng.integers(len(j) // 3, len(j)))]
+            elif kind == 1:
+                jb[int(rng.integers(len(j) // 4, len(j) - 4))] ^= 1 << int(rng.integers(0, 8))
+            else:
+                p = int(rng.integers(len(j) // 4, len(j) - 4))
+                jb[p:p] = b"\xff\xd9"
+            bad.append(bytes(jb))
+    res = (40, 40)
+    got, st = engine.decode_resize(bad, res)
+    for k, j in enumerate(bad):
+        ost, ref = _oracle_result(j, res)
+        assert int(st[k]) == ost, f"sample {k}: gpu {int(st[k])} vs oracle {ost}"
+        if ost == O.OK:
+            np.testing.assert_array_equal(got[k].cpu().numpy(), ref, err_msg=f"sample {k}")

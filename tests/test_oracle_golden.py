@@ -15,11 +15,6 @@ def test_g1_decode_and_pipeline(case, jpg, arrs):
         with pytest.raises(O.OracleError):
             O.decode(jpg)
         return
-    if name.startswith("progressive"):
-        # the reference decodes it through PIL; the oracle (like the MI355X path) reports UNSUPPORTED
-        st, _ = O.probe(jpg)
-        assert st == O.UNSUPPORTED
-        return
     np.testing.assert_array_equal(O.decode(jpg), arrs["rgb"])
     for key, out in case["outputs"].items():
         res = tuple(int(v) for v in key.split("x"))
@@ -100,3 +95,51 @@ def test_oracle_resize_matches_pil_on_raw_frames(size, res, filt):
     l, t, r, b = O.crop_box(w, h, out_h, out_w)
     img = Image.fromarray(rgb).crop((l, t, r, b)).resize((out_w, out_h), getattr(Image, filt.upper()))
     np.testing.assert_array_equal(O.resize(np.ascontiguousarray(rgb[t:b, l:r]), out_h, out_w, filt), np.asarray(img))
+
+
+def test_oracle_progressive_matches_pil():
+    """Progressive JPEGs: the oracle's restatement of jdphuff.c decodes what PIL
+    decodes, bit for bit (random sizes, samplings, qualities, optimized tables, restart intervals, gray)."""
+    import io
+
+    from PIL import Image
+
+    from tests.golden.synth import progressive_jpegs
+    for k, j in enumerate(progressive_jpegs(5, 60)):
+        ref = np.array(Image.open(io.BytesIO(j)).convert("RGB"))
+        np.testing.assert_array_equal(O.decode(j), ref, err_msg=f"image {k}")
+
+
+def test_oracle_progressive_damaged_status_matches_pil():
+    """Damaged progressive streams (truncations, bit flips, a stray EOI): the oracle raises exactly when
+    PIL raises.  Pixels are not compared: a scan cut short leaves coefficients incomplete and libjpeg
+    then smooths blocks across (jdcoefct.c decompress_smooth_data), which is not restated."""
+    import io
+
+    from PIL import Image
+
+    from tests.golden.synth import progressive_jpegs
+    for seed in (7, 8, 9):
+        rng = np.random.default_rng(seed)
+        for j in progressive_jpegs(seed, 12):
+            for _ in range(10):
+                kind, jb = int(rng.integers(0, 3)), bytearray(j)
+                if kind == 0:
+                    jb = jb[:int(rng.integers(len(j) // 3, len(j)))]
+                elif kind == 1:
+                    jb[int(rng.integers(len(j) // 4, len(j) - 4))] ^= 1 << int(rng.integers(0, 8))
+                else:
+                    p = int(rng.integers(len(j) // 4, len(j) - 4))
+                    jb[p:p] = b"\xff\xd9"
+                jb = bytes(jb)
+                try:
+                    Image.open(io.BytesIO(jb)).convert("RGB")
+                    pil_ok = True
+                except Exception:
+                    pil_ok = False
+                try:
+                    O.decode(jb)
+                    oracle_ok = True
+                except O.OracleError:
+                    oracle_ok = False
+                assert pil_ok == oracle_ok, (seed, kind)
