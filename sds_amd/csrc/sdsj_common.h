@@ -168,12 +168,11 @@ struct SubState {
   int32_t pad;
 };
 
-// Table state of the progressive decoder (k_prog), one per progressive image in scratch: derived
-// Huffman tables (jpeg_make_d_derived_tbl) of the 4 DC and 4 AC slots, the current DQT tables and
-// the per-component latched quant tables (jdinput.c latch_quant_tables).
+// Table state of the progressive decoder (k_prog), one per progressive image in scratch: the
+// Huffman specs of the 4 DC and 4 AC slots as DHT segments define them (the scan's derived tables
+// live in LDS), the current DQT tables and which components have latched theirs (jdinput.c
+// latch_quant_tables).
 struct ProgTables {
-  int32_t maxcode[8][18];
-  int32_t valoff[8][18];
   uint8_t vals[8][256];
   uint8_t bits[8][17];
   uint8_t defined[8];

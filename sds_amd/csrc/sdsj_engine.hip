@@ -202,8 +202,9 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   mark(2);
   SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, s));
   SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, ln.descs, e->scratch, s));
-  SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s));
   mark(3);
+  // (after mark 3: the next lane may start while this lane's progressive images decode)
+  SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s));
   SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s,
                              e->lane_mid < 0 ? after_spec : nullptr));
   mark(4);

@@ -25,7 +25,21 @@ struct PBits {
   int64_t n, pos;
   uint64_t buf;
   int nbits, hit_marker, marker, pad_bits, insufficient, eof;
+  uintptr_t wbase;  // 16-byte window of the stream held in registers (one load per 16 bytes)
+  uint4 w;
 };
+
+// Byte i of the stream (0 <= i < n) through the window: the aligned 16 bytes around it come in as
+// one load (the blob allocation holds the whole granule).
+__device__ __forceinline__ int pbyte(PBits& b, int64_t i) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(b.d + i), base = a & ~(uintptr_t)15;
+  if (base != b.wbase) {
+    b.wbase = base;
+    b.w = *reinterpret_cast<const uint4*>(base);
+  }
+  const uint32_t o = (uint32_t)(a - base), v = o < 8 ? (o < 4 ? b.w.x : b.w.y) : (o < 12 ? b.w.z : b.w.w);
+  return (int)((v >> (8 * (o & 3))) & 0xFF);
+}
 
 __device__ void pfill(PBits& b) {
   while (b.nbits <= 56) {
@@ -35,11 +49,11 @@ __device__ void pfill(PBits& b) {
       c = 0;
       b.pad_bits += 8;
     } else {
-      c = b.d[b.pos++];
+      c = pbyte(b, b.pos++);
       if (c == 0xFF) {
         int c2;
         do {
-          c2 = b.pos < b.n ? b.d[b.pos++] : -1;
+          c2 = b.pos < b.n ? pbyte(b, b.pos++) : -1;
         } while (c2 == 0xFF);
         if (c2 == 0) {
           c = 0xFF;
@@ -69,15 +83,30 @@ __device__ int pgetbits(PBits& b, int n) {
   return v;
 }
 
-// jdhuff.c jpeg_huff_decode (bit-serial canonical decode; > 16 bits: bad code, symbol 0)
-__device__ int phuff(PBits& b, const ProgTables* P, int slot) {
-  int l = 1, code = pgetbits(b, 1);
-  while (l <= 16 && code > P->maxcode[slot][l]) {
-    code = (code << 1) | pgetbits(b, 1);
-    l++;
-  }
+// The derived tables of the scan being decoded, in LDS (one slot per lane = per image).
+struct PLds {
+  int32_t maxcode[8][17];  // [slot][l], l = 1..16 (index 0 unused)
+  int32_t valoff[8][17];
+  uint8_t vals[8][256];
+  alignas(16) int16_t blk[64];  // the block an AC refinement scan updates (read-modify-write in LDS)
+};
+__shared__ uint8_t s_nat[80];  // jpeg_natural_order (+ guards) for the workgroup
+
+// jdhuff.c jpeg_huff_decode: the code length is the first l whose l-bit prefix is <= maxcode[l]
+// (all 16 compares issue together on 17 peeked bits); no match = bad code: 17 bits, symbol 0.
+// Bits are consumed only after the length is known, so insufficient_data follows the consumed
+// count as with a bit-serial decode.
+__device__ int phuff(PBits& b, const PLds& L, int slot) {
+  if (b.nbits < 17) pfill(b);
+  const uint32_t peek = (uint32_t)(b.buf >> 47);
+  int l = 17;
+#pragma unroll
+  for (int k = 16; k >= 1; k--) l = (int32_t)(peek >> (17 - k)) <= L.maxcode[slot][k] ? k : l;
+  b.buf <<= l;
+  b.nbits -= l;
+  if (b.nbits < b.pad_bits) b.insufficient = 1;
   if (l > 16) return 0;
-  return P->vals[slot][(code + P->valoff[slot][l]) & 0xFF];
+  return L.vals[slot][((int32_t)(peek >> (17 - l)) + L.valoff[slot][l]) & 0xFF];
 }
 
 __device__ int pextend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)((~0u << s) + 1) : x; }
@@ -85,14 +114,15 @@ __device__ int pextend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)((~0
 // jdmarker.c next_marker from the byte cursor: pos ends on the marker's last FF; -1 at the end
 __device__ int pnext_marker(PBits& b) {
   for (;;) {
-    while (b.pos < b.n && b.d[b.pos] != 0xFF) b.pos++;
+    while (b.pos < b.n && pbyte(b, b.pos) != 0xFF) b.pos++;
     if (b.pos >= b.n) return -1;
     int64_t p = b.pos + 1;
-    while (p < b.n && b.d[p] == 0xFF) p++;
+    while (p < b.n && pbyte(b, p) == 0xFF) p++;
     if (p >= b.n) return -1;
-    if (b.d[p] != 0) {
+    const int m = pbyte(b, p);
+    if (m != 0) {
       b.pos = p - 1;
-      return b.d[p];
+      return m;
     }
     b.pos = p + 1;
   }
@@ -151,13 +181,13 @@ __device__ int rd16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
 // jdhuff.c jpeg_make_d_derived_tbl for slot (0..3 DC, 4..7 AC): canonical bounds; false when the
 // code assignment overflows (JERR_BAD_HUFF_TABLE), or a DC table holds a symbol > 15
-__device__ bool pderive(ProgTables* P, int slot) {
+__device__ bool pderive(const ProgTables* P, PLds& L, int slot) {
   if (!P->defined[slot]) return false;
   int code = 0, p = 0;
   for (int l = 1; l <= 16; l++) {
     const int cnt = P->bits[slot][l];
-    P->maxcode[slot][l] = cnt ? code + cnt - 1 : -1;
-    P->valoff[slot][l] = cnt ? p - code : 0;
+    L.maxcode[slot][l] = cnt ? code + cnt - 1 : -1;
+    L.valoff[slot][l] = cnt ? p - code : 0;
     p += cnt;
     code += cnt;
     if (cnt && code >= (1 << l)) return false;  // (the all-ones code is reserved)
@@ -167,8 +197,7 @@ __device__ bool pderive(ProgTables* P, int slot) {
   if (slot < 4)
     for (int i = 0; i < p; i++)
       if (P->vals[slot][i] > 15) return false;
-  P->maxcode[slot][17] = 0xFFFFF;
-  P->valoff[slot][17] = 0;
+  for (int i = 0; i < 256; i++) L.vals[slot][i] = P->vals[slot][i];
   return true;
 }
 
@@ -210,7 +239,7 @@ __device__ int pread_dqt(ProgTables* P, const uint8_t* s, int sl) {
 }
 
 // One block of one scan (jdphuff.c decode_mcu_DC_first / _DC_refine / _AC_first / _AC_refine).
-__device__ void pblock(PBits& b, const ProgTables* P, int dslot, int aslot, int16_t* blk, int ss, int se, int ah,
+__device__ void pblock(PBits& b, const PLds& P, int dslot, int aslot, int16_t* blk, int ss, int se, int ah,
                        int al, int* last_dc, int* eobrun) {
   if (ss == 0) {
     if (ah == 0) {  // decode_mcu_DC_first
@@ -235,7 +264,7 @@ __device__ void pblock(PBits& b, const ProgTables* P, int dslot, int aslot, int1
       if (s) {
         k += r;
         const int x = pgetbits(b, s);
-        blk[natural_order(k)] = (int16_t)((unsigned)pextend(x, s) << al);
+        blk[s_nat[k]] = (int16_t)((unsigned)pextend(x, s) << al);
       } else if (r == 15) {
         k += 15;
       } else {
@@ -247,7 +276,15 @@ __device__ void pblock(PBits& b, const ProgTables* P, int dslot, int aslot, int1
     }
     return;
   }
-  // decode_mcu_AC_refine
+  // decode_mcu_AC_refine, on an LDS copy of the block (its nonzero coefficients are read back)
+  int16_t* const gblk = blk;
+  {
+    uint4* dst = reinterpret_cast<uint4*>(const_cast<int16_t*>(P.blk));
+    const uint4* src = reinterpret_cast<const uint4*>(gblk);
+#pragma unroll
+    for (int i = 0; i < 8; i++) dst[i] = src[i];
+  }
+  blk = const_cast<int16_t*>(P.blk);
   const int p1 = 1 << al, m1 = -(1 << al);
   int k = ss;
   if (*eobrun == 0) {
@@ -262,7 +299,7 @@ __device__ void pblock(PBits& b, const ProgTables* P, int dslot, int aslot, int1
         break;
       }
       do {
-        int16_t* c = blk + natural_order(k);
+        int16_t* c = blk + s_nat[k];
         if (*c != 0) {
           if (pgetbits(b, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
         } else if (--r < 0) {
@@ -270,21 +307,27 @@ __device__ void pblock(PBits& b, const ProgTables* P, int dslot, int aslot, int1
         }
         k++;
       } while (k <= se);
-      if (s) blk[natural_order(k)] = (int16_t)s;
+      if (s) blk[s_nat[k]] = (int16_t)s;
     }
   }
   if (*eobrun > 0) {
     for (; k <= se; k++) {
-      int16_t* c = blk + natural_order(k);
+      int16_t* c = blk + s_nat[k];
       if (*c != 0 && pgetbits(b, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
     }
     (*eobrun)--;
+  }
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(blk);
+    uint4* dst = reinterpret_cast<uint4*>(gblk);
+#pragma unroll
+    for (int i = 0; i < 8; i++) dst[i] = src[i];
   }
 }
 
 // Every scan of image d, then the markers up to EOI.  Returns an SDSJ status.
 __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, int64_t n, int16_t* coef,
-                                  ProgTables* P) {
+                                  ProgTables* P, PLds& L) {
   // table state as k_parse left it (the DHT / DQT segments before the first SOS)
   for (int q = 0; q < 4; q++) {
     P->qt_defined[q] = t->qt_defined[q];
@@ -298,6 +341,7 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
     }
   }
   for (int c = 0; c < kMaxComp; c++) P->latched[c] = 0;
+  d->t_spec = d->t_sync = d->t_scan = d->t_write = 0;
   int restart_interval = d->restart_interval;
   int boff[kMaxComp] = {0, 0, 0};
   for (int c = 1; c < d->ncomp; c++) boff[c] = boff[c - 1] + d->comp[c - 1].h * d->comp[c - 1].v;
@@ -335,11 +379,20 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
         P->latched[c] = 1;
       }
       if (ss == 0 && ah == 0) {
-        if (td[q] > 3 || !pderive(P, td[q])) return SDSJ_CORRUPT;
+        if (td[q] > 3 || !pderive(P, L, td[q])) return SDSJ_CORRUPT;
       } else if (ss != 0) {
-        if (ta[q] > 3 || !pderive(P, 4 + ta[q])) return SDSJ_CORRUPT;
+        if (ta[q] > 3 || !pderive(P, L, 4 + ta[q])) return SDSJ_CORRUPT;
       }
     }
+    // the scan's geometry in registers (descriptor reads would repeat for every block: the
+    // coefficient stores may alias them as far as the compiler knows)
+    int sh[4], sv[4], sbw[4];
+    for (int q = 0; q < ns; q++) {
+      sh[q] = d->comp[comps[q]].h;
+      sv[q] = d->comp[comps[q]].v;
+      sbw[q] = d->comp[comps[q]].bw;
+    }
+    const int mcux = d->mcux, bpm = d->bpm, ncomp = d->ncomp;
     // jdinput.c per_scan_setup: a single-component scan walks that component's own block grid
     int nmcu, cwb = 0;
     if (ns == 1) {
@@ -347,14 +400,16 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
       cwb = (cp.dw + 7) / 8;
       nmcu = cwb * ((cp.dh + 7) / 8);
     } else {
-      nmcu = d->mcux * d->mcuy;
+      nmcu = mcux * d->mcuy;
     }
+    const unsigned long long t_scan0 = __builtin_amdgcn_s_memtime();
     PBits b;
     b.d = raw;
     b.n = n;
     b.pos = pos + len;
     b.buf = 0;
     b.nbits = b.hit_marker = b.marker = b.pad_bits = b.insufficient = b.eof = 0;
+    b.wbase = 1;  // (no window yet: never 16-byte aligned)
     int last_dc[4] = {0, 0, 0, 0}, eobrun = 0;
     int restarts_left = restart_interval, next_num = 0;
     for (int m = 0; m < nmcu; m++) {
@@ -370,27 +425,34 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
       if (b.insufficient) continue;  // the MCU's coefficients stay as they are
       for (int q = 0; q < ns; q++) {
         const int c = comps[q];
-        const CompDesc& cp = d->comp[c];
-        const int hh = ns == 1 ? 1 : cp.h, vv = ns == 1 ? 1 : cp.v;
+        const int ch = sh[q], cv = sv[q];
+        const int hh = ns == 1 ? 1 : ch, vv = ns == 1 ? 1 : cv;
         for (int v = 0; v < vv; v++)
           for (int h = 0; h < hh; h++) {
-            const int bx = ns == 1 ? m % cwb : (m % d->mcux) * cp.h + h;
-            const int by = ns == 1 ? m / cwb : (m / d->mcux) * cp.v + v;
+            const int bx = ns == 1 ? m % cwb : (m % mcux) * ch + h;
+            const int by = ns == 1 ? m / cwb : (m / mcux) * cv + v;
             // block (bx, by) of component c in the MCU-ordered coefficient array
-            const int64_t g = d->ncomp == 1
-                                  ? (int64_t)by * cp.bw + bx
-                                  : ((int64_t)(by / cp.v) * d->mcux + bx / cp.h) * d->bpm + boff[c] +
-                                        (by % cp.v) * cp.h + (bx % cp.h);
-            pblock(b, P, td[q] & 3, 4 + (ta[q] & 3), coef + g * 64, ss, se, ah, al, &last_dc[q], &eobrun);
+            const int64_t g = ncomp == 1 ? (int64_t)by * sbw[q] + bx
+                                         : ((int64_t)(by / cv) * mcux + bx / ch) * bpm + boff[c] + (by % cv) * ch +
+                                               (bx % ch);
+            pblock(b, L, td[q] & 3, 4 + (ta[q] & 3), coef + g * 64, ss, se, ah, al, &last_dc[q], &eobrun);
           }
       }
+    }
+    {  // diagnostics: s_memtime ticks per scan kind (DC first / AC first / DC refine / AC refine)
+      const long long dt = (long long)(__builtin_amdgcn_s_memtime() - t_scan0);
+      const int kind = (ss ? 1 : 0) + (ah ? 2 : 0);
+      if (kind == 0) d->t_spec += dt;
+      else if (kind == 1) d->t_sync += dt;
+      else if (kind == 2) d->t_scan += dt;
+      else d->t_write += dt;
     }
     if (b.eof) return SDSJ_CORRUPT;  // the input ended inside the scan (Pillow: truncated)
     if (!b.hit_marker && pnext_marker(b) < 0) return SDSJ_CORRUPT;
     // jdmarker.c read_markers until the next SOS or EOI
     for (;;) {
       if (b.pos + 1 >= n) return SDSJ_CORRUPT;
-      const int m = b.d[b.pos + 1];
+      const int m = pbyte(b, b.pos + 1);
       const int64_t body = b.pos + 2;
       if (m == 0xD9) {
         // k_idct reads each component's latched table from slot c
@@ -440,27 +502,32 @@ __global__ void __launch_bounds__(256) k_prog_zero(const ImgDesc* __restrict__ d
     p[i] = make_uint4(0, 0, 0, 0);
 }
 
-// One lane per progressive image: all its scans (see the header).
-__global__ void __launch_bounds__(64) k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables,
+// One wave per progressive image: its lane walks all the scans (see the header); kProgLanes images per workgroup,
+// each with its derived tables in LDS.
+constexpr int kProgLanes = 1;  // (lanes of one wave walking different images would diverge on every branch)
+__global__ void __launch_bounds__(kProgLanes) k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables,
                                              const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
                                              const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
                                              const int32_t* __restrict__ routes, int cap) {
-  const int li = blockIdx.x * 64 + threadIdx.x;
+  __shared__ PLds lds[kProgLanes];
+  for (int i = threadIdx.x; i < 80; i += kProgLanes) s_nat[i] = (uint8_t)natural_order(i);
+  __syncthreads();
+  const int li = blockIdx.x * kProgLanes + threadIdx.x;
   if (li >= routes[kRtProg]) return;
   const int img = route_list(routes, cap, kRtProg)[li];
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
   const int st = decode_progressive(d, &tables[img], blob + offsets[img], lengths[img],
                                     reinterpret_cast<int16_t*>(scratch + d->off_coef),
-                                    reinterpret_cast<ProgTables*>(scratch + d->off_ptab));
+                                    reinterpret_cast<ProgTables*>(scratch + d->off_ptab), lds[threadIdx.x]);
   if (st != SDSJ_OK) d->status = st;
 }
 
 hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* blob, const int64_t* offsets,
                        const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s) {
   hipLaunchKernelGGL(k_prog_zero, dim3(n, 16), dim3(256), 0, s, descs, scratch, routes, cap);
-  hipLaunchKernelGGL(k_prog, dim3((n + 63) / 64), dim3(64), 0, s, descs, tables, blob, offsets, lengths, scratch,
-                     routes, cap);
+  hipLaunchKernelGGL(k_prog, dim3((n + kProgLanes - 1) / kProgLanes), dim3(kProgLanes), 0, s, descs, tables, blob,
+                     offsets, lengths, scratch, routes, cap);
   return hipGetLastError();
 }
 
