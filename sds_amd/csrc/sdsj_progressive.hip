@@ -41,7 +41,7 @@ __device__ __forceinline__ int pbyte(PBits& b, int64_t i) {
   return (int)((v >> (8 * (o & 3))) & 0xFF);
 }
 
-__device__ void pfill(PBits& b) {
+__device__ __forceinline__ void pfill(PBits& b) {
   while (b.nbits <= 56) {
     int c;
     if (b.hit_marker || b.pos >= b.n) {
@@ -73,7 +73,7 @@ __device__ void pfill(PBits& b) {
   }
 }
 
-__device__ int pgetbits(PBits& b, int n) {
+__device__ __forceinline__ int pgetbits(PBits& b, int n) {
   if (n == 0) return 0;
   if (b.nbits < n) pfill(b);
   const int v = (int)(b.buf >> (64 - n));
@@ -88,20 +88,31 @@ struct PLds {
   int32_t maxcode[8][17];  // [slot][l], l = 1..16 (index 0 unused)
   int32_t valoff[8][17];
   uint8_t vals[8][256];
+  uint16_t look[4][1 << 9];  // per scan position: (length << 8) | symbol of the codes of <= 9 bits, 0 = longer
   alignas(16) int16_t blk[64];  // the block an AC refinement scan updates (read-modify-write in LDS)
+  int32_t qh[4], qv[4], qbo[4], qdsl[4], ldc[4];  // interleaved DC scans: per scan position h, v, block
+                                                  // offset in the MCU, DC table slot, DC predictor
 };
-__shared__ uint8_t s_nat[80];  // jpeg_natural_order (+ guards) for the workgroup
 
-// jdhuff.c jpeg_huff_decode: the code length is the first l whose l-bit prefix is <= maxcode[l]
-// (all 16 compares issue together on 17 peeked bits); no match = bad code: 17 bits, symbol 0.
-// Bits are consumed only after the length is known, so insufficient_data follows the consumed
-// count as with a bit-serial decode.
-__device__ int phuff(PBits& b, const PLds& L, int slot) {
+// jdhuff.c jpeg_huff_decode: codes of <= 9 bits come from the scan position's lookahead table in one
+// LDS read; longer (and bad) codes take the first l whose l-bit prefix is <= maxcode[l] (all 16
+// compares issue together on 17 peeked bits); no match = bad code: 17 bits, symbol 0.  Bits are
+// consumed only after the length is known, so insufficient_data follows the consumed count as with
+// a bit-serial decode.
+__device__ __forceinline__ int phuff(PBits& b, const PLds& L, int slot, int q) {
   if (b.nbits < 17) pfill(b);
+  const uint32_t e = L.look[q][(uint32_t)(b.buf >> 55)];
+  if (e) {
+    const int l = (int)(e >> 8);
+    b.buf <<= l;
+    b.nbits -= l;
+    if (b.nbits < b.pad_bits) b.insufficient = 1;
+    return (int)(e & 0xFF);
+  }
   const uint32_t peek = (uint32_t)(b.buf >> 47);
   int l = 17;
 #pragma unroll
-  for (int k = 16; k >= 1; k--) l = (int32_t)(peek >> (17 - k)) <= L.maxcode[slot][k] ? k : l;
+  for (int k = 16; k >= 10; k--) l = (int32_t)(peek >> (17 - k)) <= L.maxcode[slot][k] ? k : l;
   b.buf <<= l;
   b.nbits -= l;
   if (b.nbits < b.pad_bits) b.insufficient = 1;
@@ -112,7 +123,7 @@ __device__ int phuff(PBits& b, const PLds& L, int slot) {
 __device__ int pextend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)((~0u << s) + 1) : x; }
 
 // jdmarker.c next_marker from the byte cursor: pos ends on the marker's last FF; -1 at the end
-__device__ int pnext_marker(PBits& b) {
+__device__ __forceinline__ int pnext_marker(PBits& b) {
   for (;;) {
     while (b.pos < b.n && pbyte(b, b.pos) != 0xFF) b.pos++;
     if (b.pos >= b.n) return -1;
@@ -128,14 +139,14 @@ __device__ int pnext_marker(PBits& b) {
   }
 }
 
-__device__ void pconsume_marker(PBits& b) {
+__device__ __forceinline__ void pconsume_marker(PBits& b) {
   b.pos += 2;
   b.hit_marker = 0;
   b.marker = 0;
 }
 
 // read_restart_marker + jpeg_resync_to_restart (actions 1 / 2 / 3); -1 when the input ends first
-__device__ int pread_restart(PBits& b, int desired) {
+__device__ __forceinline__ int pread_restart(PBits& b, int desired) {
   if (!b.hit_marker) {
     const int m = pnext_marker(b);
     if (m < 0) return -1;
@@ -167,7 +178,7 @@ __device__ int pread_restart(PBits& b, int desired) {
   }
 }
 
-__device__ int pprocess_restart(PBits& b, int* next_num) {
+__device__ __forceinline__ int pprocess_restart(PBits& b, int* next_num) {
   b.buf = 0;
   b.nbits = 0;
   b.pad_bits = 0;
@@ -179,9 +190,10 @@ __device__ int pprocess_restart(PBits& b, int* next_num) {
 
 __device__ int rd16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
-// jdhuff.c jpeg_make_d_derived_tbl for slot (0..3 DC, 4..7 AC): canonical bounds; false when the
-// code assignment overflows (JERR_BAD_HUFF_TABLE), or a DC table holds a symbol > 15
-__device__ bool pderive(const ProgTables* P, PLds& L, int slot) {
+// jdhuff.c jpeg_make_d_derived_tbl for slot (0..3 DC, 4..7 AC) and scan position q: canonical
+// bounds plus the 9-bit lookahead table (a code of length l <= 9 fills its 2^(9-l) entries); false
+// when the code assignment overflows (JERR_BAD_HUFF_TABLE), or a DC table holds a symbol > 15
+__device__ bool pderive(const ProgTables* P, PLds& L, int slot, int q) {
   if (!P->defined[slot]) return false;
   int code = 0, p = 0;
   for (int l = 1; l <= 16; l++) {
@@ -198,6 +210,19 @@ __device__ bool pderive(const ProgTables* P, PLds& L, int slot) {
     for (int i = 0; i < p; i++)
       if (P->vals[slot][i] > 15) return false;
   for (int i = 0; i < 256; i++) L.vals[slot][i] = P->vals[slot][i];
+  uint4* lk = reinterpret_cast<uint4*>(L.look[q]);
+  for (int i = 0; i < 64; i++) lk[i] = make_uint4(0, 0, 0, 0);
+  code = 0;
+  p = 0;
+  for (int l = 1; l <= 9; l++) {
+    const int cnt = P->bits[slot][l], span = 1 << (9 - l);
+    for (int i = 0; i < cnt; i++, code++) {
+      const uint16_t e = (uint16_t)((l << 8) | P->vals[slot][p + i]);
+      for (int j = 0; j < span; j++) L.look[q][(code << (9 - l)) + j] = e;
+    }
+    p += cnt;
+    code <<= 1;
+  }
   return true;
 }
 
@@ -238,12 +263,16 @@ __device__ int pread_dqt(ProgTables* P, const uint8_t* s, int sl) {
   return SDSJ_OK;
 }
 
-// One block of one scan (jdphuff.c decode_mcu_DC_first / _DC_refine / _AC_first / _AC_refine).
-__device__ void pblock(PBits& b, const PLds& P, int dslot, int aslot, int16_t* blk, int ss, int se, int ah,
-                       int al, int* last_dc, int* eobrun) {
+// Blocks are kept in zigzag order while the scans run (k_prog_unzig puts them in natural order for
+// k_idct): zigzag index k is natural_order(k), and natural_order's guard entries past 63 are all 63.
+__device__ __forceinline__ int zig(int k) { return k < 63 ? k : 63; }
+
+// One block of a DC scan or an AC first scan (jdphuff.c decode_mcu_DC_first / _DC_refine / _AC_first).
+__device__ __forceinline__ void pblock(PBits& b, const PLds& P, int dslot, int aslot, int lq, int16_t* blk, int ss, int se,
+                       int ah, int al, int* last_dc, int* eobrun) {
   if (ss == 0) {
     if (ah == 0) {  // decode_mcu_DC_first
-      int s = phuff(b, P, dslot);
+      int s = phuff(b, P, dslot, lq);
       if (s) s = pextend(pgetbits(b, s), s);
       s += *last_dc;
       *last_dc = s;
@@ -253,44 +282,81 @@ __device__ void pblock(PBits& b, const PLds& P, int dslot, int aslot, int16_t* b
     }
     return;
   }
-  if (ah == 0) {  // decode_mcu_AC_first
-    if (*eobrun > 0) {
-      (*eobrun)--;
-      return;
-    }
-    for (int k = ss; k <= se; k++) {
-      const int sym = phuff(b, P, aslot);
-      const int r = sym >> 4, s = sym & 15;
-      if (s) {
-        k += r;
-        const int x = pgetbits(b, s);
-        blk[s_nat[k]] = (int16_t)((unsigned)pextend(x, s) << al);
-      } else if (r == 15) {
-        k += 15;
-      } else {
-        *eobrun = 1 << r;
-        if (r) *eobrun += pgetbits(b, r);
-        (*eobrun)--;
-        break;
-      }
-    }
+  // decode_mcu_AC_first
+  if (*eobrun > 0) {
+    (*eobrun)--;
     return;
   }
-  // decode_mcu_AC_refine, on an LDS copy of the block (its nonzero coefficients are read back)
-  int16_t* const gblk = blk;
-  {
-    uint4* dst = reinterpret_cast<uint4*>(const_cast<int16_t*>(P.blk));
-    const uint4* src = reinterpret_cast<const uint4*>(gblk);
-#pragma unroll
-    for (int i = 0; i < 8; i++) dst[i] = src[i];
+  for (int k = ss; k <= se; k++) {
+    const int sym = phuff(b, P, aslot, lq);
+    const int r = sym >> 4, s = sym & 15;
+    if (s) {
+      k += r;
+      const int x = pgetbits(b, s);
+      blk[zig(k)] = (int16_t)((unsigned)pextend(x, s) << al);
+    } else if (r == 15) {
+      k += 15;
+    } else {
+      *eobrun = 1 << r;
+      if (r) *eobrun += pgetbits(b, r);
+      (*eobrun)--;
+      break;
+    }
   }
-  blk = const_cast<int16_t*>(P.blk);
+}
+
+// bit 0: the low halfword of x is non-zero; bit 1: the high one
+__device__ __forceinline__ uint32_t nz2(uint32_t x) {
+  const uint32_t y = ((x & 0x7FFF7FFFu) + 0x7FFF7FFFu) | x;
+  return ((y >> 15) & 1u) | ((y >> 30) & 2u);
+}
+
+// Correction bits for the non-zero coefficients flagged in span, in zigzag order (one bit each, read
+// in chunks of up to 16): a 1 adds p1 away from zero unless that bit is already set.
+__device__ __forceinline__ void pcorrect(PBits& b, int16_t* blk, uint64_t span, int p1) {
+  while (span) {
+    const int cnt = min(__popcll(span), 16);
+    const int bits = pgetbits(b, cnt);
+    for (int i = cnt - 1; i >= 0; i--) {
+      const int pos = __ffsll((unsigned long long)span) - 1;
+      span &= span - 1;
+      if ((bits >> i) & 1) {
+        const int c = blk[pos];
+        if ((c & p1) == 0) blk[pos] = (int16_t)(c >= 0 ? c + p1 : c - p1);
+      }
+    }
+  }
+}
+
+// One block of an AC refinement scan (jdphuff.c decode_mcu_AC_refine).  The block (zigzag order) is
+// staged in LDS and a 64-bit mask of its
+// non-zero coefficients replaces the coefficient-by-coefficient walk: the stop of a run of r zeros
+// is the (r + 1)-th zero bit at or after k, and the non-zero coefficients passed on the way each
+// take one correction bit.
+__device__ __forceinline__ void prefine(PBits& b, PLds& P, int aslot, int16_t* gblk, int ss, int se, int al, int* eobrun) {
+  uint4 v[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = reinterpret_cast<const uint4*>(gblk)[i];
+  uint4* lb = reinterpret_cast<uint4*>(P.blk);
+  uint32_t mlo = 0, mhi = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    lb[i] = v[i];
+    lb[i + 4] = v[i + 4];
+    mlo |= (nz2(v[i].x) | nz2(v[i].y) << 2 | nz2(v[i].z) << 4 | nz2(v[i].w) << 6) << (8 * i);
+    mhi |= (nz2(v[i + 4].x) | nz2(v[i + 4].y) << 2 | nz2(v[i + 4].z) << 4 | nz2(v[i + 4].w) << 6) << (8 * i);
+  }
+  uint64_t nz = ((uint64_t)mhi << 32) | mlo;
+  int16_t* blk = P.blk;
   const int p1 = 1 << al, m1 = -(1 << al);
+  const uint64_t band = se >= 63 ? ~0ull : ((1ull << (se + 1)) - 1);  // positions <= se
+  auto below = [](int z) { return z >= 64 ? ~0ull : ((1ull << z) - 1); };
   int k = ss;
   if (*eobrun == 0) {
     for (; k <= se; k++) {
-      const int sym = phuff(b, P, aslot);
-      int r = sym >> 4, s = sym & 15;
+      const int sym = phuff(b, P, aslot, 0);
+      const int r = sym >> 4;
+      int s = sym & 15;
       if (s) {
         s = pgetbits(b, 1) ? p1 : m1;  // (s != 1: JWRN_HUFF_BAD_CODE, decoding goes on)
       } else if (r != 15) {
@@ -298,31 +364,25 @@ __device__ void pblock(PBits& b, const PLds& P, int dslot, int aslot, int16_t* b
         if (r) *eobrun += pgetbits(b, r);
         break;
       }
-      do {
-        int16_t* c = blk + s_nat[k];
-        if (*c != 0) {
-          if (pgetbits(b, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
-        } else if (--r < 0) {
-          break;
-        }
-        k++;
-      } while (k <= se);
-      if (s) blk[s_nat[k]] = (int16_t)s;
+      // skip r zero coefficients (correcting the non-zero ones passed), stop on the next zero
+      uint64_t zeros = ~nz & band & (~0ull << k);
+      for (int i = 0; i < r; i++) zeros &= zeros - 1;
+      const int z = zeros ? __ffsll((unsigned long long)zeros) - 1 : se + 1;
+      pcorrect(b, blk, nz & below(z) & (~0ull << k), p1);
+      k = z;
+      if (s) {
+        blk[zig(k)] = (int16_t)s;
+        nz |= 1ull << zig(k);
+      }
     }
   }
   if (*eobrun > 0) {
-    for (; k <= se; k++) {
-      int16_t* c = blk + s_nat[k];
-      if (*c != 0 && pgetbits(b, 1) && (*c & p1) == 0) *c = (int16_t)(*c >= 0 ? *c + p1 : *c + m1);
-    }
+    if (k <= se) pcorrect(b, blk, nz & band & (~0ull << k), p1);
     (*eobrun)--;
   }
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(blk);
-    uint4* dst = reinterpret_cast<uint4*>(gblk);
+  uint4* dst = reinterpret_cast<uint4*>(gblk);
 #pragma unroll
-    for (int i = 0; i < 8; i++) dst[i] = src[i];
-  }
+  for (int i = 0; i < 8; i++) dst[i] = lb[i];
 }
 
 // Every scan of image d, then the markers up to EOI.  Returns an SDSJ status.
@@ -343,8 +403,9 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
   for (int c = 0; c < kMaxComp; c++) P->latched[c] = 0;
   d->t_spec = d->t_sync = d->t_scan = d->t_write = 0;
   int restart_interval = d->restart_interval;
-  int boff[kMaxComp] = {0, 0, 0};
-  for (int c = 1; c < d->ncomp; c++) boff[c] = boff[c - 1] + d->comp[c - 1].h * d->comp[c - 1].v;
+  // first block of components 1 and 2 within an MCU
+  const int boff1 = d->ncomp > 1 ? d->comp[0].h * d->comp[0].v : 0;
+  const int boff2 = d->ncomp > 2 ? boff1 + d->comp[1].h * d->comp[1].v : 0;
   int64_t pos = d->sos_pos;
   for (;;) {
     if (pos + 2 > n) return SDSJ_CORRUPT;
@@ -354,8 +415,11 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
     if (sl < 1) return SDSJ_CORRUPT;
     const int ns = s[0];
     if (ns < 1 || ns > 4 || sl != 2 * ns + 4) return SDSJ_CORRUPT;  // get_sos: JERR_BAD_LENGTH
-    int comps[4], td[4], ta[4];
-    for (int q = 0; q < ns; q++) {
+    // (per-position arrays are indexed only from unrolled loops, so they stay in registers)
+    int comps[4] = {0, 0, 0, 0}, td[4] = {0, 0, 0, 0}, ta[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (q >= ns) break;
       const int cid = s[1 + 2 * q];
       int c = 0;
       while (c < d->ncomp && d->comp_id[c] != cid) c++;
@@ -371,7 +435,9 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
     if (ah != 0 && al != ah - 1) bad = true;
     if (al > 13) bad = true;
     if (bad) return SDSJ_CORRUPT;  // JERR_BAD_PROGRESSION
-    for (int q = 0; q < ns; q++) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (q >= ns) break;
       const int c = comps[q], tq = d->comp[c].tq;
       if (!P->latched[c]) {  // latch_quant_tables: the component's table at its first scan
         if (!P->qt_defined[tq]) return SDSJ_CORRUPT;
@@ -379,18 +445,29 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
         P->latched[c] = 1;
       }
       if (ss == 0 && ah == 0) {
-        if (td[q] > 3 || !pderive(P, L, td[q])) return SDSJ_CORRUPT;
+        if (td[q] > 3 || !pderive(P, L, td[q], q)) return SDSJ_CORRUPT;
       } else if (ss != 0) {
-        if (ta[q] > 3 || !pderive(P, L, 4 + ta[q])) return SDSJ_CORRUPT;
+        if (ta[q] > 3 || !pderive(P, L, 4 + ta[q], q)) return SDSJ_CORRUPT;
       }
     }
     // the scan's geometry in registers (descriptor reads would repeat for every block: the
     // coefficient stores may alias them as far as the compiler knows)
-    int sh[4], sv[4], sbw[4];
-    for (int q = 0; q < ns; q++) {
+    int sh[4] = {1, 1, 1, 1}, sv[4] = {1, 1, 1, 1}, sbw[4] = {0, 0, 0, 0}, sbo[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (q >= ns) break;
       sh[q] = d->comp[comps[q]].h;
       sv[q] = d->comp[comps[q]].v;
       sbw[q] = d->comp[comps[q]].bw;
+      sbo[q] = comps[q] == 0 ? 0 : comps[q] == 1 ? boff1 : boff2;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      L.qh[q] = sh[q];
+      L.qv[q] = sv[q];
+      L.qbo[q] = sbo[q];
+      L.qdsl[q] = td[q] & 3;
+      L.ldc[q] = 0;
     }
     const int mcux = d->mcux, bpm = d->bpm, ncomp = d->ncomp;
     // jdinput.c per_scan_setup: a single-component scan walks that component's own block grid
@@ -410,32 +487,68 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
     b.buf = 0;
     b.nbits = b.hit_marker = b.marker = b.pad_bits = b.insufficient = b.eof = 0;
     b.wbase = 1;  // (no window yet: never 16-byte aligned)
-    int last_dc[4] = {0, 0, 0, 0}, eobrun = 0;
+    int ldc0 = 0, eobrun = 0;  // (a single-component scan's DC predictor; interleaved ones: L.ldc)
     int restarts_left = restart_interval, next_num = 0;
+    // block cursor of a single-component scan, kept incrementally (no divisions per block): (bx, by)
+    // in the component's grid, (mx, my) its MCU, (sx, sy) its place in the MCU
+    int bx = 0, by = 0, mx = 0, my = 0, sx = 0, sy = 0;
+    const int ch0 = sh[0], cv0 = sv[0], bw0 = sbw[0], bo0 = sbo[0];
+    const int dsl0 = td[0] & 3, asl0 = 4 + (ta[0] & 3);
+    auto gpos = [&]() -> int64_t {
+      return ncomp == 1 ? (int64_t)by * bw0 + bx : ((int64_t)my * mcux + mx) * bpm + bo0 + sy * ch0 + sx;
+    };
+    const bool refine = ss != 0 && ah != 0;
+    int64_t gn = ns == 1 ? gpos() : 0;
     for (int m = 0; m < nmcu; m++) {
+      const int64_t g1 = gn;
+      if (ns == 1) {
+        bx++;
+        if (++sx == ch0) {
+          sx = 0;
+          mx++;
+        }
+        if (bx == cwb) {
+          bx = sx = mx = 0;
+          by++;
+          if (++sy == cv0) {
+            sy = 0;
+            my++;
+          }
+        }
+        gn = gpos();
+      }
       if (restart_interval) {
         if (restarts_left == 0) {
           if (pprocess_restart(b, &next_num)) return SDSJ_CORRUPT;
-          last_dc[0] = last_dc[1] = last_dc[2] = last_dc[3] = 0;
+          ldc0 = L.ldc[0] = L.ldc[1] = L.ldc[2] = L.ldc[3] = 0;
           eobrun = 0;
           restarts_left = restart_interval;
         }
         restarts_left--;
       }
+      if (refine) {
+        if (!b.insufficient) prefine(b, L, asl0, coef + g1 * 64, ss, se, al, &eobrun);
+        continue;
+      }
       if (b.insufficient) continue;  // the MCU's coefficients stay as they are
+      if (ns == 1) {
+        pblock(b, L, dsl0, asl0, 0, coef + g1 * 64, ss, se, ah, al, &ldc0, &eobrun);
+        continue;
+      }
       for (int q = 0; q < ns; q++) {
-        const int c = comps[q];
-        const int ch = sh[q], cv = sv[q];
-        const int hh = ns == 1 ? 1 : ch, vv = ns == 1 ? 1 : cv;
-        for (int v = 0; v < vv; v++)
-          for (int h = 0; h < hh; h++) {
-            const int bx = ns == 1 ? m % cwb : (m % mcux) * ch + h;
-            const int by = ns == 1 ? m / cwb : (m / mcux) * cv + v;
-            // block (bx, by) of component c in the MCU-ordered coefficient array
-            const int64_t g = ncomp == 1 ? (int64_t)by * sbw[q] + bx
-                                         : ((int64_t)(by / cv) * mcux + bx / ch) * bpm + boff[c] + (by % cv) * ch +
-                                               (bx % ch);
-            pblock(b, L, td[q] & 3, 4 + (ta[q] & 3), coef + g * 64, ss, se, ah, al, &last_dc[q], &eobrun);
+        const int ch = L.qh[q], cv = L.qv[q];
+        for (int v = 0; v < cv; v++)
+          for (int h = 0; h < ch; h++) {
+            // block (h, v) of component c in MCU m: ((by / cv) * mcux + bx / ch) * bpm + ... with
+            // bx = (m % mcux) * ch + h, by = (m / mcux) * cv + v reduces to m * bpm + ...
+            int64_t g;
+            if (ncomp == 1) {  // (a single-component frame lists its component more than once)
+              const int gx = (m % mcux) * ch + h, gy = (m / mcux) * cv + v;
+              g = (int64_t)gy * sbw[q] + gx;
+            } else {
+              g = (int64_t)m * bpm + L.qbo[q] + v * ch + h;
+            }
+            pblock(b, L, L.qdsl[q], 4, q, coef + g * 64, ss, se, ah, al, &L.ldc[q], &eobrun);
           }
       }
     }
@@ -502,6 +615,43 @@ __global__ void __launch_bounds__(256) k_prog_zero(const ImgDesc* __restrict__ d
     p[i] = make_uint4(0, 0, 0, 0);
 }
 
+// Zigzag -> natural order for the blocks of the progressive images (one block per thread, through LDS).
+__global__ void __launch_bounds__(256) k_prog_unzig(const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                                    const int32_t* __restrict__ routes, int cap) {
+  __shared__ uint8_t nat[64];
+  __shared__ int16_t t[256][65];
+  if (threadIdx.x < 64) nat[threadIdx.x] = (uint8_t)natural_order(threadIdx.x);
+  __syncthreads();
+  if ((int)blockIdx.x >= routes[kRtProg]) return;
+  const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[blockIdx.x]];
+  if (d->status != SDSJ_OK) return;
+  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
+  const int64_t nb = d->total_blocks;
+  for (int64_t b0 = (int64_t)blockIdx.y * 256; b0 < nb; b0 += (int64_t)gridDim.y * 256) {
+    // 256 blocks: coalesced dword reads into LDS rows, each thread permutes its row, coalesced writes
+    const int nblk = (int)min<int64_t>(256, nb - b0);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(coef + b0 * 64);
+    for (int i = threadIdx.x; i < nblk * 32; i += 256) {
+      const uint32_t w = src[i];
+      t[i >> 5][(i & 31) * 2] = (int16_t)(w & 0xFFFF);
+      t[i >> 5][(i & 31) * 2 + 1] = (int16_t)(w >> 16);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nblk) {
+      int16_t z[64];
+#pragma unroll
+      for (int k = 0; k < 64; k++) z[k] = t[threadIdx.x][k];
+#pragma unroll
+      for (int k = 0; k < 64; k++) t[threadIdx.x][nat[k]] = z[k];
+    }
+    __syncthreads();
+    uint32_t* dst = reinterpret_cast<uint32_t*>(coef + b0 * 64);
+    for (int i = threadIdx.x; i < nblk * 32; i += 256)
+      dst[i] = (uint32_t)(uint16_t)t[i >> 5][(i & 31) * 2] | (uint32_t)(uint16_t)t[i >> 5][(i & 31) * 2 + 1] << 16;
+    __syncthreads();
+  }
+}
+
 // One wave per progressive image: its lane walks all the scans (see the header); kProgLanes images per workgroup,
 // each with its derived tables in LDS.
 constexpr int kProgLanes = 1;  // (lanes of one wave walking different images would diverge on every branch)
@@ -510,8 +660,6 @@ __global__ void __launch_bounds__(kProgLanes) k_prog(ImgDesc* __restrict__ descs
                                              const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
                                              const int32_t* __restrict__ routes, int cap) {
   __shared__ PLds lds[kProgLanes];
-  for (int i = threadIdx.x; i < 80; i += kProgLanes) s_nat[i] = (uint8_t)natural_order(i);
-  __syncthreads();
   const int li = blockIdx.x * kProgLanes + threadIdx.x;
   if (li >= routes[kRtProg]) return;
   const int img = route_list(routes, cap, kRtProg)[li];
@@ -528,6 +676,7 @@ hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* 
   hipLaunchKernelGGL(k_prog_zero, dim3(n, 16), dim3(256), 0, s, descs, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog, dim3((n + kProgLanes - 1) / kProgLanes), dim3(kProgLanes), 0, s, descs, tables, blob,
                      offsets, lengths, scratch, routes, cap);
+  hipLaunchKernelGGL(k_prog_unzig, dim3(n, 8), dim3(256), 0, s, descs, scratch, routes, cap);
   return hipGetLastError();
 }
 
