@@ -40,7 +40,7 @@ extern "C" {
 /* status codes (per call and per sample) */
 #define SDSJ_OK 0
 #define SDSJ_EINVAL (-1)      /* bad argument */
-#define SDSJ_UNSUPPORTED (-2) /* valid JPEG the MI355X path does not decode (progressive, CMYK, ...) */
+#define SDSJ_UNSUPPORTED (-2) /* valid JPEG the MI355X path does not decode (arithmetic, 12-bit, CMYK, ...) */
 #define SDSJ_CORRUPT (-3)     /* malformed / truncated stream (PIL raises OSError) */
 #define SDSJ_ENOMEM (-4)      /* allocation failed */
 #define SDSJ_EHIP (-5)        /* HIP runtime error (see sdsj_last_error) */
