@@ -73,6 +73,15 @@ __device__ __forceinline__ void pfill(PBits& b) {
   }
 }
 
+// n (1..32) bits the caller knows are in the buffer (phuff left >= 32 after its symbol's start)
+__device__ __forceinline__ int pgetbits_nc(PBits& b, int n) {
+  const int v = (int)(b.buf >> (64 - n));
+  b.buf <<= n;
+  b.nbits -= n;
+  if (b.nbits < b.pad_bits) b.insufficient = 1;
+  return v;
+}
+
 __device__ __forceinline__ int pgetbits(PBits& b, int n) {
   if (n == 0) return 0;
   if (b.nbits < n) pfill(b);
@@ -99,8 +108,10 @@ struct PLds {
 // compares issue together on 17 peeked bits); no match = bad code: 17 bits, symbol 0.  Bits are
 // consumed only after the length is known, so insufficient_data follows the consumed count as with
 // a bit-serial decode.
+// The buffer holds >= 32 bits when the symbol starts, so its extra bits (<= 15, or 1 + a correction
+// bit) need no second check.
 __device__ __forceinline__ int phuff(PBits& b, const PLds& L, int slot, int q) {
-  if (b.nbits < 17) pfill(b);
+  if (b.nbits < 32) pfill(b);
   const uint32_t e = L.look[q][(uint32_t)(b.buf >> 55)];
   if (e) {
     const int l = (int)(e >> 8);
@@ -273,7 +284,7 @@ __device__ __forceinline__ void pblock(PBits& b, const PLds& P, int dslot, int a
   if (ss == 0) {
     if (ah == 0) {  // decode_mcu_DC_first
       int s = phuff(b, P, dslot, lq);
-      if (s) s = pextend(pgetbits(b, s), s);
+      if (s) s = pextend(pgetbits_nc(b, s), s);
       s += *last_dc;
       *last_dc = s;
       blk[0] = (int16_t)((unsigned)s << al);
@@ -292,17 +303,42 @@ __device__ __forceinline__ void pblock(PBits& b, const PLds& P, int dslot, int a
     const int r = sym >> 4, s = sym & 15;
     if (s) {
       k += r;
-      const int x = pgetbits(b, s);
+      const int x = pgetbits_nc(b, s);
       blk[zig(k)] = (int16_t)((unsigned)pextend(x, s) << al);
     } else if (r == 15) {
       k += 15;
     } else {
       *eobrun = 1 << r;
-      if (r) *eobrun += pgetbits(b, r);
+      if (r) *eobrun += pgetbits_nc(b, r);
       (*eobrun)--;
       break;
     }
   }
+}
+
+// Position of the (r + 1)-th zero bit of nz within window (popcount binary search, no loop over r);
+// se + 1 when the window holds r or fewer zeros.
+__device__ __forceinline__ int pnth_zero(uint64_t nz, uint64_t window, int r, int se) {
+  const uint64_t zeros = ~nz & window;
+  if (__popcll(zeros) <= r) return se + 1;
+  uint32_t w = (uint32_t)zeros;
+  int pos = 0;
+  const int c32 = __popc(w);
+  if (r >= c32) {
+    r -= c32;
+    w = (uint32_t)(zeros >> 32);
+    pos = 32;
+  }
+#pragma unroll
+  for (int h = 16; h >= 1; h >>= 1) {
+    const int c = __popc(w & ((1u << h) - 1));
+    if (r >= c) {
+      r -= c;
+      w >>= h;
+      pos += h;
+    }
+  }
+  return pos;
 }
 
 // bit 0: the low halfword of x is non-zero; bit 1: the high one
@@ -358,16 +394,14 @@ __device__ __forceinline__ void prefine(PBits& b, PLds& P, int aslot, int16_t* g
       const int r = sym >> 4;
       int s = sym & 15;
       if (s) {
-        s = pgetbits(b, 1) ? p1 : m1;  // (s != 1: JWRN_HUFF_BAD_CODE, decoding goes on)
+        s = pgetbits_nc(b, 1) ? p1 : m1;  // (s != 1: JWRN_HUFF_BAD_CODE, decoding goes on)
       } else if (r != 15) {
         *eobrun = 1 << r;
-        if (r) *eobrun += pgetbits(b, r);
+        if (r) *eobrun += pgetbits_nc(b, r);
         break;
       }
       // skip r zero coefficients (correcting the non-zero ones passed), stop on the next zero
-      uint64_t zeros = ~nz & band & (~0ull << k);
-      for (int i = 0; i < r; i++) zeros &= zeros - 1;
-      const int z = zeros ? __ffsll((unsigned long long)zeros) - 1 : se + 1;
+      const int z = pnth_zero(nz, band & (~0ull << k), r, se);
       pcorrect(b, blk, nz & below(z) & (~0ull << k), p1);
       k = z;
       if (s) {
