@@ -649,40 +649,36 @@ __global__ void __launch_bounds__(256) k_prog_zero(const ImgDesc* __restrict__ d
     p[i] = make_uint4(0, 0, 0, 0);
 }
 
-// Zigzag -> natural order for the blocks of the progressive images (one block per thread, through LDS).
+// Zigzag -> natural order for the blocks of the progressive images: one block per thread, its 128
+// bytes in registers, the permutation resolved at compile time (no LDS, so the launch stays cheap
+// for batches without progressive images).
 __global__ void __launch_bounds__(256) k_prog_unzig(const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
                                                     const int32_t* __restrict__ routes, int cap) {
-  __shared__ uint8_t nat[64];
-  __shared__ int16_t t[256][65];
-  if (threadIdx.x < 64) nat[threadIdx.x] = (uint8_t)natural_order(threadIdx.x);
-  __syncthreads();
   if ((int)blockIdx.x >= routes[kRtProg]) return;
   const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[blockIdx.x]];
   if (d->status != SDSJ_OK) return;
   int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
   const int64_t nb = d->total_blocks;
-  for (int64_t b0 = (int64_t)blockIdx.y * 256; b0 < nb; b0 += (int64_t)gridDim.y * 256) {
-    // 256 blocks: coalesced dword reads into LDS rows, each thread permutes its row, coalesced writes
-    const int nblk = (int)min<int64_t>(256, nb - b0);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(coef + b0 * 64);
-    for (int i = threadIdx.x; i < nblk * 32; i += 256) {
-      const uint32_t w = src[i];
-      t[i >> 5][(i & 31) * 2] = (int16_t)(w & 0xFFFF);
-      t[i >> 5][(i & 31) * 2 + 1] = (int16_t)(w >> 16);
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < nblk) {
-      int16_t z[64];
+  for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < nb; i += (int64_t)gridDim.y * 256) {
+    uint4* p = reinterpret_cast<uint4*>(coef + i * 64);
+    uint32_t z[32], o[32];
 #pragma unroll
-      for (int k = 0; k < 64; k++) z[k] = t[threadIdx.x][k];
-#pragma unroll
-      for (int k = 0; k < 64; k++) t[threadIdx.x][nat[k]] = z[k];
+    for (int q = 0; q < 8; q++) {
+      const uint4 v = p[q];
+      z[4 * q] = v.x;
+      z[4 * q + 1] = v.y;
+      z[4 * q + 2] = v.z;
+      z[4 * q + 3] = v.w;
     }
-    __syncthreads();
-    uint32_t* dst = reinterpret_cast<uint32_t*>(coef + b0 * 64);
-    for (int i = threadIdx.x; i < nblk * 32; i += 256)
-      dst[i] = (uint32_t)(uint16_t)t[i >> 5][(i & 31) * 2] | (uint32_t)(uint16_t)t[i >> 5][(i & 31) * 2 + 1] << 16;
-    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 32; q++) o[q] = 0;
+#pragma unroll
+    for (int k = 0; k < 64; k++) {
+      const int j = natural_order(k);
+      o[j >> 1] |= ((z[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu) << ((j & 1) * 16);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
   }
 }
 
