@@ -246,3 +246,17 @@ def test_progressive_full_resolution_and_damaged_streams(engine):
         assert int(st[k]) == ost, f"sample {k}: gpu {int(st[k])} vs oracle {ost}"
         if ost == O.OK:
             np.testing.assert_array_equal(got[k].cpu().numpy(), ref, err_msg=f"sample {k}")
+
+
+def test_progressive_bench_sized_images_vs_oracle(engine):
+    """The progressive bench's own inputs (640x480 q90, PIL's scan script) and a 1920x1080 4:4:4
+    one, decoded + resized on the GPU, bit-exact against the oracle (tools/prog_bench.py measures
+    these shapes)."""
+    from tests.golden.synth import encode_jpeg, synth_rgb
+    jpgs = [encode_jpeg(synth_rgb(np.random.default_rng(1234 + i), 640, 480), 90, progressive=True) for i in range(3)]
+    jpgs.append(encode_jpeg(synth_rgb(np.random.default_rng(99), 1920, 1080), 95, progressive=True, subsampling=0))
+    for res in ((256, 256), (480, 640)):
+        got, st = engine.decode_resize(jpgs, res)
+        assert (st == 0).all(), st
+        for k, j in enumerate(jpgs):
+            np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res), err_msg=f"image {k} at {res}")
