@@ -43,6 +43,27 @@ __device__ __forceinline__ int pbyte(PBits& b, int64_t i) {
 
 __device__ __forceinline__ void pfill(PBits& b) {
   while (b.nbits <= 56) {
+    // fast path: 4 bytes inside the window with no 0xFF among them go in at once
+    if (b.nbits <= 32 && !b.hit_marker && b.pos + 4 <= b.n) {
+      const uintptr_t a = reinterpret_cast<uintptr_t>(b.d + b.pos), base = a & ~(uintptr_t)15;
+      const uint32_t o = (uint32_t)(a - base);
+      if (o <= 12) {
+        if (base != b.wbase) {
+          b.wbase = base;
+          b.w = *reinterpret_cast<const uint4*>(base);
+        }
+        const uint32_t i = o >> 2;
+        const uint32_t lo = i == 0 ? b.w.x : i == 1 ? b.w.y : i == 2 ? b.w.z : b.w.w;
+        const uint32_t hi = i == 0 ? b.w.y : i == 1 ? b.w.z : b.w.w;  // (unused when o == 12)
+        const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, o & 3), t = ~x;
+        if (((t - 0x01010101u) & ~t & 0x80808080u) == 0) {
+          b.buf |= (uint64_t)__builtin_bswap32(x) << (32 - b.nbits);
+          b.nbits += 32;
+          b.pos += 4;
+          continue;
+        }
+      }
+    }
     int c;
     if (b.hit_marker || b.pos >= b.n) {
       if (!b.hit_marker) b.eof = 1;
