@@ -37,8 +37,12 @@ __device__ __forceinline__ int pbyte(PBits& b, int64_t i) {
     b.wbase = base;
     b.w = *reinterpret_cast<const uint4*>(base);
   }
-  const uint32_t o = (uint32_t)(a - base), v = o < 8 ? (o < 4 ? b.w.x : b.w.y) : (o < 12 ? b.w.z : b.w.w);
-  return (int)((v >> (8 * (o & 3))) & 0xFF);
+  // (the window is picked from computed values, not from field loads: a select between loads of
+  // b.w's fields becomes a select between their addresses, and the bit reader state then stays in
+  // scratch memory instead of registers)
+  const uint32_t o = (uint32_t)(a - base);
+  const uint64_t lo = ((uint64_t)b.w.y << 32) | b.w.x, hi = ((uint64_t)b.w.w << 32) | b.w.z;
+  return (int)((((o & 8) ? hi : lo) >> (8 * (o & 7))) & 0xFF);
 }
 
 __device__ __forceinline__ void pfill(PBits& b) {
@@ -52,10 +56,11 @@ __device__ __forceinline__ void pfill(PBits& b) {
           b.wbase = base;
           b.w = *reinterpret_cast<const uint4*>(base);
         }
-        const uint32_t i = o >> 2;
-        const uint32_t lo = i == 0 ? b.w.x : i == 1 ? b.w.y : i == 2 ? b.w.z : b.w.w;
-        const uint32_t hi = i == 0 ? b.w.y : i == 1 ? b.w.z : b.w.w;  // (unused when o == 12)
-        const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, o & 3), t = ~x;
+        // bytes o .. o + 3 of the 16-byte window (a 128-bit shift; see pbyte)
+        const uint64_t lo = ((uint64_t)b.w.y << 32) | b.w.x, hi = ((uint64_t)b.w.w << 32) | b.w.z;
+        const uint32_t sh = 8 * (o & 7);
+        const uint64_t q = (o & 8) ? hi >> sh : (sh ? (lo >> sh) | (hi << (64 - sh)) : lo);
+        const uint32_t x = (uint32_t)q, t = ~x;
         if (((t - 0x01010101u) & ~t & 0x80808080u) == 0) {
           b.buf |= (uint64_t)__builtin_bswap32(x) << (32 - b.nbits);
           b.nbits += 32;
