@@ -5,15 +5,22 @@ Workload (BASELINE.json configs[1]): synthetic 640x480 q90 bas
 (4:2:0, Annex-K tables, no DRI) resident in HBM -- 100,000 rows per GPU, row i holding the
 encoded bytes of pool image i % POOL (each row is its own copy in HBM, so every launch reads its
 compressed bytes from HBM) -- decoded, centre-cropped and bilinear-resized to 256x256 uint8 CHW
-by the C-ABI engine.  One step = one batch of ``--batch`` rows.  Multi-GPU: one process per GPU,
-rank r owns rows [r*N, (r+1)*N) of an R*N-row index (sds/index.py:227-246 INTER_NODE slicing),
-no collective on the data path ("scaling": "weak").
+by the C-ABI engine.  One step = one batch of ``--batch`` rows.
+
+Multi-GPU (configs[3]): one process per GPU.  ``--gpus N`` outside torchrun starts N fresh child
+processes (before anything touches the GPU here), each with RANK / WORLD_SIZE / LOCAL_RANK set;
+under torchrun the ranks come from its environment.  Rank r owns rows [r*N_r, (r+1)*N_r) of an
+R*N_r-row index (sds/index.py:227-246 INTER_NODE slicing), no collective on the data path
+("scaling": "weak"); the process group (RCCL) only carries the barriers and the max-over-ranks of
+the timed region.
 
 Prints ONE JSON line (rank 0).  ``roofline`` prices the dominant kernel: algorithmic bytes per
-launch (compressed bytes in + output bytes out) / that kernel's mean device time
-from HIP events recorded around it on the launch stream during the timed region.
-``cpu_baseline`` times the reference's PIL/libjpeg-turbo pipeline (functional.py:94-110 op order)
-on a bounded sample of the same workload on this host's cores (rank 0, N=1 only).
+launch (compressed bytes in + output bytes out) / that kernel's mean duration,
+measured with HIP events on its launch stream in a single-lane pass after the timed region (one
+dispatch per kernel per batch, nothing overlapping it; rocprofv3 summaries under profiles/).
+``cpu_baseline`` times the reference's PIL/libjpeg-turbo pipeline (functional.py:94-110 op order,
+files read as LoadFromDiskTransform does) over a folder of the same JPEGs on this host's cores
+(rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -21,7 +28,11 @@ import argparse
 import json
 import multiprocessing as mp
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -31,25 +42,17 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 PMC_JSON = os.path.join(REPO, "profiles", "pmc_latest.json")  # tools/pmc.sh + tools/pmc_summary.py output
+BOX_CPU_SHARE = 16  # host CPUs a one-GPU box allots (nproc there shows the whole machine)
 # engine stage -> kernels launched in it (rocprofv3 kernel names contain these)
-STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_unstuff"], "entsync": ["k_entsync"],
-                 "entwrite": ["k_entwrite"], "idct": ["k_idct"], "color": ["k_color"], "coeffs": ["k_coeffs"],
-                 "hpass": ["k_hpass"], "vpass": ["k_vpass"], "resample": ["k_resample", "k_rs420"]}
-
-
-def engine_lanes(batch: int) -> int:
-    """Lanes the engine splits a batch into (sdsj_engine.hip run_chunk: SDSJ_LANES, default 4, at most 4,
-    at least 256 images per lane).  Each lane dispatches every kernel once per batch."""
-    n = max(1, min(int(os.environ.get("SDSJ_LANES", "4")), 4))
-    while n > 1 and batch < 256 * n:
-        n -= 1
-    return n
+STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_unstuff"],
+                 "entsync": ["k_enttab", "k_entspec", "k_entsync"], "entwrite": ["k_entwrite"], "idct": ["k_idct"],
+                 "color": ["k_color"], "coeffs": ["k_coeffs"], "hpass": ["k_hpass"], "vpass": ["k_vpass"],
+                 "resample": ["k_resample", "k_rs420", "k_finish"]}
 
 
 def pmc_traffic(stage: str, batch: int, lanes: int):
-    """HBM bytes per launch (one lane's dispatch) of `stage` from the committed PMC summary
-    (FETCH_SIZE + WRITE_SIZE, KB as rocprofv3 reports them, summed over the stage's kernels), if it
-    was collected at this batch size and lane count."""
+    """HBM bytes per launch of `stage` from the committed PMC summary (FETCH_SIZE + WRITE_SIZE, KB as
+    rocprofv3 reports them, summed over the stage's kernels), if collected at this batch and lane count."""
     try:
         with open(PMC_JSON) as f:
             pmc = json.load(f)
@@ -62,9 +65,10 @@ def pmc_traffic(stage: str, batch: int, lanes: int):
         if any(k in name for k in STAGE_KERNELS.get(stage, [])) and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
             tot += (ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024.0
             hit = True
-    return {"bytes_per_launch": round(tot), "source": os.path.relpath(PMC_JSON, REPO),
-            "note": "FETCH_SIZE + WRITE_SIZE as reported (MI355X_MICROARCH.md: FETCH_SIZE counts 1/2 of 16-B/lane "
-                    "streaming reads; these kernels read <= 4 B/lane, uncalibrated)"} if hit else None
+    return {"bytes_per_launch": round(tot), "source": os.path.relpath(PMC_JSON, REPO), "head": pmc.get("head"),
+            "note": "FETCH_SIZE + WRITE_SIZE as reported, separate --pmc passes (MI355X_MICROARCH.md: FETCH_SIZE "
+                    "counts 1/2 of 16-B/lane streaming reads; these kernels read <= 4 B/lane, uncalibrated)"} \
+        if hit else None
 
 
 def _make_pool_image(i: int) -> bytes:
@@ -118,22 +122,24 @@ def _pil_pipeline(jpg: bytes, res: int = 256, flip: bool = False, normalize: boo
 
 
 def _cpu_worker(args):
-    jpgs, seconds, res, mixed = args
+    paths, seconds, res, mixed = args
     import torch
     torch.set_num_threads(1)
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        _pil_pipeline(jpgs[n % len(jpgs)], res, flip=mixed and n % 2 == 1, normalize=mixed)
+        with open(paths[n % len(paths)], "rb") as f:  # LoadFromDiskTransform, presets.py:613-626
+            jpg = f.read()
+        _pil_pipeline(jpg, res, flip=mixed and n % 2 == 1, normalize=mixed)
         n += 1
     return n, time.perf_counter() - t0
 
 
-def cpu_baseline(pool: list[bytes], procs: int, seconds: float, res: int = 256, mixed: bool = False) -> float:
+def cpu_baseline(paths: list[str], procs: int, seconds: float, res: int = 256, mixed: bool = False) -> float:
     if procs <= 1:
-        n, dt = _cpu_worker((pool, seconds, res, mixed))
+        n, dt = _cpu_worker((paths, seconds, res, mixed))
         return n / dt
     with mp.get_context("spawn").Pool(procs) as p:
-        res_ = p.map(_cpu_worker, [(pool[k::procs] or pool, seconds, res, mixed) for k in range(procs)])
+        res_ = p.map(_cpu_worker, [(paths[k::procs] or paths, seconds, res, mixed) for k in range(procs)])
     return sum(n for n, _ in res_) / max(dt for _, dt in res_)
 
 
@@ -142,6 +148,68 @@ def host_cores() -> int:
         return len(os.sched_getaffinity(0))
     except AttributeError:
         return os.cpu_count() or 1
+
+
+# ---------------------------------------------------------------- multi-rank launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv: list[str], timeout: float = 3000.0) -> int:
+    """Starts n fresh rank processes of this script (nothing here has touched the GPU) and waits for
+    them; if one fails, the others are stopped (by PID) so no rank waits at a barrier forever."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    t0, rc = time.time(), 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is not None:
+                live.remove(p)
+                rc = rc or c
+        if rc or time.time() - t0 > timeout:
+            for p in live:
+                p.kill()
+            for p in live:
+                p.wait()
+            return rc or 124
+        time.sleep(0.05)
+    return rc
+
+
+class StubEngine:
+    """CPU stand-in of JpegEngine for the launcher test (--engine stub): touches its inputs, writes
+    zeros and OK statuses; no decoding."""
+
+    def __init__(self, *a, **k):
+        self.lanes = 4
+
+    def decode_resize_device(self, blob, offsets, lengths, resolution, *, out, status, normalize=False, flip=None,
+                             **kw):
+        out.zero_()
+        status.zero_()
+        return out, status
+
+    def set_timing(self, enable):
+        pass
+
+    def set_lanes(self, lanes):
+        self.lanes = lanes
+
+    def stage_times(self):
+        return {"entwrite": 1.0}
+
+    def counters(self, reset=False):
+        return {}
 
 
 # ---------------------------------------------------------------- main
@@ -158,8 +226,12 @@ def main():
     ap.add_argument("--pool", type=int, default=None, help="distinct encoded images")
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--cpu-files", type=int, default=1000, help="files in the CPU-baseline folder (configs[0])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-steps", type=int, default=5, help="single-lane steps timed for the roofline")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl", help="process group (nccl = RCCL)")
+    ap.add_argument("--engine", choices=["hip", "stub"], default="hip", help="stub: CPU stand-in (launcher tests)")
     args = ap.parse_args()
     mixed = args.workload == "mixed512"
     defaults = {"batch": 512, "rows": 16384, "pool": 96, "res": 512} if mixed else \
@@ -168,22 +240,35 @@ def main():
         if getattr(args, k) is None:
             setattr(args, k, v)
 
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+
     import torch
     import torch.distributed as dist
 
+    stub = args.engine == "stub"
     rank, world, local_rank = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), \
         int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus and "RANK" in os.environ and args.gpus > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    dev = torch.device("cpu") if stub else torch.device("cuda", local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+        if stub:
+            dist.init_process_group(args.backend, rank=rank, world_size=world)
+        else:
+            torch.cuda.set_device(dev)
+            dist.init_process_group(args.backend, rank=rank, world_size=world, device_id=dev)
+    elif not stub:
+        torch.cuda.set_device(dev)
+
+    def sync():
+        if not stub:
+            torch.cuda.synchronize()
 
     from sds_amd.distributed import compute_index_slice, max_over_ranks
-    from sds_amd.engine import JpegEngine
 
-    workers = max(1, min(16, host_cores()) // max(1, world))
+    workers = max(1, min(BOX_CPU_SHARE, host_cores()) // max(1, world))
     pool = make_pool(args.pool, workers, _make_mixed_image if mixed else _make_pool_image)
 
     # this rank's slice of the R*N-row index: row i holds pool image i % POOL.  The slice is laid
@@ -212,14 +297,18 @@ def main():
     d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_lens = torch.from_numpy(lens.astype(np.int32)).to(dev)
     del d_tmpl
-    torch.cuda.synchronize()
+    sync()
 
     B = args.batch
     if mixed:  # per-image scratch grows with the pixel count (4K: ~30 MB)
         scratch = int(B * 22e6) + (1 << 30)
     else:
         scratch = int(B * 3.2e6) + (256 << 20)
-    eng = JpegEngine(dev, max_batch=B, scratch_bytes=scratch)
+    if stub:
+        eng = StubEngine()
+    else:
+        from sds_amd.engine import JpegEngine
+        eng = JpegEngine(dev, max_batch=B, scratch_bytes=scratch)
     out = torch.empty((B, 3, args.res, args.res), dtype=torch.float32 if mixed else torch.uint8, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
     # hflip flags for every row, seeded (the user HorizontalFlipTransform, p = 0.5)
@@ -236,7 +325,7 @@ def main():
 
     # correctness gate before timing: the first batch's statuses are all OK
     step()
-    torch.cuda.synchronize()
+    sync()
     n_bad = int((status != 0).sum().item())
     if n_bad:
         raise SystemExit(f"rank {rank}: {n_bad} samples failed to decode")
@@ -248,83 +337,138 @@ def main():
             dist.barrier()
 
     barrier()
-    torch.cuda.synchronize()
-    eng.set_timing(True)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
     barrier()
-    stages = eng.stage_times()  # summed over the timed steps (HIP events on the launch stream)
     n_bad = int((status != 0).sum().item())  # the last timed batch decoded completely as well
     if n_bad:
         raise SystemExit(f"rank {rank}: {n_bad} samples of the last timed batch failed to decode")
-    eng.set_timing(False)
-    elapsed = max_over_ranks(t1 - t0, device=dev)
+    my_elapsed = t1 - t0
+    elapsed = max_over_ranks(my_elapsed, device=None if stub or args.backend == "gloo" else dev)
+    per_rank = [my_elapsed]
+    if world > 1:
+        tl = [torch.zeros(1, dtype=torch.float64, device=dev if args.backend == "nccl" and not stub else "cpu")
+              for _ in range(world)]
+        dist.all_gather(tl, torch.tensor([my_elapsed], dtype=torch.float64, device=tl[0].device))
+        per_rank = [float(x.item()) for x in tl]
+        world_seen = dist.get_world_size()
+    else:
+        world_seen = 1
     imgs = B * args.steps * world
     value = imgs / elapsed
-    if args.profile_steps and rank == 0:
-        print(json.dumps({"stage_ms_per_step": {k: v / args.steps for k, v in stages.items()}}), file=sys.stderr)
+
+    # pixel check after timing: the batch holding pool image 0 at its start row, against PIL (the
+    # reference's arithmetic) -- and for configs[1] also the reference-generated golden digest
+    pixel_check = None
+    if not stub:
+        k0 = (-r0) % args.pool
+        cursor[0] = 0
+        step()
+        sync()
+        got = out[k0].cpu()
+        fl = bool(flips[k0].item()) if mixed else False
+        ref = _pil_pipeline(pool[0], args.res, flip=fl, normalize=mixed)
+        ok = int(status[k0].item()) == 0 and torch.equal(got, ref.contiguous())
+        pixel_check = {"row": r0 + k0, "pool_image": 0, "equal_to_pil": bool(ok)}
+        if not mixed:
+            from tests import goldens as G
+            meta = G.load_json("g2_synth.json")
+            if meta.get("seed") == 1234 and (meta.get("w"), meta.get("h"), meta.get("quality")) == (640, 480, 90):
+                pixel_check["golden_sha256_match"] = G.sha(got.numpy()) == meta["images"][0]["u8_256_sha256"]
+        if not ok or not pixel_check.get("golden_sha256_match", True):
+            raise SystemExit(f"rank {rank}: pixel check failed: {pixel_check}")
+
+    # roofline: every kernel timed alone in a single-lane pass (one dispatch per kernel per batch)
+    eng.set_lanes(1)
+    eng.set_timing(True)
+    for _ in range(args.roofline_steps):
+        step()
+    stages = eng.stage_times()  # summed device ms per stage over the roofline steps
+    eng.set_timing(False)
+    eng.set_lanes(4)
+    sync()
 
     mean_in = float(np.mean(t_lens))
     out_bytes = 3 * args.res * args.res * (4 if mixed else 1)
     alg_bytes_per_img = mean_in + out_bytes
-    # Each lane (B / lanes images) launches every stage once per step on its own stream; the stage
-    # times are HIP events around each lane's launches, summed over lanes and steps.  A "launch" below
-    # is one lane's dispatch of the dominant stage: B / lanes images in dom_ms / lanes on average.
-    lanes = engine_lanes(B)
     dom = max(stages, key=stages.get)
-    launch_ms = stages[dom] / (args.steps * lanes)
-    launch_bytes = B * alg_bytes_per_img / lanes
+    launch_ms = stages[dom] / args.roofline_steps
+    launch_bytes = B * alg_bytes_per_img
     achieved = launch_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    traffic = pmc_traffic(dom, B, lanes)
+    traffic = pmc_traffic(dom, B, 1)
+    if args.profile_steps and rank == 0:
+        print(json.dumps({"stage_ms_per_step_single_lane": {k: v / args.roofline_steps for k, v in stages.items()}}),
+              file=sys.stderr)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        procs = min(16, host_cores())
-        sample = pool[:256]
-        v1 = cpu_baseline(sample, 1, args.cpu_seconds / 2, args.res, mixed)
-        vp = cpu_baseline(sample, procs, args.cpu_seconds, args.res, mixed)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not stub:
+        procs = min(BOX_CPU_SHARE, host_cores())
+        folder = tempfile.mkdtemp(prefix="sdsj_cpu_")
+        try:
+            paths = []
+            for i in range(args.cpu_files):  # configs[0]: a local folder of JPEG files
+                p = os.path.join(folder, f"{i:05d}.jpg")
+                with open(p, "wb") as f:
+                    f.write(pool[i % len(pool)])
+                paths.append(p)
+            v1 = cpu_baseline(paths, 1, args.cpu_seconds / 2, args.res, mixed)
+            vp = cpu_baseline(paths, procs, args.cpu_seconds, args.res, mixed)
+        finally:
+            shutil.rmtree(folder, ignore_errors=True)
         import platform
         what = (f"centre crop, BILINEAR resize {args.res}x{args.res}, to CHW tensor, hflip every other image, "
-                f"x/127.5-1) over the {len(sample)} mixed VGA..4K pool JPEGs" if mixed else
-                f"centre crop, BILINEAR resize {args.res}x{args.res}, to CHW tensor) over 256 of the same 640x480 "
-                f"q90 JPEGs")
+                f"x/127.5-1) over a folder of {args.cpu_files} files of the {len(pool)} mixed VGA..4K pool JPEGs"
+                if mixed else
+                f"centre crop, BILINEAR resize {args.res}x{args.res}, to CHW tensor) over a folder of "
+                f"{args.cpu_files} 640x480 q90 JPEG files (configs[0] shape)")
         cpu = {"value": round(vp, 1), "unit": "images/s", "cores": procs, "kind": "reference",
                "sample": f"PIL {__import__('PIL').__version__}/libjpeg-turbo pipeline (functional.py:94-110 op order: "
-                         f"open+convert RGB, {what} from host memory, {procs} processes x {args.cpu_seconds:.0f} s "
-                         f"(single process: {v1:.1f} images/s)",
+                         f"file read, open+convert RGB, {what}, {procs} processes x {args.cpu_seconds:.0f} s "
+                         f"(single process: {v1:.1f} images/s; {procs} = this box's CPU share, "
+                         f"{host_cores()} visible)",
                "single_core_value": round(v1, 1), "host": platform.processor() or platform.machine()}
 
     if rank == 0:
         workload = (f"configs[2]: synthetic mixed VGA..4K q90 4:2:0 baseline JPEGs resident in HBM -> centre crop + "
                     f"bilinear resize {args.res}x{args.res} + hflip (p=0.5, seeded) + float32 CHW x/127.5-1"
                     if mixed else
-                    "configs[1]: synthetic 640x480 q90 4:2:0 baseline JPEGs resident in HBM -> "
+                    ("configs[3]: " if world > 1 else "configs[1]: ") +
+                    "synthetic 640x480 q90 4:2:0 baseline JPEGs resident in HBM -> "
                     f"centre crop + bilinear resize {args.res}x{args.res} uint8 CHW")
         line = {
             "metric": ("images/s device-resident JPEG decode+crop+resize@512+hflip+normalise (mixed VGA..4K)" if mixed
                        else "images/s device-resident JPEG decode+resize@256, 1/2/4/8 MI355X; %HBM roofline"),
             "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if mixed else "u8", "data": "synthetic",
             "config": {"workload": workload,
                        "rows_per_gpu": nrows, "distinct_images": args.pool, "global_batch": B * world,
-                       "mean_jpeg_bytes": round(mean_in, 1), "parallelism": f"index-sharded x{world}, no collective"},
+                       "batch_per_gpu": B, "mean_jpeg_bytes": round(mean_in, 1),
+                       "parallelism": f"index-sharded x{world}, no collective on the data path"},
+            "per_rank_images_per_s": [round(B * args.steps / t, 1) for t in per_rank],
+            "process_group": {"backend": args.backend if world > 1 else None, "world_size": world_seen},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": (traffic or {}).get("bytes_per_launch"),
                          "traffic_detail": traffic,
                          "algorithmic_bytes_per_launch": round(launch_bytes),
                          "algorithmic_bytes_per_image": round(alg_bytes_per_img, 1),
-                         "launch_ms": round(launch_ms, 4), "images_per_launch": B / lanes, "lanes": lanes,
-                         "pipeline_achieved": round(value * alg_bytes_per_img / 1e9, 2)},
-            "stage_ms_per_step": {k: round(v / args.steps, 4) for k, v in stages.items()},
+                         "launch_ms": round(launch_ms, 4), "images_per_launch": B, "lanes": 1,
+                         "timing": "HIP events on the launch stream, single-lane pass after the timed region",
+                         "limiter": "not HBM: integer VALU issue and dependent-latency of the serial Huffman decode "
+                                    "and fixed-point resample (DESIGN.md §4)",
+                         "pipeline_achieved": round(value / world * alg_bytes_per_img / 1e9, 2)},
+            "stage_ms_per_step_single_lane": {k: round(v / args.roofline_steps, 4) for k, v in stages.items()},
+            "pixel_check": pixel_check,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -142,6 +142,34 @@ int sdsj_resize_frames_device(sdsj_engine* eng, int n, const uint8_t* d_frames, 
                               int64_t frame_stride, const sdsj_op* op, const uint8_t* d_flip, void* d_out,
                               int32_t* d_status, void* hip_stream);
 
+/* Per-process counters (SURVEY.md §5 metrics; sds itself only logs through loguru, sds/__init__.py:5-17).
+ * Accumulated on the device by every batch an engine decodes, over all entry points: samples by
+ * status, encoded bytes in, output bytes out.  sdsj_engine_counters waits for the work queued so far
+ * and copies up to `cap` counters (index = SDSJ_CTR_*); `reset` != 0 zeroes them afterwards. */
+#define SDSJ_CTR_IMAGES 0      /* JPEG samples submitted */
+#define SDSJ_CTR_OK 1          /* samples (images or frames) decoded / resized */
+#define SDSJ_CTR_UNSUPPORTED 2 /* valid images this path does not decode (PNG, WebP, arithmetic, 12-bit, CMYK...) */
+#define SDSJ_CTR_CORRUPT 3     /* malformed / truncated streams */
+#define SDSJ_CTR_CAPACITY 4    /* samples that did not fit the scratch */
+#define SDSJ_CTR_OTHER 5       /* other per-sample errors (unreadable files) */
+#define SDSJ_CTR_BYTES_IN 6    /* encoded bytes of the JPEG samples */
+#define SDSJ_CTR_BYTES_OUT 7   /* output tensor bytes written (failed samples included: zeros) */
+#define SDSJ_CTR_FRAMES 8      /* raw frames resized (sdsj_resize_frames_device) */
+#define SDSJ_CTR_PROGRESSIVE 9 /* progressive JPEGs decoded */
+#define SDSJ_NUM_COUNTERS 10
+int sdsj_engine_counters(sdsj_engine* eng, uint64_t* out, int cap, int reset);
+const char* sdsj_counter_name(int k);
+
+/* Kernel lanes: a batch of >= 256 x L images runs as L contiguous lanes on L streams whose kernel
+ * sequences overlap (default 4, at most 4).  1 = one dispatch of every kernel per batch, the setting
+ * under which a kernel's launch duration is measured alone (bench.py roofline). */
+int sdsj_engine_set_lanes(sdsj_engine* eng, int lanes);
+
+/* Grows the engine's device scratch to at least `bytes` (waits for the device first).  The device-resident
+ * entry point never grows scratch by itself (it does not synchronise): its capacity is the engine's
+ * cfg->scratch_bytes, or 2 GiB at the first call; samples beyond it report SDSJ_ECAPACITY. */
+int sdsj_engine_reserve(sdsj_engine* eng, int64_t bytes);
+
 /* Stage timing: sdsj_engine_set_timing(e, 1) starts (and restarts) accumulation; every chunk launched
  * afterwards records HIP events around each kernel on the caller's stream.  sdsj_engine_stage_times
  * waits for the last recorded chunk and returns, per stage, the summed device milliseconds. */

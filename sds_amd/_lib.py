@@ -32,8 +32,10 @@ EXPORTS = [
     "sdsj_abi_version", "sdsj_probe", "sdsj_engine_create", "sdsj_engine_destroy", "sdsj_decode_resize_batch",
     "sdsj_decode_resize_batch_device", "sdsj_engine_set_timing", "sdsj_engine_stage_times", "sdsj_last_error",
     "sdsj_stage_name", "sdsj_engine_debug_buffers", "sdsj_resize_frames_device", "sdsj_submit_batch",
-    "sdsj_submit_files", "sdsj_wait_batch",
+    "sdsj_submit_files", "sdsj_wait_batch", "sdsj_engine_counters", "sdsj_counter_name", "sdsj_engine_set_lanes",
+    "sdsj_engine_reserve",
 ]
+NUM_COUNTERS = 10  # SDSJ_NUM_COUNTERS
 SLOTS = 2  # SDSJ_SLOTS: batches in flight on the asynchronous host path
 
 
@@ -103,6 +105,11 @@ def load() -> ctypes.CDLL:
         lib.sdsj_stage_name.restype = ctypes.c_char_p
         lib.sdsj_engine_debug_buffers.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp),
                                                   ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        lib.sdsj_engine_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int]
+        lib.sdsj_counter_name.argtypes = [ctypes.c_int]
+        lib.sdsj_counter_name.restype = ctypes.c_char_p
+        lib.sdsj_engine_set_lanes.argtypes = [vp, ctypes.c_int]
+        lib.sdsj_engine_reserve.argtypes = [vp, i64]
         for name in EXPORTS:
             getattr(lib, name)  # AttributeError if the library lacks a declared symbol
         if lib.sdsj_abi_version() != SDSJ_ABI_VERSION:

@@ -2,9 +2,10 @@
 // (parse kernel).  One implementation, compiled for both sides.
 //
 // The parser restates libjpeg-turbo's jdmarker.c for the subset this path decodes (SOF0/SOF1
-// 8-bit, one interleaved scan holding every component, Huffman coding, optional DRI) -- the
-// decoder Pillow calls from sds/transforms/functional.py:100.  Everything else is reported as
-// SDSJ_UNSUPPORTED (progressive, lossless, arithmetic, 12-bit, CMYK, Adobe-RGB, multi-scan).
+// 8-bit sequential with one interleaved scan holding every component, SOF2 progressive -- whose
+// scans k_prog parses --, Huffman coding, optional DRI): the decoder Pillow calls from
+// sds/transforms/functional.py:100.  Everything else is reported as SDSJ_UNSUPPORTED (non-JPEG
+// input, lossless, arithmetic, 12-bit, CMYK, Adobe-RGB, multi-scan sequential).
 #pragma once
 #include <stdint.h>
 
@@ -278,7 +279,10 @@ SDSJ_HD int parse_headers(const Reader& rd, int64_t n, ImgDesc* d, ImgTables* t,
     t->dc_spec[q].defined = 0;
     t->ac_spec[q].defined = 0;
   }
-  if (n < 4 || rd(0) != 0xFF || rd(1) != 0xD8) return SDSJ_CORRUPT;
+  // not a JPEG stream (PNG, WebP, GIF, ... every other IMAGE_EXT format PIL opens, sds/structs.py:42):
+  // outside this path, reported as unsupported; a JPEG cut inside its first marker is corrupt
+  if (n < 2 || rd(0) != 0xFF || rd(1) != 0xD8) return SDSJ_UNSUPPORTED;
+  if (n < 4) return SDSJ_CORRUPT;
   int64_t i = 2;
   bool saw_sof = false;
   for (;;) {

@@ -55,6 +55,8 @@ struct sdsj_engine {
   ImgDesc* h_fdescs = nullptr;
   int32_t* h_froutes = nullptr;
   float* d_lut = nullptr;
+  unsigned long long* d_counters = nullptr;  // SDSJ_CTR_* (k_finish)
+  int64_t host_ctr_adj[SDSJ_NUM_COUNTERS] = {};  // host-side corrections (unreadable files)
   // host-bytes path
   uint8_t* h_stage = nullptr;
   size_t h_stage_cap = 0;
@@ -221,7 +223,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s));
   mark(10);
   SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s));
-  SDSJ_HIP(e, launch_finish(n, ln.descs, op, d_out, d_status, e->d_lut, s));
+  SDSJ_HIP(e, launch_finish(n, ln.descs, op, d_out, d_status, e->d_lut, d_lengths, e->d_counters, s));
   mark(11);
   return SDSJ_OK;
 }
@@ -505,8 +507,13 @@ int sdsj_wait_batch(sdsj_engine* e, int slot, int32_t* status) {
   Slot& sl = e->slots[slot];
   SDSJ_HIP(e, hipEventSynchronize(sl.ev_done));
   sl.pending = false;
-  for (int i = 0; i < sl.n; i++)
+  for (int i = 0; i < sl.n; i++) {
     if (status) status[i] = sl.h_pre[i] != SDSJ_OK ? sl.h_pre[i] : sl.h_status[i];
+    if (sl.h_pre[i] != SDSJ_OK) {  // the device decoded an empty sample (CORRUPT): count it as unreadable
+      e->host_ctr_adj[SDSJ_CTR_CORRUPT]--;
+      e->host_ctr_adj[SDSJ_CTR_OTHER]++;
+    }
+  }
   return SDSJ_OK;
 }
 
@@ -568,6 +575,8 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   if (hipMalloc(&e->d_routes, sizeof(int32_t) * (kRouteSlots + (size_t)kNumRoutes * e->max_batch)) != hipSuccess)
     return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_lut, sizeof(float) * 256) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMalloc(&e->d_counters, sizeof(unsigned long long) * SDSJ_NUM_COUNTERS) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipMemset(e->d_counters, 0, sizeof(unsigned long long) * SDSJ_NUM_COUNTERS) != hipSuccess) return cleanup(SDSJ_EHIP);
   {
     // presets.py:161 `x.float() / 127.5 - 1.0` in float32 (IEEE division then subtraction)
     float lut[256];
@@ -609,6 +618,7 @@ int sdsj_engine_destroy(sdsj_engine* e) {
   (void)hipHostFree(e->h_fdescs);
   (void)hipHostFree(e->h_froutes);
   (void)hipFree(e->d_lut);
+  (void)hipFree(e->d_counters);
   (void)hipFree(e->d_blob);
   (void)hipFree(e->d_offsets);
   (void)hipFree(e->d_lengths);
@@ -768,7 +778,7 @@ int sdsj_resize_frames_device(sdsj_engine* e, int n, const uint8_t* d_frames, in
     SDSJ_HIP(e, launch_coeffs(m, e->descs, *op, e->scratch, s));
     SDSJ_HIP(e, launch_hpass(m, e->descs, *op, e->scratch, e->d_routes, cap, s));
     SDSJ_HIP(e, launch_vpass(m, e->descs, *op, e->scratch, flip, out, e->d_routes, cap, e->d_lut, s));
-    SDSJ_HIP(e, launch_finish(m, e->descs, *op, out, d_status + c0, e->d_lut, s));
+    SDSJ_HIP(e, launch_finish(m, e->descs, *op, out, d_status + c0, e->d_lut, nullptr, e->d_counters, s));
   }
   return SDSJ_OK;
 }
@@ -814,5 +824,39 @@ int sdsj_engine_debug_buffers(const sdsj_engine* e, void** scratch, void** descs
 }
 
 const char* sdsj_stage_name(int k) { return k >= 0 && k < kStages ? kStageNames[k] : ""; }
+
+int sdsj_engine_counters(sdsj_engine* e, uint64_t* out, int cap, int reset) {
+  if (!e || (cap > 0 && !out)) return SDSJ_EINVAL;
+  DeviceGuard g(e->device);
+  unsigned long long h[SDSJ_NUM_COUNTERS];
+  SDSJ_HIP(e, hipDeviceSynchronize());
+  SDSJ_HIP(e, hipMemcpy(h, e->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+  for (int k = 0; k < cap && k < SDSJ_NUM_COUNTERS; k++) out[k] = (uint64_t)((int64_t)h[k] + e->host_ctr_adj[k]);
+  if (reset) {
+    SDSJ_HIP(e, hipMemset(e->d_counters, 0, sizeof(h)));
+    for (auto& a : e->host_ctr_adj) a = 0;
+  }
+  return SDSJ_OK;
+}
+
+const char* sdsj_counter_name(int k) {
+  static const char* names[SDSJ_NUM_COUNTERS] = {"images",    "ok",        "unsupported", "corrupt", "capacity",
+                                                 "other",     "bytes_in",  "bytes_out",   "frames",  "progressive"};
+  return k >= 0 && k < SDSJ_NUM_COUNTERS ? names[k] : "";
+}
+
+int sdsj_engine_set_lanes(sdsj_engine* e, int lanes) {
+  if (!e || lanes < 1 || lanes > kMaxLanes) return SDSJ_EINVAL;
+  e->lanes = lanes;
+  return SDSJ_OK;
+}
+
+int sdsj_engine_reserve(sdsj_engine* e, int64_t bytes) {
+  if (!e || bytes < 0) return SDSJ_EINVAL;
+  DeviceGuard g(e->device);
+  if (bytes <= e->capacity && e->scratch) return SDSJ_OK;
+  SDSJ_HIP(e, hipDeviceSynchronize());
+  return ensure_scratch(e, bytes);
+}
 
 }  // extern "C"

@@ -34,8 +34,9 @@ hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const
 hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
                               const uint8_t* flip, void* out, const int32_t* routes, int cap, const float* lut,
                               hipStream_t s);
+// lengths: the samples' encoded sizes (null: raw frames); counters: SDSJ_CTR_* accumulators (or null)
 hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
-                         hipStream_t s);
+                         const int32_t* lengths, unsigned long long* counters, hipStream_t s);
 // host-side planning (same code as k_parse): returns the scratch bytes image `jpg` needs, or < 0
 int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status);
 // host-side planning of one raw RGB frame (width x height) for the unfused passes; returns scratch bytes

@@ -335,17 +335,33 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
 }
 
 // k_finish: publishes every sample's status and writes the zeros of failed samples and of empty
-// crops (presets.py:160-162 normalise maps them to -1.0 through the LUT, as zeros would).
+// crops (presets.py:160-162 normalise maps them to -1.0 through the LUT, as zeros would).  Also
+// accumulates the engine's per-process counters (SDSJ_CTR_*): one thread per sample, a few 64-bit
+// atomics per sample (lengths == null: the frames path).
 __global__ void __launch_bounds__(256) k_finish(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                 void* __restrict__ out, int32_t* __restrict__ status,
-                                                const float* __restrict__ lut) {
+                                                const float* __restrict__ lut, const int32_t* __restrict__ lengths,
+                                                unsigned long long* __restrict__ counters) {
   const int img = blockIdx.x;
   if (img >= n) return;
   const ImgDesc* d = &descs[img];
   const int st = d->status;
-  if (threadIdx.x == 0) status[img] = st;
-  if (st == SDSJ_OK && d->geo != kGeoZeros) return;
   const int64_t plane = (int64_t)op.out_h * op.out_w, total = plane * 3;
+  if (threadIdx.x == 0) {
+    status[img] = st;
+    if (counters) {
+      const int k = st == SDSJ_OK ? SDSJ_CTR_OK
+                    : st == SDSJ_UNSUPPORTED ? SDSJ_CTR_UNSUPPORTED
+                    : st == SDSJ_CORRUPT ? SDSJ_CTR_CORRUPT
+                    : st == SDSJ_ECAPACITY ? SDSJ_CTR_CAPACITY : SDSJ_CTR_OTHER;
+      atomicAdd(&counters[lengths ? SDSJ_CTR_IMAGES : SDSJ_CTR_FRAMES], 1ull);
+      atomicAdd(&counters[k], 1ull);
+      if (lengths) atomicAdd(&counters[SDSJ_CTR_BYTES_IN], (unsigned long long)(uint32_t)lengths[img]);
+      atomicAdd(&counters[SDSJ_CTR_BYTES_OUT], (unsigned long long)(total * (op.out_dtype == SDSJ_DTYPE_F32 ? 4 : 1)));
+      if (lengths && st == SDSJ_OK && d->progressive) atomicAdd(&counters[SDSJ_CTR_PROGRESSIVE], 1ull);
+    }
+  }
+  if (st == SDSJ_OK && d->geo != kGeoZeros) return;
   if (op.out_dtype == SDSJ_DTYPE_F32) {
     float* o = reinterpret_cast<float*>(out) + img * total;
     const float z = lut[0];
@@ -1215,8 +1231,8 @@ hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, Im
   return hipGetLastError();
 }
 hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_finish, dim3(n), dim3(256), 0, s, n, descs, op, out, status, lut);
+                         const int32_t* lengths, unsigned long long* counters, hipStream_t s) {
+  hipLaunchKernelGGL(k_finish, dim3(n), dim3(256), 0, s, n, descs, op, out, status, lut, lengths, counters);
   return hipGetLastError();
 }
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,

@@ -30,7 +30,11 @@ class ImageDecodeError(OSError):
 
 
 class UnsupportedImageError(ImageDecodeError):
-    """A valid image the MI355X path does not decode (progressive/arithmetic/12-bit JPEG, CMYK, PNG...)."""
+    """A valid image the MI355X path does not decode: a format other than JPEG (PNG, WebP, GIF, ... --
+    everything else in sds/structs.py:42 IMAGE_EXT), or an arithmetic-coded / 12-bit / lossless /
+    CMYK JPEG.  This is a documented divergence from functional.py:94-100 (PIL decodes them): the
+    sample raises this OSError, so sds's skip handler drops it (dataset.py:366-371), and the engine's
+    ``unsupported`` counter records it."""
 
 
 def raise_for_status(status: int, index: int = 0) -> None:
@@ -96,10 +100,33 @@ class JpegEngine:
         return SdsjOp(out_h, out_w, int(bool(crop_before_resize)), _lib.FILTERS[filter],
                       _lib.DTYPE_F32 if normalize else _lib.DTYPE_U8, lay)
 
-    def _alloc_out(self, n: int, op: SdsjOp) -> torch.Tensor:
+    def _out_spec(self, n: int, op: SdsjOp):
         shape = (n, 3, op.out_h, op.out_w) if op.layout == _lib.LAYOUT_CHW else (n, op.out_h, op.out_w, 3)
-        dtype = torch.float32 if op.out_dtype == _lib.DTYPE_F32 else torch.uint8
+        return shape, (torch.float32 if op.out_dtype == _lib.DTYPE_F32 else torch.uint8)
+
+    def _alloc_out(self, n: int, op: SdsjOp) -> torch.Tensor:
+        shape, dtype = self._out_spec(n, op)
         return torch.empty(shape, dtype=dtype, device=f"cuda:{self.device}")
+
+    def _on_engine(self, t: torch.Tensor) -> bool:
+        return t.device.type == "cuda" and (t.device.index if t.device.index is not None else
+                                             torch.cuda.current_device()) == self.device
+
+    def _check_out(self, out: torch.Tensor, n: int, op: SdsjOp) -> None:
+        """The native side writes n * out_h * out_w * 3 elements of the op's dtype through a raw pointer:
+        ``out`` must be exactly what _alloc_out would give (shape, dtype, contiguous, this engine's device)."""
+        shape, dtype = self._out_spec(n, op)
+        if not isinstance(out, torch.Tensor) or tuple(out.shape) != shape or out.dtype != dtype or \
+                not out.is_contiguous() or not self._on_engine(out):
+            raise ValueError(f"out must be a contiguous {dtype} tensor of shape {shape} on cuda:{self.device}, got "
+                             f"{getattr(out, 'dtype', type(out))} {tuple(getattr(out, 'shape', ()))} on "
+                             f"{getattr(out, 'device', '?')}")
+
+    def _check_dev(self, t: torch.Tensor, name: str, dtype, n: Optional[int] = None) -> None:
+        if not isinstance(t, torch.Tensor) or t.dtype != dtype or not t.is_contiguous() or not self._on_engine(t):
+            raise ValueError(f"{name} must be a contiguous {dtype} tensor on cuda:{self.device}")
+        if n is not None and t.numel() < n:
+            raise ValueError(f"{name} holds {t.numel()} elements, the batch has {n} samples")
 
     # -- host-bytes batch ------------------------------------------------------------------
     def decode_resize(self, jpgs: Sequence[bytes], resolution, *, crop_before_resize: bool = True,
@@ -114,6 +141,10 @@ class JpegEngine:
         n = len(jpgs)
         if out is None:
             out = self._alloc_out(n, op)
+        else:
+            self._check_out(out, n, op)
+        if flip is not None and len(flip) != n:
+            raise ValueError(f"flip has {len(flip)} entries, the batch has {n} samples")
         status = (ctypes.c_int32 * max(n, 1))()
         if n == 0:
             return out, np.zeros(0, np.int32)
@@ -146,6 +177,12 @@ class JpegEngine:
             raise ValueError(f"a slot holds at most max_batch={self.max_batch} samples, got {n}")
         if out is None:
             out = self._alloc_out(n, op)
+        else:
+            self._check_out(out, n, op)
+        if flip is not None and len(flip) != n:
+            raise ValueError(f"flip has {len(flip)} entries, the batch has {n} samples")
+        if slot not in range(_lib.SLOTS):
+            raise ValueError(f"slot must be in [0, {_lib.SLOTS})")
         flip_arr = (ctypes.c_uint8 * max(n, 1))(*[1 if f else 0 for f in flip]) if flip is not None else None
         with torch.cuda.device(self.device):
             stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -196,15 +233,21 @@ class JpegEngine:
         int32 ``lengths`` per sample, both on the device).  Fully asynchronous on the current stream."""
         op = self.make_op(resolution, crop_before_resize, filter, normalize, layout)
         n = int(offsets.numel())
-        for t, dt in ((blob, torch.uint8), (offsets, torch.int64), (lengths, torch.int32)):
-            if t.device.type != "cuda" or t.dtype != dt or not t.is_contiguous():
-                raise ValueError("blob/offsets/lengths must be contiguous cuda tensors of uint8/int64/int32")
+        self._check_dev(blob, "blob", torch.uint8)
+        self._check_dev(offsets, "offsets", torch.int64)
+        self._check_dev(lengths, "lengths", torch.int32)
+        if lengths.numel() != n:
+            raise ValueError(f"offsets ({n}) and lengths ({lengths.numel()}) must have one entry per sample")
         if out is None:
             out = self._alloc_out(n, op)
+        else:
+            self._check_out(out, n, op)
         if status is None:
             status = torch.empty(n, dtype=torch.int32, device=f"cuda:{self.device}")
-        if flip is not None and (flip.dtype != torch.uint8 or flip.device.type != "cuda"):
-            raise ValueError("flip must be a cuda uint8 tensor")
+        else:
+            self._check_dev(status, "status", torch.int32, n)
+        if flip is not None:
+            self._check_dev(flip, "flip", torch.uint8, n)
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream(self.device).cuda_stream
             rc = self.lib.sdsj_decode_resize_batch_device(
@@ -226,12 +269,18 @@ class JpegEngine:
             raise ValueError("frames must be a cuda uint8 tensor [T, H, W, 3]")
         frames = frames.contiguous()
         op = self.make_op(resolution, crop_before_resize, filter, normalize, layout)
+        if not self._on_engine(frames):
+            raise ValueError(f"frames must live on cuda:{self.device}")
         t, h, w = int(frames.shape[0]), int(frames.shape[1]), int(frames.shape[2])
         if out is None:
             out = self._alloc_out(t, op)
+        else:
+            self._check_out(out, t, op)
         status = torch.empty(t, dtype=torch.int32, device=f"cuda:{self.device}")
         if flip is not None:
             flip = torch.as_tensor(flip, dtype=torch.uint8, device=f"cuda:{self.device}").contiguous()
+            if flip.numel() != t:
+                raise ValueError(f"flip has {flip.numel()} entries, there are {t} frames")
         if t == 0:
             return out, status
         with torch.cuda.device(self.device):
@@ -242,6 +291,23 @@ class JpegEngine:
                 ctypes.c_void_p(status.data_ptr()), ctypes.c_void_p(stream))
         self._check(rc, "sdsj_resize_frames_device")
         return out, status
+
+    # -- metrics / control -------------------------------------------------------------------
+    def counters(self, reset: bool = False) -> dict[str, int]:
+        """Per-process counters of everything this engine decoded: samples by status,
+        encoded bytes in, output bytes out.  Waits for the device."""
+        buf = (ctypes.c_uint64 * _lib.NUM_COUNTERS)()
+        self._check(self.lib.sdsj_engine_counters(self._h, buf, _lib.NUM_COUNTERS, int(bool(reset))),
+                    "sdsj_engine_counters")
+        return {self.lib.sdsj_counter_name(k).decode(): int(buf[k]) for k in range(_lib.NUM_COUNTERS)}
+
+    def set_lanes(self, lanes: int) -> None:
+        """Kernel lanes per batch (1..4; see include/sdsj.h)."""
+        self._check(self.lib.sdsj_engine_set_lanes(self._h, int(lanes)), "sdsj_engine_set_lanes")
+
+    def reserve(self, nbytes: int) -> None:
+        """Grows the device scratch (the device-resident entry point never grows it by itself)."""
+        self._check(self.lib.sdsj_engine_reserve(self._h, int(nbytes)), "sdsj_engine_reserve")
 
     # -- diagnostics -----------------------------------------------------------------------
     def set_timing(self, enable: bool) -> None:

@@ -66,3 +66,21 @@ def crop_box(w: int, h: int, out_h: int, out_w: int) -> tuple[int, int, int, int
     nh = int(w / tgt)
     top = (h - nh) // 2
     return 0, top, w, top + nh
+
+
+_SIGNATURES = ((b"\x89PNG\r\n\x1a\n", "PNG"), (b"GIF87a", "GIF"), (b"GIF89a", "GIF"), (b"BM", "BMP"),
+               (b"II*\x00", "TIFF"), (b"MM\x00*", "TIFF"), (b"\x00\x00\x01\x00", "ICO"), (b"8BPS", "PSD"),
+               (b"\x00\x00\x00\x0cjP  ", "JPEG 2000"), (b"\xff\x4f\xff\x51", "JPEG 2000"))
+
+
+def sniff_format(data: bytes) -> str:
+    """Names the container of an encoded image for messages and logs (no decoding)."""
+    head = bytes(data[:16])
+    if head[:2] == b"\xff\xd8":
+        return "JPEG (a mode this path does not decode: arithmetic, 12-bit, lossless, CMYK or multi-scan)"
+    if head[:4] == b"RIFF" and head[8:12] == b"WEBP":
+        return "WebP"
+    for sig, name in _SIGNATURES:
+        if head.startswith(sig):
+            return name
+    return "non-JPEG"

@@ -11,13 +11,48 @@ the process that first calls them (a DataLoader worker after fork), never pickle
 """
 from __future__ import annotations
 
+import logging
+import os
 from typing import Any, Callable, Optional, Sequence
 
 import numpy as np
 import torch
 
 from . import functional as F
-from .engine import get_engine, raise_for_status
+from .engine import UnsupportedImageError, get_engine, raise_for_status
+
+log = logging.getLogger("sds_amd")
+_unsupported_seen = {"pid": None, "n": 0}
+
+
+def _note_unsupported(data: bytes, field: str) -> str:
+    """Logs (first time per process, then every 1,000th) a sample this path does not decode; returns
+    the format name for the error message (the drop is a documented divergence: DESIGN.md §7)."""
+    fmt = F.sniff_format(data)
+    if _unsupported_seen["pid"] != os.getpid():
+        _unsupported_seen.update(pid=os.getpid(), n=0)
+    _unsupported_seen["n"] += 1
+    n = _unsupported_seen["n"]
+    if n == 1 or n % 1000 == 0:
+        log.warning("sds_amd: field %r holds a %s image, which the MI355X path does not decode (sample skipped as "
+                    "by sds's transform-error handler; %d such samples in this process so far)", field, fmt, n)
+    return fmt
+
+
+def _engine_in_worker(device):
+    """get_engine with a clear error for the one DataLoader set-up that cannot work: a worker forked
+    after the parent process initialised HIP (the child cannot re-initialise it)."""
+    try:
+        return get_engine(device)
+    except RuntimeError as e:
+        if "forked subprocess" not in str(e):
+            raise
+        raise RuntimeError(
+            "GpuDecodeResizeImageTransform runs in a DataLoader worker that was forked after the parent "
+            "process initialised the GPU, and HIP cannot be re-initialised in a forked child. Create the "
+            "DataLoader before any GPU call in the parent, pass multiprocessing_context='spawn', or keep the "
+            "workers on bytes and decode each collated batch in the main process with "
+            "sds_amd.batched.GpuDecodeBatch (INTEGRATION.md §1).") from e
 
 SampleData = dict  # sds/structs.py:68
 SampleTransform = Callable[[SampleData], Any]  # sds/structs.py:69
@@ -96,11 +131,19 @@ class GpuDecodeResizeImageTransform(BaseTransform):
     crop_before_resize, allow_vertical, random_resize (np global RNG, same calls), interpolation_mode.
     ``hflip_prob`` (extension, default 0) fuses README.md:99-108's HorizontalFlipTransform: the coin is
     ``torch.rand(1) < hflip_prob`` from the global torch RNG, as that transform draws it.
+
+    ``output_device`` (extension): None = the tensor stays on the decoding GPU; ``"cpu"`` = it is
+    copied back to host memory -- the reference's own output type -- for DataLoaders with
+    ``pin_memory=True`` (examples/iter_image_dataset.py:72-80), whose pin step rejects device
+    tensors.  Inside forked DataLoader workers the engine is created per worker; device tensors
+    reach the parent through HIP IPC.
     """
 
     def __init__(self, input_field: str, output_field: Optional[str] = None, resolution=(256, 256),
-                 normalize: bool = False, device=None, hflip_prob: float = 0.0, **resize_kwargs):
+                 normalize: bool = False, device=None, hflip_prob: float = 0.0, output_device=None,
+                 **resize_kwargs):
         super().__init__(input_field, output_field)
+        self.output_device = None if output_device is None else torch.device(output_device)
         self.resolution = tuple(int(v) for v in resolution)
         assert len(self.resolution) == 2, f"Wrong resolution: {resolution}"
         self.normalize = bool(normalize)
@@ -127,12 +170,20 @@ class GpuDecodeResizeImageTransform(BaseTransform):
         flip = None
         if self.hflip_prob > 0.0:
             flip = [bool(torch.rand(1) < self.hflip_prob)]
-        eng = get_engine(self.device)
+        eng = _engine_in_worker(self.device)
         out, status = eng.decode_resize([data], resolution, crop_before_resize=kw.get("crop_before_resize", True),
                                         filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),
                                         normalize=self.normalize, flip=flip, layout="hwc")
-        raise_for_status(int(status[0]))
-        sample[self.output_field] = out[0].permute(2, 0, 1)  # [3, h, w] view of HWC storage
+        try:
+            raise_for_status(int(status[0]))
+        except UnsupportedImageError as e:
+            fmt = _note_unsupported(data, self.input_field)
+            raise UnsupportedImageError(e.status, 0, f"field {self.input_field!r}: {fmt} input is not decoded by the "
+                                                     f"MI355X JPEG path (documented divergence, DESIGN.md §7)") from None
+        img = out[0]
+        if self.output_device is not None and self.output_device != img.device:
+            img = img.to(self.output_device)
+        sample[self.output_field] = img.permute(2, 0, 1)  # [3, h, w] view of HWC storage
         return sample
 
 
@@ -290,12 +341,14 @@ def create_standard_image_pipeline(
     *,
     device=None,
     hflip_prob: float = 0.0,
+    output_device=None,
 ) -> Sequence[SampleTransform]:
     """presets.py:716-744 with the decode/resize/to-tensor/normalise chain fused on the GPU."""
     transforms: list = [
         LoadFromDiskTransform([image_field]),
         GpuDecodeResizeImageTransform(input_field=image_field, output_field=output_field, resolution=resolution,
-                                      normalize=normalize, device=device, hflip_prob=hflip_prob, **resize_kwargs),
+                                      normalize=normalize, device=device, hflip_prob=hflip_prob,
+                                      output_device=output_device, **resize_kwargs),
     ]
     if return_image_as_single_frame_video:
         transforms.extend([

@@ -61,6 +61,9 @@ def test_host_probe_matches_oracle(case, jpg, arrs):
 
 
 def test_probe_rejects_garbage():
+    """Input that is not a JPEG stream (no SOI) is another format PIL would open (sds/structs.py:42
+    IMAGE_EXT): unsupported by this path.  A JPEG cut inside its first marker is corrupt."""
     from sds_amd import _lib
-    assert _lib.probe(b"")[0] == _lib.CORRUPT
-    assert _lib.probe(b"\x89PNG\r\n\x1a\n" + b"\0" * 64)[0] == _lib.CORRUPT
+    assert _lib.probe(b"")[0] == _lib.UNSUPPORTED
+    assert _lib.probe(b"\x89PNG\r\n\x1a\n" + b"\0" * 64)[0] == _lib.UNSUPPORTED
+    assert _lib.probe(b"\xff\xd8\xff")[0] == _lib.CORRUPT

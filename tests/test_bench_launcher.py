@@ -1,0 +1,39 @@
+"""bench.py's multi-rank launcher (configs[3] shape) on CPU: ``--gpus 2`` outside torchrun starts two
+fresh rank processes that join a gloo process group, each owning its compute_index_slice rows, and
+rank 0 prints one line with the aggregate rate and both per-rank rates.  The engine is the CPU
+stand-in (``--engine stub``); the HIP path of the same script runs on the GPU box."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(gpus):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--engine", "stub", "--backend",
+           "gloo", "--rows", "64", "--pool", "4", "--batch", "16", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--roofline-steps", "1"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    return json.loads(lines[0])
+
+
+def test_two_rank_launch_reports_the_whole_job():
+    line = _run(2)
+    assert line["n_gpus"] == 2
+    assert line["process_group"] == {"backend": "gloo", "world_size": 2}
+    assert len(line["per_rank_images_per_s"]) == 2
+    assert line["config"]["global_batch"] == 32 and line["config"]["rows_per_gpu"] == 64
+    # value = all ranks' images over the slowest rank's time
+    slowest = min(line["per_rank_images_per_s"])
+    assert abs(line["value"] - 2 * slowest) <= 0.01 * line["value"] + 1
+
+
+def test_one_gpu_run_is_unchanged():
+    line = _run(1)
+    assert line["n_gpus"] == 1 and line["process_group"]["world_size"] == 1
+    assert len(line["per_rank_images_per_s"]) == 1

@@ -1,0 +1,169 @@
+"""The per-sample drop-in (sds_amd.presets.create_standard_image_pipeline(..., device="cuda")) on the GPU:
+the transform list the reference's factory returns (presets.py:716-744), run sample by sample as
+sds/dataset.py:535-561 runs it, against the reference-generated goldens (G2, G3, G4) -- including
+crop_before_resize=False and normalize with the single-frame-video branch -- and inside torch
+DataLoader workers (examples/iter_image_dataset.py:72-80 shape, each case in a fresh process)."""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from tests import goldens as G  # noqa: E402
+from tests.test_routing import _describe  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _write(tmp, name, data):
+    p = os.path.join(tmp, name)
+    with open(p, "wb") as f:
+        f.write(data)
+    return p
+
+
+def _run(transforms, sample):
+    for t in transforms:
+        sample = t(sample)
+    return sample
+
+
+def test_pipeline_on_g2_matches_reference_goldens():
+    from sds_amd.presets import create_standard_image_pipeline
+    meta, jpgs = G.g2_jpegs()
+    tmp = tempfile.mkdtemp()
+    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda")
+    tn = create_standard_image_pipeline("jpg", (256, 256), normalize=True, device="cuda")
+    for i, j in enumerate(jpgs):
+        p = _write(tmp, f"{i}.jpg", j)
+        s = _run(ts, {"index": i, "jpg": p})
+        img = s["image"]
+        assert img.device.type == "cuda" and img.dtype == torch.uint8 and tuple(img.shape) == (3, 256, 256)
+        assert img.stride() == (1, 768, 3)  # the reference's HWC storage viewed as CHW (functional.py:104-108)
+        assert s["jpg"] == j  # LoadFromDiskTransform leaves the encoded bytes in the image field
+        assert G.sha(img.cpu().contiguous().numpy()) == meta["images"][i]["u8_256_sha256"]
+        f = _run(tn, {"index": i, "jpg": p})["image"]
+        assert f.dtype == torch.float32
+        assert G.sha(f.cpu().contiguous().numpy()) == meta["images"][i]["f32_256_sha256"]
+
+
+def test_pipeline_on_g3_mixed_sizes_with_flip_and_normalize():
+    from sds_amd.presets import create_standard_image_pipeline
+    meta, jpgs = G.g3_jpegs()
+    tmp = tempfile.mkdtemp()
+    for i, (im, j) in enumerate(zip(meta["images"], jpgs)):
+        p = _write(tmp, f"{i}.jpg", j)
+        hp = 1.0 if im["flip"] else 0.0  # torch.rand(1) < 1.0 always flips, < 0.0 never
+        u8 = _run(create_standard_image_pipeline("jpg", (512, 512), device="cuda", hflip_prob=hp), {"jpg": p})
+        f32 = _run(create_standard_image_pipeline("jpg", (512, 512), normalize=True, device="cuda", hflip_prob=hp),
+                   {"jpg": p})
+        assert G.sha(u8["image"].cpu().contiguous().numpy()) == im["u8_512_sha256"], im
+        assert G.sha(f32["image"].cpu().contiguous().numpy()) == im["f32_512_sha256"], im
+
+
+@pytest.mark.parametrize("branch", list(G.load_json("g4_routing.json")["branches"]))
+def test_routing_branches_on_gpu(branch):
+    """G4 with the real GPU engine: key order/values, the tensor's bytes (rect_no_crop is
+    crop_before_resize=False; video_normalize_custom_fields is normalize + single-frame video)."""
+    from sds_amd.presets import EnsureFieldsTransform, create_standard_image_pipeline
+    meta, jpgs = G.g2_jpegs()
+    p = _write(tempfile.mkdtemp(), "0.jpg", jpgs[0])
+    entry = G.load_json("g4_routing.json")["branches"][branch]
+    kw = dict(entry["kwargs"])
+    kw["resolution"] = tuple(kw["resolution"])
+    sample = {"index": 7, "jpg": p, "caption": "a cat", "__sample_key__": 7, "__data_type__": "IMAGE"}
+    sample = _run(create_standard_image_pipeline(device="cuda", **kw), sample)
+    tkey = [k for k, v in sample.items() if isinstance(v, torch.Tensor)][0]
+    assert sample[tkey].device.type == "cuda"
+    cpu = {k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in sample.items()}
+    assert _describe(cpu) == entry["keys"]
+    assert G.sha(cpu[tkey].contiguous().numpy()) == entry["tensor_sha256"]
+    ens = EnsureFieldsTransform(fields_whitelist=["index", tkey], drop_others=True, check_dummy_values=True)
+    out = ens(dict(sample))  # the dummy check runs torch.isnan on the device tensor
+    assert _describe({k: (v.cpu() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}) == \
+        entry["after_ensure_drop_others"]
+
+
+def test_output_device_cpu_returns_the_reference_type():
+    from sds_amd.presets import create_standard_image_pipeline
+    meta, jpgs = G.g2_jpegs()
+    p = _write(tempfile.mkdtemp(), "0.jpg", jpgs[0])
+    s = _run(create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device="cpu"), {"jpg": p})
+    assert s["image"].device.type == "cpu" and s["image"].stride() == (1, 768, 3)
+    assert G.sha(s["image"].contiguous().numpy()) == meta["images"][0]["u8_256_sha256"]
+
+
+def test_png_sample_is_counted_and_reported_not_silently_dropped(caplog):
+    """A PNG in the image field (sds/structs.py:42 IMAGE_EXT lists it): the MI355X path does not decode it.
+    The transform raises UnsupportedImageError (an OSError, so sds skips the sample as it skips any
+    transform error, dataset.py:366-371), logs it, and the engine counts it."""
+    import io
+
+    from PIL import Image
+
+    from sds_amd.engine import UnsupportedImageError, get_engine
+    from sds_amd.presets import create_standard_image_pipeline
+    buf = io.BytesIO()
+    Image.fromarray(np.zeros((20, 30, 3), np.uint8)).save(buf, format="PNG")
+    p = _write(tempfile.mkdtemp(), "0.png", buf.getvalue())
+    eng = get_engine("cuda")
+    before = eng.counters()
+    with caplog.at_level("WARNING", logger="sds_amd"):
+        with pytest.raises(UnsupportedImageError, match="PNG"):
+            _run(create_standard_image_pipeline("png", (64, 64), device="cuda"), {"png": p})
+    after = eng.counters()
+    assert after["unsupported"] == before["unsupported"] + 1
+    assert after["images"] == before["images"] + 1
+    assert after["bytes_in"] == before["bytes_in"] + len(buf.getvalue())
+    assert any("PNG" in r.getMessage() for r in caplog.records)
+
+
+def _case(name):
+    env = dict(os.environ)
+    r = subprocess.run([sys.executable, "-m", "tests.loader_cases", name], capture_output=True, text=True,
+                       timeout=240, cwd=REPO, env=env)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and lines, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    return json.loads(lines[-1])
+
+
+def test_dataloader_workers_yield_device_tensors_equal_to_goldens():
+    rec = _case("workers_device")
+    assert "error" not in rec, rec
+    assert rec["device"].startswith("cuda") and rec["n"] == 8 and rec["equal_to_goldens"], rec
+
+
+def test_dataloader_pin_memory_with_cpu_output_matches_goldens():
+    rec = _case("workers_pinned_cpu_output")
+    assert "error" not in rec, rec
+    assert rec["device"] == "cpu" and rec["pinned"] and rec["equal_to_goldens"], rec
+
+
+def test_dataloader_pin_memory_rejects_device_tensors():
+    """The reference example's exact shape (pin_memory=True) with device outputs: torch's pin step
+    refuses device tensors (INTEGRATION.md §1 documents output_device='cpu' / pin_memory=False)."""
+    rec = _case("workers_pinned_device_output")
+    assert "cannot pin" in rec.get("error", ""), rec
+
+
+def test_fork_after_parent_gpu_init_fails_with_a_clear_error():
+    rec = _case("parent_touched_gpu_fork")
+    assert "GpuDecodeBatch" in rec.get("error", "") and "forked" in rec["error"], rec
+
+
+def test_spawned_workers_work_after_parent_gpu_init():
+    rec = _case("parent_touched_gpu_spawn")
+    assert "error" not in rec, rec
+    assert rec["device"].startswith("cuda") and rec["equal_to_goldens"], rec
