@@ -26,10 +26,11 @@
 using namespace sdsj;
 
 namespace {
-constexpr int kStages = 11;
+constexpr int kStages = 13;
 constexpr int kMaxLanes = 4;
-const char* kStageNames[kStages] = {"parse", "plan",  "unstuff", "entsync", "entwrite", "idct",
-                                    "color", "coeffs", "hpass",   "vpass",   "resample"};
+const char* kStageNames[kStages] = {"parse", "plan",  "unstuff", "prog",  "entspec", "entsync", "entwrite",
+                                    "idct",  "color", "coeffs",  "hpass", "vpass",   "resample"};
+constexpr int kMarkAfterSpec = 5;  // mark index at the end of the entspec stage
 }  // namespace
 
 struct sdsj_engine {
@@ -46,7 +47,7 @@ struct sdsj_engine {
   int32_t* d_routes = nullptr;  // per-variant image lists built by k_plan (sdsj_common.h Route)
   // lanes 2.. of a chunk (run_chunk): route lists and scratch totals, streams and events
   int lanes = 4;     // SDSJ_LANES (experiments)
-  int lane_mid = 3;  // lane k + 1 starts after lane k's stage lane_mid (>= 2: k_plan done; -1: its spec pass)
+  int lane_mid = 3;  // lane k + 1 starts at lane k's mark lane_mid (>= 2: k_plan done; -1: its spec pass)
   int64_t* d_totals_x = nullptr;
   int32_t* d_routes_x = nullptr;
   hipStream_t aux[kMaxLanes - 1] = {};
@@ -194,7 +195,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   }
   auto mark = [&](int k) {
     if (evs) (void)hipEventRecord((*evs)[k], s);
-    if (after_spec && e->lane_mid == k) (void)hipEventRecord(after_spec, s);
+    if (after_spec && (e->lane_mid == k || (e->lane_mid < 0 && k == kMarkAfterSpec))) (void)hipEventRecord(after_spec, s);
   };
   mark(0);
   SDSJ_HIP(e, launch_parse(n, d_blob, d_offsets, d_lengths, op, e->warm_bits, ln.descs, ln.tables, s));
@@ -207,24 +208,26 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   mark(3);
   // (after mark 3: the next lane may start while this lane's progressive images decode)
   SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s));
-  SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s,
-                             e->lane_mid < 0 ? after_spec : nullptr));
   mark(4);
-  SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
+  SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s));
   mark(5);
-  SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
+  SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
   mark(6);
-  SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s));
+  SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
   mark(7);
-  SDSJ_HIP(e, launch_coeffs(n, ln.descs, op, e->scratch, s));
+  SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
   mark(8);
-  SDSJ_HIP(e, launch_hpass(n, ln.descs, op, e->scratch, ln.routes, cap, s));
+  SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s));
   mark(9);
-  SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s));
+  SDSJ_HIP(e, launch_coeffs(n, ln.descs, op, e->scratch, s));
   mark(10);
+  SDSJ_HIP(e, launch_hpass(n, ln.descs, op, e->scratch, ln.routes, cap, s));
+  mark(11);
+  SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s));
+  mark(12);
   SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s));
   SDSJ_HIP(e, launch_finish(n, ln.descs, op, d_out, d_status, e->d_lut, d_lengths, e->d_counters, s));
-  mark(11);
+  mark(13);
   return SDSJ_OK;
 }
 

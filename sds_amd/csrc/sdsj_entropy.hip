@@ -1167,8 +1167,8 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ 
 
 size_t enttab_bytes() { return sizeof(EntTables); }
 
-hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s, hipEvent_t after_spec) {
+hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
+                          int cap, hipStream_t s) {
   const int g = n;  // one workgroup per image on the main route
   EntTables* tables = static_cast<EntTables*>(etab);
   hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
@@ -1177,7 +1177,13 @@ hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* e
   hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 2>), dim3(gm, kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables, scratch,
                      routes, cap);
   hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  if (after_spec) (void)hipEventRecord(after_spec, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, int32_t* routes, int cap, hipStream_t s) {
+  const int g = n;
+  EntTables* tables = static_cast<EntTables*>(etab);
+  const int gs = g < 256 ? g : 256;
   hipLaunchKernelGGL((k_entsync<11, kRtEnt11, 0, kSyncThreads>), dim3(g), dim3(kSyncThreads), 0, s, descs, tables, scratch,
                      routes, cap);
   hipLaunchKernelGGL((k_entsync<11, kRtEnt11M, 1, kEntThreads>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch,

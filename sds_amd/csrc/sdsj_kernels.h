@@ -18,8 +18,11 @@ hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, Im
 hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* blob, const int64_t* offsets,
                        const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s);
 size_t enttab_bytes();  // per-image decode tables (k_enttab) held in HBM between the entropy kernels
-hipError_t launch_entsync(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s, hipEvent_t after_spec);  // recorded between the two passes
+// k_enttab (decode tables) + k_entspec (subsequence layout, warm-up, speculative decode)
+hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
+                          int cap, hipStream_t s);
+// k_entsync (sync rounds + segmented scan)
+hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, int32_t* routes, int cap, hipStream_t s);
 hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
                            hipStream_t s);
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);

@@ -49,10 +49,13 @@ def _engine_in_worker(device):
             raise
         raise RuntimeError(
             "GpuDecodeResizeImageTransform runs in a DataLoader worker that was forked after the parent "
-            "process initialised the GPU, and HIP cannot be re-initialised in a forked child. Create the "
-            "DataLoader before any GPU call in the parent, pass multiprocessing_context='spawn', or keep the "
-            "workers on bytes and decode each collated batch in the main process with "
-            "sds_amd.batched.GpuDecodeBatch (INTEGRATION.md §1).") from e
+            "process initialised the GPU (any GPU call, and DataLoader(pin_memory=True) itself, which queries "
+            "the GPU before forking its workers), and HIP cannot be re-initialised in a forked child. Pass "
+            "multiprocessing_context='spawn' to the DataLoader (with pin_memory=True also output_device='cpu'), "
+            "use pin_memory=False, persistent_workers=True and no GPU call in the parent before the workers "
+            "start (device tensors received from the workers initialise HIP in the parent), or keep the workers on "
+            "bytes and decode each collated batch in the main process with sds_amd.batched.GpuDecodeBatch "
+            "(INTEGRATION.md §1).") from e
 
 SampleData = dict  # sds/structs.py:68
 SampleTransform = Callable[[SampleData], Any]  # sds/structs.py:69

@@ -44,13 +44,21 @@ def run(case: str) -> dict:
             f.write(j)
         paths.append(p)
     kw, dl_kw = {}, {"num_workers": 2, "pin_memory": False}
+    epochs = 1
     if case == "workers_device":
         pass
-    elif case == "workers_pinned_cpu_output":
+    elif case == "workers_device_persistent_two_epochs":
+        dl_kw["persistent_workers"] = True
+        epochs = 2
+    elif case == "workers_device_two_epochs":  # new workers each epoch, forked from a parent that now holds HIP
+        epochs = 2
+    elif case == "workers_pinned_fork":  # the reference example's exact shape
+        dl_kw["pin_memory"] = True
+    elif case == "workers_pinned_spawn_cpu_output":
         kw["output_device"] = "cpu"
-        dl_kw["pin_memory"] = True
-    elif case == "workers_pinned_device_output":
-        dl_kw["pin_memory"] = True
+        dl_kw.update(pin_memory=True, multiprocessing_context="spawn")
+    elif case == "workers_pinned_spawn_device_output":
+        dl_kw.update(pin_memory=True, multiprocessing_context="spawn")
     elif case in ("parent_touched_gpu_fork", "parent_touched_gpu_spawn"):
         torch.zeros(1, device="cuda")  # the parent initialises HIP before the workers start
         if case.endswith("spawn"):
@@ -62,13 +70,14 @@ def run(case: str) -> dict:
         dl = DataLoader(FolderDataset(paths, create_standard_image_pipeline("jpg", (256, 256), device="cuda", **kw)),
                         batch_size=4, **dl_kw)
         got = {}
-        for b in dl:
+        for b in (b for _ in range(epochs) for b in dl):
             rec["device"] = str(b["image"].device)
             rec["pinned"] = bool(b["image"].is_pinned()) if b["image"].device.type == "cpu" else None
             rec["stride"] = list(b["image"].stride())
             for i, im in zip(b["index"].tolist(), b["image"]):
                 got[i] = G.sha(im.cpu().contiguous().numpy())
         rec["n"] = len(got)
+        rec["epochs"] = epochs
         rec["equal_to_goldens"] = len(got) == len(jpgs) and all(
             got[i] == meta["images"][i]["u8_256_sha256"] for i in range(len(jpgs)))
     except Exception as e:  # noqa: BLE001  (the test inspects the error)

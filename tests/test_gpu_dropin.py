@@ -145,16 +145,37 @@ def test_dataloader_workers_yield_device_tensors_equal_to_goldens():
     assert rec["device"].startswith("cuda") and rec["n"] == 8 and rec["equal_to_goldens"], rec
 
 
-def test_dataloader_pin_memory_with_cpu_output_matches_goldens():
-    rec = _case("workers_pinned_cpu_output")
+def test_dataloader_persistent_workers_serve_every_epoch():
+    rec = _case("workers_device_persistent_two_epochs")
+    assert "error" not in rec, rec
+    assert rec["epochs"] == 2 and rec["equal_to_goldens"], rec
+
+
+def test_dataloader_refork_after_device_tensors_fails_with_a_clear_error():
+    """Non-persistent workers are forked again for epoch 2, from a parent that has received device
+    tensors (HIP initialised): the transform's error names the working set-ups."""
+    rec = _case("workers_device_two_epochs")
+    assert "persistent" in rec.get("error", "") or "GpuDecodeBatch" in rec.get("error", ""), rec
+
+
+def test_dataloader_reference_shape_fails_with_a_clear_error():
+    """examples/iter_image_dataset.py:72-80 exactly (fork, num_workers=2, pin_memory=True): the
+    DataLoader queries the GPU in the parent before forking (pin_memory needs it), so a worker cannot
+    initialise HIP; the transform says so and names the working set-ups."""
+    rec = _case("workers_pinned_fork")
+    assert "GpuDecodeBatch" in rec.get("error", "") and "pin_memory=True" in rec["error"], rec
+
+
+def test_dataloader_spawn_pin_memory_with_cpu_output_matches_goldens():
+    rec = _case("workers_pinned_spawn_cpu_output")
     assert "error" not in rec, rec
     assert rec["device"] == "cpu" and rec["pinned"] and rec["equal_to_goldens"], rec
 
 
 def test_dataloader_pin_memory_rejects_device_tensors():
-    """The reference example's exact shape (pin_memory=True) with device outputs: torch's pin step
-    refuses device tensors (INTEGRATION.md §1 documents output_device='cpu' / pin_memory=False)."""
-    rec = _case("workers_pinned_device_output")
+    """pin_memory=True with device outputs (spawned workers): torch's pin step refuses device
+    tensors (output_device='cpu', or pin_memory=False)."""
+    rec = _case("workers_pinned_spawn_device_output")
     assert "cannot pin" in rec.get("error", ""), rec
 
 

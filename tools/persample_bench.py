@@ -20,12 +20,21 @@ import torch  # noqa: E402
 from torch.utils.data import DataLoader  # noqa: E402
 
 
-def main():
-    n_files = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    seconds = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
+MODES = {
+    # name: (num_workers, pin_memory, multiprocessing_context, output_device)
+    "dataloader_fork_workers2_device_out": (2, False, None, None),
+    "dataloader_fork_workers4_device_out": (4, False, None, None),
+    "dataloader_fork_workers8_device_out": (8, False, None, None),
+    "dataloader_spawn_workers4_pinned_cpu_out": (4, True, "spawn", "cpu"),
+    "main_process_per_sample": (0, False, None, None),
+}
+
+
+def run_mode(mode, n_files, seconds):
     from sds_amd.presets import create_standard_image_pipeline
     from tests.golden.synth import synth_jpegs
     from tests.loader_cases import FolderDataset
+    nw, pin, ctx, odev = MODES[mode]
     jpgs = synth_jpegs(64, seed=2024)
     d = tempfile.mkdtemp()
     paths = []
@@ -34,34 +43,43 @@ def main():
         with open(p, "wb") as f:
             f.write(jpgs[i % len(jpgs)])
         paths.append(p)
+    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device=odev)
+    ds = FolderDataset(paths, ts)
+    if nw:
+        # persistent workers: forked once, before the parent receives its first device tensor
+        src = DataLoader(ds, batch_size=4, num_workers=nw, pin_memory=pin, multiprocessing_context=ctx,
+                         persistent_workers=True)
+    else:
+        src = ds
+    n, t0, first = 0, time.perf_counter(), None
+    while time.perf_counter() - t0 < seconds:
+        for b in src:
+            x = b["image"]
+            if first is None:
+                first = (str(x.device), list(x.shape))
+                n, t0 = 0, time.perf_counter()  # worker start-up and HIP initialisation excluded
+                continue
+            n += x.shape[0] if x.dim() == 4 else 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"mode": mode, "images_per_s": round(n / dt, 1), "images": n, "seconds": round(dt, 2),
+                      "num_workers": nw, "pin_memory": pin, "context": ctx or "fork", "output_device": odev or "cuda",
+                      "first_batch": first}), flush=True)
 
-    def rate(loader_fn, label, **info):
-        n, t0 = 0, time.perf_counter()
-        first = None
-        while time.perf_counter() - t0 < seconds:
-            for b in loader_fn():
-                x = b["image"]
-                if first is None:
-                    first = (str(x.device), list(x.shape))
-                n += x.shape[0] if x.dim() == 4 else 1
-                if time.perf_counter() - t0 >= seconds:
-                    break
-        if torch.cuda.is_initialized():
-            torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        print(json.dumps({"mode": label, "images_per_s": round(n / dt, 1), "images": n, "seconds": round(dt, 2),
-                          "first_batch": first, **info}), flush=True)
 
-    # DataLoader workers first (the parent has not touched the GPU yet), then the main process
-    for nw in (2, 4, 8):
-        ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda")
-        rate(lambda: DataLoader(FolderDataset(paths, ts), batch_size=4, num_workers=nw, pin_memory=False),
-             f"dataloader_workers{nw}_device_out", num_workers=nw, pin_memory=False)
-    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device="cpu")
-    rate(lambda: DataLoader(FolderDataset(paths, ts), batch_size=4, num_workers=2, pin_memory=True),
-         "dataloader_workers2_pinned_cpu_out", num_workers=2, pin_memory=True)
-    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda")
-    rate(lambda: FolderDataset(paths, ts), "main_process_per_sample", num_workers=0)
+def main():
+    n_files = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    seconds = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
+    if len(sys.argv) > 3:
+        run_mode(sys.argv[3], n_files, seconds)
+        return
+    import subprocess
+    for mode in MODES:  # each mode in a fresh process (a forked worker needs a parent that never touched HIP)
+        subprocess.run([sys.executable, os.path.abspath(__file__), str(n_files), str(seconds), mode], check=True,
+                       timeout=300)
 
 
 if __name__ == "__main__":
