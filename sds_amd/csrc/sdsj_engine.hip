@@ -39,6 +39,7 @@ struct sdsj_engine {
   int64_t capacity = 0;
   bool grow = true;
   int warm_bits = -1;  // entropy warm-up override (SDSJ_WARM_BITS, experiments); < 0 = plan default
+  int skip = 0;        // SDSJ_SKIP_STAGES (timing experiments only: bit k skips mark-k's stage; outputs invalid)
   uint8_t* scratch = nullptr;
   ImgDesc* descs = nullptr;
   ImgTables* tables = nullptr;
@@ -209,13 +210,13 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   // (after mark 3: the next lane may start while this lane's progressive images decode)
   SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s));
   mark(4);
-  SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s));
+  if (!(e->skip >> 4 & 1)) SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s));
   mark(5);
-  SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
+  if (!(e->skip >> 5 & 1)) SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
   mark(6);
-  SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
+  if (!(e->skip >> 6 & 1)) SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
   mark(7);
-  SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
+  if (!(e->skip >> 7 & 1)) SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
   mark(8);
   SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s));
   mark(9);
@@ -225,7 +226,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   mark(11);
   SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s));
   mark(12);
-  SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s));
+  if (!(e->skip >> 12 & 1)) SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s));
   SDSJ_HIP(e, launch_finish(n, ln.descs, op, d_out, d_status, e->d_lut, d_lengths, e->d_counters, s));
   mark(13);
   return SDSJ_OK;
@@ -557,6 +558,7 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   if (!e) return SDSJ_ENOMEM;
   e->device = hip_device;
   if (const char* w = getenv("SDSJ_WARM_BITS")) e->warm_bits = atoi(w);
+  if (const char* w = getenv("SDSJ_SKIP_STAGES")) e->skip = atoi(w);
   if (cfg && cfg->max_batch > 0) e->max_batch = cfg->max_batch;
   DeviceGuard g(hip_device);
   int st = SDSJ_OK;
