@@ -223,16 +223,23 @@ SDSJ_HD inline SegView seg_view(uint8_t* base, int nseg) {
 // [counts (kRouteSlots)][kNumRoutes lists of cap entries].
 enum Route : int32_t {
   kRtUnfused = 0,  // k_color -> k_hpass -> k_vpass
-  kRtGeneric,      // k_resample
+  kRtGen0,         // k_resample<0>: any horizontal tap count (coefficients from the table)
+  kRtGen1,         // k_resample<1>: no horizontal pass
+  kRtGen3, kRtGen5, kRtGen7, kRtGen9, kRtGen11,  // k_resample<KT>
   kRt3, kRt5, kRt7, kRt9, kRt11,  // k_rs420<KT>
   kRtEnt10, kRtEnt11,             // entropy kernels by lookahead width
   kRtEnt11M,                      // LB = 11 images decoded by several workgroups (ent_groups > 1)
   kRtProg,                        // progressive images (k_prog)
   kNumRoutes
 };
-constexpr int kRouteSlots = 16;  // counts [0, kNumRoutes), the rest zero
+constexpr int kRouteSlots = 32;  // counts [0, kNumRoutes), the rest zero
+static_assert(kNumRoutes <= kRouteSlots, "route counts must fit the count slots");
 SDSJ_HD inline const int32_t* route_list(const int32_t* routes, int cap, int r) { return routes + kRouteSlots + r * cap; }
 SDSJ_HD inline int rs_route(int kt) { return kRt3 + (kt - 3) / 2; }
+// generic fused resample route of an image whose horizontal pass has kt taps (1: none)
+SDSJ_HD inline int gen_route(int kt) {
+  return kt == 1 ? kRtGen1 : (kt >= 3 && kt <= 11 && (kt & 1) ? kRtGen3 + (kt - 3) / 2 : kRtGen0);
+}
 
 SDSJ_HD inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 SDSJ_HD inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }

@@ -319,7 +319,8 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         int32_t* lst = routes + kRouteSlots + re * cap;
         lst[atomicAdd(&rcnt[re], 1)] = i;
         if (d.geo != kGeoZeros) {
-          const int rr = !d.fused ? kRtUnfused : (d.rs_fast ? rs_route(d.rs_fast) : kRtGeneric);
+          const int rr = !d.fused ? kRtUnfused
+                         : (d.rs_fast ? rs_route(d.rs_fast) : gen_route(d.need_h ? d.ksh : 1));
           lst = routes + kRouteSlots + rr * cap;
           lst[atomicAdd(&rcnt[rr], 1)] = i;
         }

@@ -340,12 +340,13 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
 }
 
 // One image's share (output rows of strip blockIdx.y, column tiles from blockIdx.z) of the generic
-// fused colour + resample (route kRtGeneric; status and zero outputs: k_finish).
+// fused colour + resample (route gen_route(KT); status and zero outputs: k_finish).  One
+// instantiation per horizontal tap count keeps each kernel's registers to what that count needs.
+template <int KT>
 __device__ void resample_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
                                const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
                                void* __restrict__ out, const float* __restrict__ lut) {
   const ImgDesc* d = &descs[img];
-  const int t = threadIdx.x;
   RsArgs A;
   A.ow = op.out_w;
   A.oh = op.out_h;
@@ -387,28 +388,21 @@ __device__ void resample_image(int img, const ImgDesc* __restrict__ descs, const
     if (A.ncomp == 1 || (c1.rh == 1 && c1.rv == 1 && c2.rh == 1 && c2.rv == 1)) A.layout = kLayFull;
     else if (c1.rh == 2 && c1.rv == 2 && c2.rh == 2 && c2.rv == 2 && c1.dw > 2 && c2.dw == c1.dw) A.layout = kLay420;
   }
-  const int kt = A.need_h ? A.ksh : 1;
   for (int tile = blockIdx.z; tile < A.ntiles; tile += gridDim.z) {
-    switch (kt) {
-      case 1: resample_tile<1>(L, A, tile); break;
-      case 3: resample_tile<3>(L, A, tile); break;
-      case 5: resample_tile<5>(L, A, tile); break;
-      case 7: resample_tile<7>(L, A, tile); break;
-      case 9: resample_tile<9>(L, A, tile); break;
-      case 11: resample_tile<11>(L, A, tile); break;
-      default: resample_tile<0>(L, A, tile); break;
-    }
+    resample_tile<KT>(L, A, tile);
     __syncthreads();  // LDS reuse by the next tile
   }
 }
 
+template <int KT>
 __global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                          int strip_h, const uint8_t* __restrict__ scratch,
                                                          const uint8_t* __restrict__ flip, void* __restrict__ out,
                                                          const int32_t* __restrict__ routes, int cap,
                                                          const float* __restrict__ lut) {
-  if ((int)blockIdx.x >= routes[kRtGeneric]) return;  // one workgroup column per list entry
-  resample_image(route_list(routes, cap, kRtGeneric)[blockIdx.x], descs, op, strip_h, scratch, flip, out, lut);
+  constexpr int r = KT == 0 ? kRtGen0 : (KT == 1 ? kRtGen1 : kRtGen3 + (KT - 3) / 2);
+  if ((int)blockIdx.x >= routes[r]) return;  // one workgroup column per list entry
+  resample_image<KT>(route_list(routes, cap, r)[blockIdx.x], descs, op, strip_h, scratch, flip, out, lut);
 }
 
 hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
@@ -417,8 +411,14 @@ hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const
   const int strip_h = n >= 512 ? kMaxStrip : 16;
   const int tiles = (op.out_w + kRsThreads - 1) / kRsThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
-  hipLaunchKernelGGL(k_resample, dim3(n, strips, tiles), dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip,
-                     out, routes, cap, lut);
+  const dim3 grid(n, strips, tiles);
+  hipLaunchKernelGGL(k_resample<0>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_resample<1>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_resample<3>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_resample<5>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_resample<7>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_resample<9>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL(k_resample<11>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   (void)status;  // published by k_finish after every resample variant
