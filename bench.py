@@ -301,15 +301,13 @@ def main():
     sync()
 
     B = args.batch
-    if mixed:  # per-image scratch grows with the pixel count (4K: ~30 MB)
-        scratch = int(B * 22e6) + (1 << 30)
-    else:
-        scratch = int(B * 3.2e6) + (256 << 20)
     if stub:
         eng = StubEngine()
     else:
         from sds_amd.engine import JpegEngine
-        eng = JpegEngine(dev, max_batch=B, scratch_bytes=scratch)
+        # device scratch from host planning (sdsj_plan_need): a batch holds at most B of the largest
+        needs = [JpegEngine.scratch_need([p], (args.res, args.res), normalize=mixed) for p in pool]
+        eng = JpegEngine(dev, max_batch=B, scratch_bytes=B * max(needs) + (64 << 20))
     out = torch.empty((B, 3, args.res, args.res), dtype=torch.float32 if mixed else torch.uint8, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
     # hflip flags for every row, seeded (the user HorizontalFlipTransform, p = 0.5)

@@ -89,6 +89,11 @@ int sdsj_abi_version(void);
 /* Host-side header parse of one JPEG (no GPU needed). */
 int sdsj_probe(const uint8_t* jpg, size_t n, sdsj_info* out);
 
+/* Device scratch one JPEG needs for `op` (host planning, no GPU): *need = bytes (256-aligned share of
+ * the engine's scratch).  Returns the header status (SDSJ_OK, SDSJ_UNSUPPORTED, SDSJ_CORRUPT); a
+ * batch on the device-resident entry point needs the sum over its samples (sdsj_engine_reserve). */
+int sdsj_plan_need(const uint8_t* jpg, size_t n, const sdsj_op* op, int64_t* need);
+
 /* Creates an engine bound to HIP device `hip_device`.  Scratch memory is owned by the engine. */
 int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out);
 int sdsj_engine_destroy(sdsj_engine* eng);

@@ -33,7 +33,7 @@ EXPORTS = [
     "sdsj_decode_resize_batch_device", "sdsj_engine_set_timing", "sdsj_engine_stage_times", "sdsj_last_error",
     "sdsj_stage_name", "sdsj_engine_debug_buffers", "sdsj_resize_frames_device", "sdsj_submit_batch",
     "sdsj_submit_files", "sdsj_wait_batch", "sdsj_engine_counters", "sdsj_counter_name", "sdsj_engine_set_lanes",
-    "sdsj_engine_reserve",
+    "sdsj_engine_reserve", "sdsj_plan_need",
 ]
 NUM_COUNTERS = 10  # SDSJ_NUM_COUNTERS
 SLOTS = 2  # SDSJ_SLOTS: batches in flight on the asynchronous host path
@@ -110,6 +110,7 @@ def load() -> ctypes.CDLL:
         lib.sdsj_counter_name.restype = ctypes.c_char_p
         lib.sdsj_engine_set_lanes.argtypes = [vp, ctypes.c_int]
         lib.sdsj_engine_reserve.argtypes = [vp, i64]
+        lib.sdsj_plan_need.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(SdsjOp), ctypes.POINTER(i64)]
         for name in EXPORTS:
             getattr(lib, name)  # AttributeError if the library lacks a declared symbol
         if lib.sdsj_abi_version() != SDSJ_ABI_VERSION:

@@ -551,6 +551,14 @@ int sdsj_probe(const uint8_t* jpg, size_t n, sdsj_info* out) {
   return st;
 }
 
+int sdsj_plan_need(const uint8_t* jpg, size_t n, const sdsj_op* op, int64_t* need) {
+  if (!jpg || !need || !valid_op(op)) return SDSJ_EINVAL;
+  int st = SDSJ_OK;
+  const int64_t b = host_plan_need(jpg, (int64_t)n, *op, &st);
+  *need = st == SDSJ_OK ? align_up(b, 256) : 0;
+  return st;
+}
+
 int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   if (!out) return SDSJ_EINVAL;
   *out = nullptr;

@@ -305,6 +305,18 @@ class JpegEngine:
         """Kernel lanes per batch (1..4; see include/sdsj.h)."""
         self._check(self.lib.sdsj_engine_set_lanes(self._h, int(lanes)), "sdsj_engine_set_lanes")
 
+    @staticmethod
+    def scratch_need(jpgs: Sequence[bytes], resolution, *, crop_before_resize: bool = True, filter: str = "bilinear",
+                     normalize: bool = False, layout: str = "chw") -> int:
+        """Device scratch bytes a batch of these JPEGs needs (host planning, sdsj_plan_need): what
+        ``reserve`` must provide before ``decode_resize_device`` decodes them in one call."""
+        op = JpegEngine.make_op(resolution, crop_before_resize, filter, normalize, layout)
+        lib, tot, need = _lib.load(), 0, ctypes.c_int64()
+        for j in jpgs:
+            lib.sdsj_plan_need(j, len(j), ctypes.byref(op), ctypes.byref(need))
+            tot += need.value
+        return tot
+
     def reserve(self, nbytes: int) -> None:
         """Grows the device scratch (the device-resident entry point never grows it by itself)."""
         self._check(self.lib.sdsj_engine_reserve(self._h, int(nbytes)), "sdsj_engine_reserve")

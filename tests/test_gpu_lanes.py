@@ -46,7 +46,7 @@ def test_lanes_equal_one_lane_and_oracle(monkeypatch):
 
 def test_lanes_capacity_failures_in_image_order(monkeypatch):
     from tests.golden.synth import synth_jpegs
-    jpgs = synth_jpegs(48, seed=5) * 12  # 576 VGA images: ~40 fit in 64 MiB of scratch
+    jpgs = synth_jpegs(48, seed=5) * 12  # 576 VGA images: about a dozen fit in 64 MiB of scratch
     lens = [len(j) for j in jpgs]
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
     blob = torch.from_numpy(np.frombuffer(b"".join(jpgs), np.uint8).copy()).cuda()

@@ -45,7 +45,7 @@ def main() -> None:
     pool = make_pool(args.pool, min(16, os.cpu_count() or 1))
     jpgs = [pool[i % len(pool)] for i in range(args.batch)]
     dev = torch.device("cuda", 0)
-    eng = JpegEngine(dev, max_batch=args.batch, scratch_bytes=int(args.batch * 3.2e6) + (256 << 20))
+    eng = JpegEngine(dev, max_batch=args.batch, scratch_bytes=int(args.batch * 7e6) + (256 << 20))
     out = torch.empty((args.batch, 3, args.res, args.res), dtype=torch.uint8, device=dev)
     host = torch.empty(out.shape, dtype=torch.uint8, pin_memory=True)
 

@@ -21,7 +21,7 @@ def main():
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
     blob = torch.from_numpy(np.frombuffer(b"".join(jpgs), np.uint8).copy()).cuda()
     d_offs, d_lens = torch.from_numpy(offs).cuda(), torch.tensor(lens, dtype=torch.int32).cuda()
-    eng = JpegEngine(max_batch=n, scratch_bytes=int(n * 3.2e6) + (256 << 20))
+    eng = JpegEngine(max_batch=n, scratch_bytes=int(n * 7e6) + (256 << 20))
     out, st = eng.decode_resize_device(blob, d_offs, d_lens, (256, 256))
     torch.cuda.synchronize()
     assert (st == 0).all()

@@ -29,7 +29,7 @@ for k, p in enumerate(pool): blob[offs[k]:offs[k] + lens[k]] = np.frombuffer(p, 
 B = 4096
 idx = np.arange(B) %% len(pool)
 d_blob = torch.from_numpy(blob).cuda(); d_off = torch.from_numpy(offs[idx]).cuda(); d_len = torch.from_numpy(lens[idx].astype(np.int32)).cuda()
-eng = JpegEngine("cuda:0", max_batch=B, scratch_bytes=int(B * 3.2e6) + (256 << 20))
+eng = JpegEngine("cuda:0", max_batch=B, scratch_bytes=int(B * 7e6) + (256 << 20))
 out = torch.empty((B, 3, 256, 256), dtype=torch.uint8, device="cuda"); st = torch.empty(B, dtype=torch.int32, device="cuda")
 for _ in range(3): eng.decode_resize_device(d_blob, d_off, d_len, (256, 256), out=out, status=st)
 torch.cuda.synchronize(); t0 = time.perf_counter()
