@@ -147,12 +147,6 @@ struct ImgDesc {
   int32_t pad3;
   int64_t sos_pos;
   int64_t off_ptab;
-  // symbol records (baseline images): per subsequence, rec_cap int32 records of the speculative pass
-  // at off_srec and of the fix pass at off_frec (layout: SymRec below); the record-walking IDCT
-  // (k_walk) reads them instead of a dense coefficient array
-  int32_t rec_cap;
-  int32_t pad4;
-  int64_t off_srec, off_frec;
 };
 
 // Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).
@@ -172,15 +166,7 @@ struct SubState {
   int32_t nblk_ex, dc_ex[kMaxComp];
   int32_t first, seg;
   uint32_t lim_bit;  // end of the interval's data: bits at or beyond it read as zeros (jpeg_fill_bit_buffer)
-  int32_t last;      // the last subsequence of its restart interval
-  // decode-once bookkeeping (k_entspec -> k_entsync -> k_entfix -> k_walk).  The speculative pass wrote
-  // nrec_s symbol records of its blocks [0, spec_nblk); the true blocks of the subsequence are the fix
-  // pass's nblk_f blocks (nrec_f records, decoded from the verified entry), then -- unless fix_n < 0 --
-  // the speculative blocks from spec_m on, whose DC records take dc_adj on top of dc_ex.
-  int32_t nrec_s, nrec_f, nblk_f;
-  int32_t fix_n;   // true blocks the fix pass decodes: 0 none, > 0 the first fix_n, -1 all of them
-  int32_t spec_m;  // first speculative block the true decode merged into
-  int32_t dc_adj[kMaxComp];
+  int32_t pad;
 };
 
 // Table state of the progressive decoder (k_prog), one per progressive image in scratch: the
@@ -195,25 +181,6 @@ struct ProgTables {
   int32_t qt_defined[4];
   int32_t latched[kMaxComp];
 };
-
-// Symbol record (decode once): one int32 per DC symbol and per non-zero AC coefficient, in decode
-// order; EOB and ZRL symbols leave none.  Bits 0-15: the coefficient value -- for the DC symbol, the
-// running sum of the component's DC differences since the subsequence's entry (int16, wrapping as
-// libjpeg's JCOEF store does) --; bits 16-22: the zigzag index k (0 = DC = the block's first record;
-// up to 78 for corrupt runs, clamped to 63 by jpeg_natural_order's guard entries).  A block has at
-// most 64 records and every record covers at least 2 bits of entropy-coded data (a DC code + an EOB
-// code, or an AC code + its value bits), so a decode over B bits leaves at most B / 2 + 1 records.
-SDSJ_HD inline uint32_t sym_rec(int k, int v) { return (uint32_t)(uint16_t)v | ((uint32_t)k << 16); }
-constexpr int kMaxBlockBits = 64 * 32;  // one block: 64 symbols of at most 16 + 16 bits
-SDSJ_HD inline int rec_cap_for(int sub_bits) { return ((sub_bits + kMaxBlockBits) / 2 + 8 + 3) & ~3; }
-// The last subsequence of a restart interval may decode up to one MCU past the interval's data
-// (jdhuff.c insufficient_data: zero bits until the MCU ends), so its fix stream gets this many
-// more records.  Fix stream of subsequence j (interval s): records [j * rec_cap + s * extra, + rec_cap
-// (+ extra for the last one)).
-SDSJ_HD inline int fix_extra(int bpm) { return bpm * (kMaxBlockBits / 2) + 64; }
-SDSJ_HD inline int64_t fix_stream(int j, int seg, int rec_cap, int bpm) {
-  return (int64_t)j * rec_cap + (int64_t)seg * fix_extra(bpm);
-}
 
 // One block boundary met by the speculative decode (for early sync detection).
 struct SyncRec {

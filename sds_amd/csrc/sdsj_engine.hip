@@ -28,7 +28,7 @@ using namespace sdsj;
 namespace {
 constexpr int kStages = 13;
 constexpr int kMaxLanes = 4;
-const char* kStageNames[kStages] = {"parse", "plan",  "unstuff", "prog",  "entspec", "entsync", "entfix",
+const char* kStageNames[kStages] = {"parse", "plan",  "unstuff", "prog",  "entspec", "entsync", "entwrite",
                                     "idct",  "color", "coeffs",  "hpass", "vpass",   "resample"};
 constexpr int kMarkAfterSpec = 5;  // mark index at the end of the entspec stage
 }  // namespace
@@ -214,12 +214,9 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   mark(5);
   if (!(e->skip >> 5 & 1)) SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
   mark(6);
-  if (!(e->skip >> 6 & 1)) SDSJ_HIP(e, launch_entfix(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
+  if (!(e->skip >> 6 & 1)) SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
   mark(7);
-  if (!(e->skip >> 7 & 1)) {
-    SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
-    SDSJ_HIP(e, launch_walk(n, ln.descs, ln.tables, e->scratch, s));
-  }
+  if (!(e->skip >> 7 & 1)) SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
   mark(8);
   SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s));
   mark(9);
@@ -775,8 +772,6 @@ int sdsj_resize_frames_device(sdsj_engine* e, int n, const uint8_t* d_frames, in
       d.off_rec += o;
       d.off_ptab += o;
       d.off_coef += o;
-      d.off_srec += o;
-      d.off_frec += o;
       d.off_planes += o;
       d.off_tmp += o;
       d.off_kh += o;

@@ -1,31 +1,25 @@
-// sdsj_entropy.hip -- parallel Huffman decoding of baseline JPEG scans on gfx950, decoding each
-// symbol once.
+// sdsj_entropy.hip -- parallel Huffman decoding of baseline JPEG scans on gfx950.
 //
 // Restates libjpeg-turbo jdhuff.c decode_mcu (the decoder Pillow runs for
 // sds/transforms/functional.py:100) with one image per 256-thread workgroup and the entropy
 // segment split into subsequences decoded in parallel (self-synchronisation, after Weissenberger &
 // Schmidt, "Massively Parallel Huffman Decoding on GPUs"):
 //
-//   k_entspec   1. speculative pass: subsequence j warms up from a few thousand bits before its
-//                  start, takes the first block boundary at or after its start as its entry and
-//                  decodes to the first block boundary at or after its end, writing one symbol
-//                  record per DC symbol / non-zero AC coefficient (sdsj_common.h SymRec) and the
-//                  bit positions of its first kRec block boundaries (SyncRec);
-//   k_entsync   2. sync: every j whose entry differs from the exit of j-1 re-decodes from that exit
-//                  and stops at the first boundary where it meets a record of its speculative pass
-//                  (the paths have merged: the rest of the speculative result -- blocks, DC sums,
-//                  symbol records -- is exact).  It notes where: the true blocks before the merge
-//                  (fix_n), the first speculative block after it (spec_m) and the DC offset between
-//                  the two decodes (dc_adj).  Rounds repeat until every entry equals its
-//                  predecessor's exit (Jacobi fixed point);
-//               3. segmented exclusive scan of (blocks, DC differences) -> each subsequence's first
-//                  block index and DC predictors (prediction resets at RSTn);
-//   k_entfix    4. the true blocks before the merge points (and every block of the last subsequence
-//                  of each restart interval, with jdhuff.c's insufficient-data rules) are decoded
-//                  again from the verified entries into fix records.
-// The record-walking IDCT (sdsj_walk.hip) then reads the fix records and the speculative records past
-// the merge points.  Only the few unsynchronised prefixes are decoded twice; nothing dense is
-// written between the entropy decoder and the IDCT.
+//   k_entsync   1. speculative pass: subsequence j decodes from its first bit assuming (block 0,
+//                  DC) and records its block boundaries (SyncRec);
+//               2. sync: every j whose entry state differs from the exit state of j-1 re-decodes
+//                  from that state and stops at the first boundary where it meets a record of its
+//                  speculative pass (the paths have merged, the rest of that result is exact).  The
+//                  re-decodes run as work stages with a doubling symbol budget: unfinished tasks
+//                  save their state and are packed into the fewest waves for the next stage, so the
+//                  few long re-decodes do not hold every wave of the workgroup.  Rounds repeat
+//                  until every entry equals its predecessor's exit (Jacobi fixed point);
+//               3. segmented exclusive scan of (blocks completed, DC differences) -> every
+//                  subsequence's first block index and DC predictors (prediction resets at RSTn).
+//   k_entwrite  4. verified decode: each lane assembles its current 8x8 block in LDS (natural order,
+//                  jpeg_natural_order with its 16 guard entries); the wave flushes completed blocks
+//                  cooperatively as 128-byte stores.  A block belongs to the subsequence in which
+//                  its DC symbol starts (the owner decodes past its end to finish it).
 //
 // Symbol decoding: 2^LB-entry lookup of (code length, size, run) -- LB = 11 for images using at
 // most 4 Huffman tables, LB = 10 otherwise (two kernel variants, each skips the other's images)
@@ -42,6 +36,8 @@ namespace sdsj {
 
 constexpr int kEntThreads = kDecodeThreads;
 constexpr int kLutEntries = 1 << 13;  // LDS lookup capacity: 4 tables x 2^11 or 8 x 2^10
+constexpr int kStageStride = 64;      // int16 per lane staging block (one 128-byte block)
+constexpr int kBudget0 = 64;          // first sync stage's symbol budget
 constexpr int kMaxTasks = kEntThreads;  // per round (more: picked up by the next round)
 // k_entsync is latency-bound (a few serial re-decodes per image): one wave per image keeps more
 // images in flight per CU than a 4-wave workgroup would (the LDS tables bound both)
@@ -391,7 +387,7 @@ __device__ inline int block_excl_scan(int v, int* tmp, int* total) {
 }
 
 // ------------------------------------------------------------------------------------------
-// k_entspec / k_entsync
+// k_entsync
 // ------------------------------------------------------------------------------------------
 template <int NT, class TT = EntTables>
 struct LdsSyncT {
@@ -405,6 +401,10 @@ struct LdsSyncT {
     } fs;
   } u;
   int32_t nsub, rounds, stages;
+  unsigned long long sym[2];
+  unsigned long long t0, t1, t2;
+  unsigned long long it[2];
+  int32_t wmax[NT / 64];
 };
 using LdsSync = LdsSyncT<kEntThreads>;
 
@@ -412,18 +412,17 @@ using LdsSync = LdsSyncT<kEntThreads>;
 // before the segment start) assuming (block 0, DC), and take the first block boundary at or after
 // start_bit as the entry; by then the decode has almost always merged with the true path (JPEG's
 // Huffman self-synchronisation; the MCU phase takes ~1k bits to lock on).  Then decode to the first
-// block boundary at or after end_bit, recording every block boundary (the first kRec) and one symbol
-// record per DC symbol / non-zero AC coefficient.  A segment's first subsequence starts exactly at its
-// (known) state.  The last subsequence of a segment only needs its entry: k_entfix decodes its blocks.
+// block boundary at or after end_bit, recording every block boundary.  A segment's first
+// subsequence starts exactly at its (known) state.
 template <int LB>
-__device__ void spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
-                          uint32_t* srec, int rec_cap, uint32_t seg_start, uint32_t warm) {
+__device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
+                         uint32_t seg_start, uint32_t warm) {
   // (bits at or beyond S.lim_bit read as zeros)
   const uint32_t start = S.start_bit, end = S.end_bit;
   const uint32_t ws = S.first ? start : (start - seg_start > warm ? start - warm : seg_start);
   Bits b;
   bits_init(b, src, ws, S.lim_bit);
-  int blk = 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, recp = 0;
+  int blk = 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
   int d0 = 0, d1 = 0, d2 = 0;
   int c = ctx_c(K, 0), sdc = ctx_dc(K, 0), sac = ctx_ac(K, 0);
   uint32_t entry = start;
@@ -447,6 +446,7 @@ __device__ void spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* s
           b.buf <<= tot;
           b.nb -= tot;
           b.pos += tot;
+          nsym++;
           if (next_z(z, sz, r)) {
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
             sdc = ctx_dc(K, blk);
@@ -465,7 +465,7 @@ __device__ void spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* s
         break;
     }
   }
-  bool run = !S.last && (b.pos < end || z != 0);
+  bool run = b.pos < end || z != 0;
   while (__builtin_amdgcn_ballot_w64(run)) {
     if (run) bits_fill(b);
     for (;;) {
@@ -476,12 +476,7 @@ __device__ void spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* s
           int s, r, val;
           const bool isdc = z == 0;
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
-          // symbol record: the DC symbol carries its component's running DC sum since the entry
-          if (isdc || s) {
-            const int dl = (c == 0 ? d0 : (c == 1 ? d1 : d2)) + val;
-            if (recp < rec_cap) srec[recp] = sym_rec(isdc ? 0 : z + r, isdc ? dl : val);
-            recp++;
-          }
+          nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           if (next_z(z, s, r)) {
             add_dc(c, dcd, d0, d1, d2);
@@ -511,13 +506,7 @@ __device__ void spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* s
   S.spec_dc[1] = S.cur_dc[1] = d1;
   S.spec_dc[2] = S.cur_dc[2] = d2;
   S.nrec = nrec < kRec ? nrec : kRec;
-  S.nrec_s = recp;
-  // the fix pass decodes every block of the segment's last subsequence, and of one whose records
-  // did not fit (cannot happen: a record covers >= 2 bits, rec_cap_for)
-  S.fix_n = S.last || recp > rec_cap ? -1 : 0;
-  S.spec_m = 0;
-  S.dc_adj[0] = S.dc_adj[1] = S.dc_adj[2] = 0;
-  S.nrec_f = S.nblk_f = 0;
+  return nsym;
 }
 
 // Re-decode of subsequence S from its corrected entry (new_entry_*) to its end -- the first block
@@ -526,28 +515,17 @@ __device__ void spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* s
 // a lane that sits on a block boundary looks it up among the speculative pass's records (binary
 // search): the same position and MCU block means the two paths have merged, and the rest of the
 // speculative result is exact (large subsequences stop there instead of decoding to their end).
-// Also notes for k_entfix / k_walk where the true decode merged (fix_n, spec_m, dc_adj).
 constexpr uint32_t kMergeBits = 768;
 constexpr int kSyncQ = kQ;  // (a deeper queue measured slower: the pull shifts it)
 
 template <int LB, class TT>
-__device__ void sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const SyncRec* rec,
-                          int rec_cap) {
-  if (S.last) {  // only its entry matters (k_entfix decodes it); its exit feeds no other subsequence
-    S.new_exit_p = S.cur_exit_p;
-    S.new_exit_bz = S.cur_exit_bz;
-    S.new_nblk = S.cur_nblk;
-    S.new_dc[0] = S.cur_dc[0];
-    S.new_dc[1] = S.cur_dc[1];
-    S.new_dc[2] = S.cur_dc[2];
-    return;
-  }
+__device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const SyncRec* rec) {
   const uint32_t end = S.end_bit;
   const int nrec = S.nrec;
   BitsQ<kSyncQ> b;
   bits_init(b, src, S.new_entry_p, S.lim_bit);
   int blk = S.new_entry_bz >> 8, z = S.new_entry_bz & 0xFF;
-  int nblk = 0, bad = 0, d0 = 0, d1 = 0, d2 = 0, dcd = 0;
+  int nblk = 0, bad = 0, nsym = 0, d0 = 0, d1 = 0, d2 = 0, dcd = 0;
   uint32_t next_chk = nrec > 0 ? b.pos + kMergeBits : 0xFFFFFFFFu;
   bool merged = false;
   int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
@@ -561,6 +539,7 @@ __device__ void sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, Sub
           int sy, r, val;
           const bool isdc = z == 0;
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, sy, r, val, bad);
+          nsym++;
           dcd = isdc ? val : dcd;
           if (next_z(z, sy, r)) {
             add_dc(c, dcd, d0, d1, d2);
@@ -591,13 +570,6 @@ __device__ void sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, Sub
           S.new_dc[0] = d0 + S.spec_dc[0] - q0;
           S.new_dc[1] = d1 + S.spec_dc[1] - q1;
           S.new_dc[2] = d2 + S.spec_dc[2] - q2;
-          // true blocks [0, nblk) come from k_entfix, the rest from speculative block lo + 1 on
-          // (whose DC records run q behind the true sums d)
-          S.fix_n = S.nrec_s <= rec_cap ? nblk : -1;
-          S.spec_m = lo + 1;
-          S.dc_adj[0] = d0 - q0;
-          S.dc_adj[1] = d1 - q1;
-          S.dc_adj[2] = d2 - q2;
           merged = true;
           run = false;
         } else {
@@ -616,8 +588,128 @@ __device__ void sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, Sub
     S.new_dc[0] = d0;
     S.new_dc[1] = d1;
     S.new_dc[2] = d2;
-    S.fix_n = -1;  // every true block from k_entfix
   }
+  return nsym;
+}
+
+// Records of the speculative pass, kRQ at a time in registers (filled with the bit queue).
+constexpr int kRQ = 6;
+
+__device__ __forceinline__ void rec_fill(const SyncRec* rec, int ri, int nrec, uint32_t* rp, uint32_t* rx) {
+  const uint2* r2 = reinterpret_cast<const uint2*>(rec);
+#pragma unroll
+  for (int k = 0; k < kRQ; k++) {
+    const int i = ri + k;
+    const uint2 v = r2[i < kRec ? i : kRec - 1];
+    rp[k] = i < nrec ? v.x : 0xFFFFFFFFu;  // past the last record: never reached
+    rx[k] = i < nrec ? v.y : 0u;           // dc (low 16 bits) | blk << 16
+  }
+}
+
+// Resumable re-decode of S (state in S.res_*), at most `budget` symbols.  Returns true when the
+// task is finished (merged with a record, or reached the subsequence end); new_exit_* / new_nblk /
+// new_dc then hold the result.  Otherwise the state is saved for the next stage.
+template <int LB>
+__device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, const SyncRec* rec,
+                          int budget, int* nsym_out) {
+  const uint32_t end = S.end_bit;
+  const int nrec = S.nrec;
+  Bits b;
+  bits_init(b, src, S.res_p, S.lim_bit);
+  int blk = S.res_bz >> 8, z = S.res_bz & 0xFF;
+  int nblk = S.res_nblk, ri = S.res_ri;
+  int d0 = S.res_dc[0], d1 = S.res_dc[1], d2 = S.res_dc[2];
+  int q0 = S.res_q[0], q1 = S.res_q[1], q2 = S.res_q[2];  // speculative DC prefix up to record ri
+  int bad = 0, nsym = 0;
+  int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
+  uint32_t rp[kRQ], rx[kRQ];
+  int nr = 0, done_blk = 0;
+  uint32_t P = 0;
+  bool adv = false, merged = false;  // adv: records up to boundary P still to be passed
+  bool run = (b.pos < end || z != 0) && budget > 0;
+  while (__builtin_amdgcn_ballot_w64(run)) {
+    if (run) {
+      bits_fill(b);
+      rec_fill(rec, ri, nrec, rp, rx);
+      nr = kRQ;
+    }
+    for (;;) {
+      const bool dry = run && (adv ? nr == 0 : !bits_can(b));
+      if (__builtin_amdgcn_ballot_w64(dry) || !__builtin_amdgcn_ballot_w64(run)) break;
+      if (run) {
+        if (!adv) {
+          int s, r, val;
+          const bool isdc = z == 0;
+          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+          nsym++;
+          add_dc(c, isdc ? val : 0, d0, d1, d2);
+          if (next_z(z, s, r)) {
+            done_blk = blk;
+            blk = blk + 1 == K.bpm ? 0 : blk + 1;
+            c = ctx_c(K, blk);
+            sdc = ctx_dc(K, blk);
+            sac = ctx_ac(K, blk);
+            nblk++;
+            adv = true;
+            P = b.pos;
+          }
+        }
+        // pass the records at or before P; a record at P of the same MCU block = merged paths
+        while (adv && nr > 0) {
+          const uint32_t Rp = rp[0], Rx = rx[0];
+          if (Rp > P) {
+            adv = false;
+            break;
+          }
+          const int rb = (int)(Rx >> 16) & 0xFF;
+          add_dc(ctx_c(K, rb), (int)(int16_t)(Rx & 0xFFFF), q0, q1, q2);
+          ri++;
+#pragma unroll
+          for (int k = 0; k + 1 < kRQ; k++) {
+            rp[k] = rp[k + 1];
+            rx[k] = rx[k + 1];
+          }
+          nr--;
+          if (Rp == P && rb == done_blk) {
+            merged = true;
+            adv = false;
+          }
+        }
+        run = !merged && (adv || ((b.pos < end || z != 0) && nsym < budget));
+      }
+    }
+  }
+  *nsym_out = nsym;
+  if (merged) {
+    // the remainder of the speculative result is exact
+    S.new_exit_p = S.spec_exit_p;
+    S.new_exit_bz = S.spec_exit_bz;
+    S.new_nblk = nblk + S.spec_nblk - ri;
+    S.new_dc[0] = d0 + S.spec_dc[0] - q0;
+    S.new_dc[1] = d1 + S.spec_dc[1] - q1;
+    S.new_dc[2] = d2 + S.spec_dc[2] - q2;
+    return true;
+  }
+  if (b.pos >= end && z == 0) {
+    S.new_exit_p = b.pos;
+    S.new_exit_bz = (uint16_t)((blk << 8) | z);
+    S.new_nblk = nblk;
+    S.new_dc[0] = d0;
+    S.new_dc[1] = d1;
+    S.new_dc[2] = d2;
+    return true;
+  }
+  S.res_p = b.pos;
+  S.res_bz = (uint16_t)((blk << 8) | z);
+  S.res_nblk = nblk;
+  S.res_ri = ri;
+  S.res_dc[0] = d0;
+  S.res_dc[1] = d1;
+  S.res_dc[2] = d2;
+  S.res_q[0] = q0;
+  S.res_q[1] = q1;
+  S.res_q[2] = q2;
+  return false;
 }
 
 template <int LB>
@@ -629,13 +721,16 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   const int t = threadIdx.x;
   const int ns = load_tables<LB>(L.T, &tables[img]);
   if (!variant_owns<LB>(ns)) return;
+  if (t == 0) {
+    L.sym[0] = 0;
+    L.it[0] = 0;
+  }
   const BlkCtx K = make_ctx(L.T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
   SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
   SyncRec* recs = reinterpret_cast<SyncRec*>(scratch + d->off_rec);
-  uint32_t* srec = reinterpret_cast<uint32_t*>(scratch + d->off_srec);
-  const int nseg = d->nseg, rec_cap = d->rec_cap;
+  const int nseg = d->nseg;
   const uint32_t SB = (uint32_t)d->sub_bits;
 
   // --- subsequence layout: restart interval s (bytes [lo[s], hi[s])) -> max(1, ceil(bits / SB)) ---
@@ -662,7 +757,6 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
           const uint32_t e = S.start_bit + SB;
           S.end_bit = e < b1 ? e : b1;
           S.first = k == 0;
-          S.last = k == cnt - 1;
           S.seg = s;
           S.lim_bit = b1;
         }
@@ -673,13 +767,33 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   }
   __syncthreads();
   const int nsub = L.nsub;
-  // --- 1. speculative pass: this workgroup's share of the subsequences (every group computes the
-  // same layout above) ---
+  unsigned long long nsym_spec = 0;
+
+  // --- 1. speculative pass ---
+  if (t == 0) L.t0 = __builtin_amdgcn_s_memtime();
+  if ((t & 63) == 0) L.wmax[t >> 6] = 0;
+  __syncthreads();
+  // this workgroup's share of the subsequences (every group computes the same layout above)
   const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
-  for (int j = j0 + t; j < j1; j += kEntThreads)
-    spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, srec + (int64_t)j * rec_cap, rec_cap,
-                  (uint32_t)sv.lo[sub[j].seg] * 8u, (uint32_t)d->warm_bits);
+  for (int j = j0 + t; j < j1; j += kEntThreads) {
+    const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, (uint32_t)sv.lo[sub[j].seg] * 8u,
+                                (uint32_t)d->warm_bits);
+    nsym_spec += k;
+    atomicMax(&L.wmax[t >> 6], k);
+  }
+  __syncthreads();
+  if (t == 0) {
+    L.t1 = __builtin_amdgcn_s_memtime();
+    for (int w = 0; w < kEntThreads / 64; w++) L.it[0] += 64ull * L.wmax[w];
+  }
+  atomicAdd(&L.sym[0], nsym_spec);
+  __syncthreads();
   if (t == 0) d->nsub = nsub;
+  if (t == 0 && grp == 0) {  // statistics: the first group's share
+    d->sym_spec = (int64_t)L.sym[0];
+    d->t_spec = (int64_t)(L.t1 - L.t0);
+    d->it_spec = (int64_t)L.it[0];
+  }
 }
 
 template <int LB, int NT>
@@ -689,13 +803,17 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
   if (d->status != SDSJ_OK) return;
   __shared__ LdsSyncT<NT, SyncTables> L;
   const int t = threadIdx.x;
-  const int nsub = d->nsub, rec_cap = d->rec_cap;
+  const int nsub = d->nsub;
   SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
   SyncRec* recs = reinterpret_cast<SyncRec*>(scratch + d->off_rec);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
+  unsigned long long nsym_sync = 0;
   if (t == 0) {
     L.rounds = 0;
     L.stages = 0;
+    L.sym[0] = L.sym[1] = 0;
+    L.it[0] = L.it[1] = 0;
+    L.t1 = __builtin_amdgcn_s_memtime();
   }
   // any subsequence whose entry differs from its predecessor's exit?  Only then are the decode
   // tables built (most images: none after the warm-up)
@@ -728,6 +846,12 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
           SubState& S = sub[j];
           S.new_entry_p = ep;
           S.new_entry_bz = ebz;
+          S.res_p = ep;
+          S.res_bz = ebz;
+          S.res_nblk = 0;
+          S.res_ri = 0;
+          S.res_dc[0] = S.res_dc[1] = S.res_dc[2] = 0;
+          S.res_q[0] = S.res_q[1] = S.res_q[2] = 0;
         }
         ntask += tot;
       }
@@ -740,7 +864,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       }
       for (int i = t; i < ntask; i += NT) {
         const int j = L.u.task[0][i];
-        sync_full<kSyncLB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, rec_cap);
+        nsym_sync += sync_full<kSyncLB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec);
       }
       __syncthreads();
       // commit every task of the round (entries first: they were read from cur_exit of j-1)
@@ -763,6 +887,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
     }
   }
   // --- 3. segmented exclusive scan of (blocks, dc0, dc1, dc2) ---
+  if (t == 0) L.t2 = __builtin_amdgcn_s_memtime();
   {
     int carry[4] = {0, 0, 0, 0};
     for (int base = 0; base < nsub; base += NT) {
@@ -809,60 +934,72 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       __syncthreads();
     }
   }
+  atomicAdd(&L.sym[1], nsym_sync);
+  __syncthreads();
   if (t == 0) {
     d->sync_rounds = L.rounds;
     d->pad0 = L.stages;
+    d->sym_sync = (int64_t)L.sym[1];
+    d->t_sync = (int64_t)(L.t2 - L.t1);
+    d->t_scan = (int64_t)(__builtin_amdgcn_s_memtime() - L.t2);
+    d->it_sync = (int64_t)L.it[1];
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// k_entfix: the true blocks the speculative records do not hold -- the prefix of a subsequence
-// before its merge point (fix_n > 0), every block of a subsequence that never merged or is the last
-// of its restart interval (fix_n < 0) -- decoded from the verified entry into fix records.  The last
-// subsequence of an interval decodes every remaining block; when its data runs out (bits past the
-// interval's end read as zeros) it finishes that MCU and stops: jdhuff.c insufficient_data (the rest
-// of the interval stays zero: SegView vend / kSegIns, read by the IDCT).
+// k_entwrite
 // ------------------------------------------------------------------------------------------
-struct LdsFix {
+struct LdsWrite {
+  unsigned long long t0, it;
   EntTables T;
+  alignas(16) int16_t stage[(kEntThreads + 1) * kStageStride];  // + one shared sink block
+  uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
+  int32_t bad;
+  unsigned long long sym;
 };
 
 template <int LB>
-__device__ void entfix_image(int img, int grp, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
-                             uint8_t* __restrict__ scratch) {
+__device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+                               uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
-  const int t = threadIdx.x;
-  const SubState* sub = reinterpret_cast<const SubState*>(scratch + d->off_sub);
-  const int nsub = d->nsub;
-  const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
-  // any work in this group?  (most subsequences have none)
-  bool mine = false;
-  for (int j = j0 + t; j < j1; j += kEntThreads) mine |= sub[j].fix_n != 0;
-  if (!__syncthreads_or(mine)) return;
-  __shared__ LdsFix L;
+  __shared__ LdsWrite L;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int ns = load_tables<LB>(L.T, &tables[img]);
   if (!variant_owns<LB>(ns)) return;
+  {
+    uint4* z4 = reinterpret_cast<uint4*>(L.stage);
+    for (int i = t; i < (kEntThreads + 1) * kStageStride * 2 / 16; i += kEntThreads) z4[i] = make_uint4(0, 0, 0, 0);
+  }
+  if (t == 0) {
+    L.bad = 0;
+    L.sym = 0;
+    L.it = 0;
+    L.t0 = __builtin_amdgcn_s_memtime();
+  }
+  __syncthreads();
   const EntTables& T = L.T;
   const BlkCtx K = make_ctx(T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
-  SubState* subw = reinterpret_cast<SubState*>(scratch + d->off_sub);
-  uint32_t* frec = reinterpret_cast<uint32_t*>(scratch + d->off_frec);
-  const int rec_cap = d->rec_cap, bpm = d->bpm;
+  const SubState* sub = reinterpret_cast<const SubState*>(scratch + d->off_sub);
+  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
+  const int nsub = d->nsub;
   const int64_t blocks_per_seg = d->restart_interval ? (int64_t)d->restart_interval * K.bpm : d->total_blocks;
+  const int my_base = t * kStageStride, sink_base = kEntThreads * kStageStride;
+  int bad = 0;
+  unsigned long long nsym = 0, witers = 0;
 
+  const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
   for (int jb = j0; jb < j1; jb += kEntThreads) {  // uniform trip count for the whole workgroup
     const int j = jb + t;
-    const bool active = j < j1 && sub[j].fix_n != 0;
-    if (!__builtin_amdgcn_ballot_w64(active)) continue;  // (wave-uniform: no barrier below)
+    const bool active = j < j1;
     Bits b;
-    int blk = 0, z = 0, c = 0, d0 = 0, d1 = 0, d2 = 0, sdc = 0, sac = 0, nblk = 0, limit = 0, bad = 0, recp = 0, cap = 0;
+    int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, pc = 0, sdc = 0, sac = 0;
     int64_t g = 0, gend = 0;
     uint32_t end_bit = 0, lim = 0;
     int s_int = 0;
-    bool last = false, run = false;
-    uint32_t* fr = frec;
+    bool writing = false, last_of_seg = false, run = false;
     if (active) {
       const SubState& S = sub[j];
       const int s = S.seg;
@@ -870,65 +1007,101 @@ __device__ void entfix_image(int img, int grp, ImgDesc* __restrict__ descs, cons
       gend = g0 + blocks_per_seg;
       if (gend > d->total_blocks) gend = d->total_blocks;
       g = g0 + S.nblk_ex;
+      p0 = S.dc_ex[0];
+      p1 = S.dc_ex[1];
+      p2 = S.dc_ex[2];
       blk = S.entry_bz >> 8;
       z = S.entry_bz & 0xFF;
       c = ctx_c(K, blk);
+      pc = c == 0 ? p0 : (c == 1 ? p1 : p2);  // the current block's component predictor
       sdc = ctx_dc(K, blk);
       sac = ctx_ac(K, blk);
+      writing = z == 0;
       end_bit = S.end_bit;
       s_int = s;
       lim = S.lim_bit;
-      last = S.last;
-      limit = S.fix_n > 0 ? S.fix_n : 0x7fffffff;
-      fr = frec + fix_stream(j, s, rec_cap, bpm);
-      cap = rec_cap + (last ? fix_extra(bpm) : 0);
+      last_of_seg = (j + 1 == nsub) || sub[j + 1].first;
       bits_init(b, src, S.entry_p, S.lim_bit);
-      run = nblk < limit && g < gend && (last ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
+      // the interval's last subsequence decodes every remaining block; when its data runs out
+      // (bits past lim, read as zeros) it finishes that MCU and stops: jdhuff.c insufficient_data
+      run = g < gend && (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
     }
     while (__builtin_amdgcn_ballot_w64(run)) {
       if (run) bits_fill(b);
       for (;;) {
 #pragma unroll
-        for (int u = 0; u < kSpecGroup; u++) {
-          if (run) {
-            int s, r, val;
-            const bool isdc = z == 0;
-            decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
-            if (isdc || s) {
-              const int dl = (c == 0 ? d0 : (c == 1 ? d1 : d2)) + val;
-              if (recp < cap) fr[recp] = sym_rec(isdc ? 0 : z + r, isdc ? dl : val);
-              recp++;
-            }
-            if (isdc) add_dc(c, val, d0, d1, d2);
-            if (next_z(z, s, r)) {
-              blk = blk + 1 == K.bpm ? 0 : blk + 1;
-              c = ctx_c(K, blk);
-              sdc = ctx_dc(K, blk);
-              sac = ctx_ac(K, blk);
-              g++;
-              nblk++;
-            }
-            run = nblk < limit && g < gend &&
-                  (last ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
+       for (int u = 0; u < kWriteGroup; u++) {
+        witers++;
+        bool ready = false;
+        uint32_t gdone = 0;
+        if (run) {
+          int s, r, val, sb = 0;
+          const bool isdc = z == 0;
+          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
+          nsym++;
+          bad |= sb;
+          // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
+          pc += isdc ? val : 0;
+          const int wpos = isdc ? 0 : (int)T.nat[z + r];
+          L.stage[((writing && (isdc || s)) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
+          if (next_z(z, s, r)) {
+            ready = writing;
+            gdone = (uint32_t)g;
+            p0 = c == 0 ? pc : p0;  // the component's predictor back, the next block's out
+            p1 = c == 1 ? pc : p1;
+            p2 = c == 2 ? pc : p2;
+            blk = blk + 1 == K.bpm ? 0 : blk + 1;
+            c = ctx_c(K, blk);
+            pc = c == 0 ? p0 : (c == 1 ? p1 : p2);
+            sdc = ctx_dc(K, blk);
+            sac = ctx_ac(K, blk);
+            g++;
+            writing = true;
           }
+          run = g < gend && (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
         }
-        if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kSpecGroup + 1)) ||
+        // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
+        const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
+        if (m) {
+          const int cnt = __popcll(m);
+          if (ready) {
+            const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            L.flist[wv][idx] = ((uint32_t)t << 24) | gdone;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+          for (int b0 = 0; b0 < cnt; b0 += 8) {
+            const int bi = b0 + (lane >> 3);
+            if (bi < cnt) {
+              const uint32_t f = L.flist[wv][bi];
+              uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
+              const uint4 v = *sp;
+              reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64)[lane & 7] = v;
+              *sp = make_uint4(0, 0, 0, 0);
+            }
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_wave_barrier();
+        }
+       }
+        if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kWriteGroup + 1)) ||
             !__builtin_amdgcn_ballot_w64(run))
           break;
       }
     }
-    if (active) {
-      // a block cut short by the end of the decode (z != 0) is not counted: libjpeg finishes the MCU's
-      // blocks before it stops, so z == 0 here except when g reached gend mid-block (impossible: g
-      // advances at block ends only)
-      SubState& S = subw[j];
-      S.nrec_f = recp < cap ? recp : cap;
-      S.nblk_f = nblk;
-      if (last) {
-        if (g < gend) sv.vend[s_int] = (int32_t)g;  // the rest of the interval stays zero
-        if (b.pos > lim) sv.flag[s_int] |= kSegIns;  // ran out of data (JWRN_HIT_MARKER)
-      }
+    if (active && last_of_seg) {
+      if (g < gend) sv.vend[s_int] = (int32_t)g;            // the rest of the interval stays zero
+      if (b.pos > lim) sv.flag[s_int] |= kSegIns;          // ran out of data (JWRN_HIT_MARKER)
     }
+  }
+  if (bad) atomicOr(&L.bad, 1);  // bad Huffman codes: libjpeg warns and decodes symbol 0 (statistics only)
+  atomicAdd(&L.sym, nsym);
+  if (lane == 0) atomicAdd(&L.it, 64ull * witers);
+  __syncthreads();
+  if (t == 0 && grp == 0) {  // statistics: the first group's share
+    d->sym_write = (int64_t)L.sym;
+    d->it_write = (int64_t)L.it;
+    d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - L.t0);
   }
 }
 
@@ -936,7 +1109,7 @@ template <int LB, int PHASE, int NTS = kSyncThreads>
 __device__ __forceinline__ void ent_phase(int img, int grp, ImgDesc* descs, const EntTables* tables, uint8_t* scratch) {
   if (PHASE == 0) entspec_image<LB>(img, grp, descs, tables, scratch);
   else if (PHASE == 1) entsync_image<LB, NTS>(img, descs, tables, scratch);
-  else entfix_image<LB>(img, grp, descs, tables, scratch);
+  else entwrite_image<LB>(img, grp, descs, tables, scratch);
 }
 
 // The entropy kernels take images from a route list.  MODE 0: one workgroup per list entry (grid =
@@ -986,9 +1159,9 @@ __global__ void __launch_bounds__(NTS) k_entsync(ImgDesc* __restrict__ descs, co
 }
 
 template <int LB, int RT, int MODE>
-__global__ void __launch_bounds__(kEntThreads) k_entfix(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
-                                                        uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
-                                                        int cap) {
+__global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+                                                          uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
+                                                          int cap) {
   ent_feed<LB, 2, RT, MODE>(descs, tables, scratch, routes, cap);
 }
 
@@ -1020,15 +1193,15 @@ hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, i
   return hipGetLastError();
 }
 
-hipError_t launch_entfix(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
-                         hipStream_t s) {
+hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
+                           hipStream_t s) {
   const int g = n;  // one workgroup per image on the main route
   const EntTables* tables = static_cast<const EntTables*>(etab);
   const int gs = g < 256 ? g : 256, gm = g < 192 ? g : 192;
-  hipLaunchKernelGGL((k_entfix<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL((k_entfix<11, kRtEnt11M, 2>), dim3(gm, kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables, scratch,
+  hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 2>), dim3(gm, kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables, scratch,
                      routes, cap);
-  hipLaunchKernelGGL((k_entfix<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 

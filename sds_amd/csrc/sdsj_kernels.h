@@ -23,13 +23,9 @@ hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* e
                           int cap, hipStream_t s);
 // k_entsync (sync rounds + segmented scan)
 hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, int32_t* routes, int cap, hipStream_t s);
-// k_entfix: the true blocks the speculative records do not hold, decoded again into fix records
-hipError_t launch_entfix(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
-                         hipStream_t s);
-// dense IDCT of progressive images' coefficients
+hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
+                           hipStream_t s);
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
-// record-walking IDCT of baseline images (sdsj_walk.hip)
-hipError_t launch_walk(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
 hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s);
 hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s);
 hipError_t launch_hpass(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, const int32_t* routes, int cap,

@@ -18,7 +18,6 @@
 #include <stdint.h>
 
 #include "sdsj_common.h"
-#include "sdsj_idct.h"
 #include "sdsj_kernels.h"
 
 #pragma clang fp contract(off)
@@ -159,11 +158,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
   d->off_sub = take((int64_t)d->nsub_cap * sizeof(SubState));
   d->off_rec = take((int64_t)d->nsub_cap * kRec * sizeof(SyncRec));
   d->off_ptab = take(prog ? (int64_t)sizeof(ProgTables) : 0);
-  // progressive images fill a dense coefficient array (k_prog); baseline images leave symbol records
-  d->off_coef = take(prog ? d->total_blocks * 128 : 0);
-  d->rec_cap = prog || frames ? 0 : rec_cap_for(d->sub_bits);
-  d->off_srec = take((int64_t)d->nsub_cap * d->rec_cap * 4);
-  d->off_frec = take(d->rec_cap ? ((int64_t)d->nsub_cap * d->rec_cap + (int64_t)d->nseg * fix_extra(d->bpm)) * 4 : 0);
+  d->off_coef = take(d->total_blocks * 128);
   int64_t planes = 0;
   for (int c = 0; c < d->ncomp; c++) planes += align_up((int64_t)d->comp[c].pitch * d->comp[c].bh * 8, 256);
   d->off_planes = take(planes);
@@ -305,8 +300,6 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         d.off_rec += start;
         d.off_ptab += start;
         d.off_coef += start;
-        d.off_srec += start;
-        d.off_frec += start;
         d.off_planes += start;
         d.off_rgb += start;
         d.off_tmp += start;
@@ -704,8 +697,7 @@ __global__ void __launch_bounds__(64) k_scanmap(int n, const uint8_t* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// k_idct: dequantisation + jpeg_idct_islow of a dense coefficient array (progressive images, which
-// k_prog decodes into one); 8 threads per block, 32 blocks per iteration.
+// k_idct: dequantisation + jpeg_idct_islow; 8 threads per block, 32 blocks per iteration.
 // ------------------------------------------------------------------------------------------
 constexpr int kIdctThreads = 256;
 constexpr int kIdctBlocks = kIdctThreads / 8;
@@ -715,10 +707,77 @@ constexpr int kIdctBlocks = kIdctThreads / 8;
 constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides over 8-block groups)
 constexpr int kWsStride = 72;  // ints per block in LDS (conflict-free column reads per half-wave)
 
+#define SDSJ_FIX_0_298631336 2446
+#define SDSJ_FIX_0_390180644 3196
+#define SDSJ_FIX_0_541196100 4433
+#define SDSJ_FIX_0_765366865 6270
+#define SDSJ_FIX_0_899976223 7373
+#define SDSJ_FIX_1_175875602 9633
+#define SDSJ_FIX_1_501321110 12299
+#define SDSJ_FIX_1_847759065 15137
+#define SDSJ_FIX_1_961570560 16069
+#define SDSJ_FIX_2_053119869 16819
+#define SDSJ_FIX_2_562915447 20995
+#define SDSJ_FIX_3_072711026 25172
+
+// One 1-D ISLOW butterfly (even/odd parts, jidctint.c); inputs x0..x7, outputs scaled sums
+// before the final DESCALE: o[0..7].
+__device__ __forceinline__ void islow_1d(int x0, int x1, int x2, int x3, int x4, int x5, int x6, int x7, int o[8]) {
+  int z2 = x2, z3 = x6;
+  int z1 = (z2 + z3) * SDSJ_FIX_0_541196100;
+  int t2 = z1 + z3 * (-SDSJ_FIX_1_847759065);
+  int t3 = z1 + z2 * SDSJ_FIX_0_765366865;
+  int t0 = (x0 + x4) * (1 << 13);
+  int t1 = (x0 - x4) * (1 << 13);
+  int t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
+  t0 = x7;
+  t1 = x5;
+  t2 = x3;
+  t3 = x1;
+  z1 = t0 + t3;
+  z2 = t1 + t2;
+  z3 = t0 + t2;
+  int z4 = t1 + t3;
+  int z5 = (z3 + z4) * SDSJ_FIX_1_175875602;
+  t0 *= SDSJ_FIX_0_298631336;
+  t1 *= SDSJ_FIX_2_053119869;
+  t2 *= SDSJ_FIX_3_072711026;
+  t3 *= SDSJ_FIX_1_501321110;
+  z1 *= -SDSJ_FIX_0_899976223;
+  z2 *= -SDSJ_FIX_2_562915447;
+  z3 *= -SDSJ_FIX_1_961570560;
+  z4 *= -SDSJ_FIX_0_390180644;
+  z3 += z5;
+  z4 += z5;
+  t0 += z1 + z3;
+  t1 += z2 + z4;
+  t2 += z2 + z3;
+  t3 += z1 + z4;
+  o[0] = t10 + t3;
+  o[7] = t10 - t3;
+  o[1] = t11 + t2;
+  o[6] = t11 - t2;
+  o[2] = t12 + t1;
+  o[5] = t12 - t1;
+  o[3] = t13 + t0;
+  o[4] = t13 - t0;
+}
+
+__device__ __forceinline__ uint32_t range_limit(int x) {
+  // IDCT_range_limit: (x & 1023) as a signed 10-bit value, + 128, clamped to [0, 255]
+  int s = ((x & 1023) ^ 512) - 512;
+  s += 128;
+  return (uint32_t)(s < 0 ? 0 : s > 255 ? 255 : s);
+}
+
 // Work unit = one wave: 8 horizontally adjacent blocks of one component (a "group"), so each of
 // the 8 row stores of the wave writes 64 contiguous bytes of a plane row.  8 threads per block
 // (thread r: row r, then column r); the 8 threads of a block share a wave, so the LDS transposes
 // need only in-wave ordering, no workgroup barrier.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
 __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __restrict__ descs,
                                                        const ImgTables* __restrict__ tables,
@@ -726,8 +785,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   const int img = blockIdx.y;
   if (img >= n) return;
   const ImgDesc* d = &descs[img];
-  // dense coefficients exist for progressive images only (k_prog); baseline images: k_walk
-  if (d->status != SDSJ_OK || d->geo == kGeoZeros || !d->progressive) return;
+  if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
   __shared__ int ws[kIdctBlocks * kWsStride];
   __shared__ int32_t qt[kMaxComp][64];
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
@@ -775,6 +833,19 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
   uint8_t* planes = scratch + d->off_planes;
   const int ngroups = gstart[ncomp];
+  // blocks the entropy decoder left zero (jdhuff.c insufficient_data): from vend[k] to the end of
+  // restart interval k, and all of an empty interval entered out of data
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+  const int nseg = d->nseg;
+  const int bps = d->restart_interval ? d->restart_interval * bpm : (int)d->total_blocks;
+  const int vend0 = d->progressive ? 0 : sv.vend[0];
+  const bool prog = d->progressive != 0;  // (k_prog decodes every block; no cut intervals)
+  auto zero_block = [&](int g) {
+    if (prog) return false;
+    if (nseg == 1) return g >= vend0;
+    const int k = g / bps;
+    return g >= sv.vend[k] || (k > 0 && (sv.flag[k] & kSegEmpty) && (sv.flag[k - 1] & kSegIns));
+  };
   // block of this lane in group grp: component, block coordinates, decode-order index
   // a / b for 0 <= a < 2^22, 1 <= b: float estimate, then one correction each way (exact)
   auto qdiv = [](int a, int b, float rb) {
@@ -803,7 +874,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
     if (valid) {
       // row r of the block, dequantised (DEQUANTIZE: coef * quantval)
       int16_t vv[8];
-      *reinterpret_cast<uint4*>(vv) = raw;
+      *reinterpret_cast<uint4*>(vv) = zero_block(g) ? make_uint4(0, 0, 0, 0) : raw;
       for (int k = 0; k < 8; k++) W[r * 8 + k] = (int)vv[k] * qt[c][r * 8 + k];
     }
     wave_lds_sync();

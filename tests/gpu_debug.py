@@ -37,8 +37,7 @@ class ImgDescC(ctypes.Structure):
                 ("it_write", i64), ("fused", i32), ("tile_w", i32), ("ring_rows", i32), ("rs_fast", i32), ("t_rs", i64 * 4),
                 ("warm_bits", i32), ("scan_end_code", i32), ("scan_end_raw", i64),
                 ("rgb_pitch", i32), ("ent_groups", i32),
-                ("progressive", i32), ("pad3", i32), ("sos_pos", i64), ("off_ptab", i64),
-                ("rec_cap", i32), ("pad4", i32), ("off_srec", i64), ("off_frec", i64)]
+                ("progressive", i32), ("pad3", i32), ("sos_pos", i64), ("off_ptab", i64)]
 
 
 def _memcpy_d2h(ptr: int, nbytes: int) -> np.ndarray:
@@ -82,9 +81,9 @@ def stage_report(engine, jpg: bytes, resolution=(256, 256)) -> list[str]:
     lines.append(f"desc: {d.width}x{d.height} ncomp={d.ncomp} bpm={d.bpm} mcu={d.mcux}x{d.mcuy} nseg={d.nseg} "
                  f"ulen={d.ulen} nsub={d.nsub} sub_bits={d.sub_bits} geo={d.geo} crop=({d.cx0},{d.cy0},{d.cw},{d.ch}) "
                  f"need_h={d.need_h} need_v={d.need_v} yf={d.yf} yl={d.yl} status={d.status}")
-    # coefficients (progressive images only: baseline images leave symbol records, k_walk)
-    coef = fetch(d.off_coef, d.total_blocks * 128).view(np.int16).reshape(-1, 64) if d.progressive else None
-    for c in range(d.ncomp if d.progressive else 0):
+    # coefficients: device layout is decode order [g][64] natural order
+    coef = fetch(d.off_coef, d.total_blocks * 128).view(np.int16).reshape(-1, 64)
+    for c in range(d.ncomp):
         ref = O.coefficients(jpg, c)  # [bh][bw][64]
         cd = d.comp[c]
         got = np.zeros_like(ref)
