@@ -27,6 +27,7 @@ def main():
             pool.append(encode_jpeg(np.array(Image.fromarray(rgb).convert("L")), 90) if kw is None
                         else encode_jpeg(rgb, 90, **kw))
         jpgs = [pool[i % len(pool)] for i in range(n)]
+        eng.reserve(JpegEngine.scratch_need(jpgs, (256, 256)) + (64 << 20))
         lens = [len(j) for j in jpgs]
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
         blob = torch.from_numpy(np.frombuffer(b"".join(jpgs), np.uint8).copy()).cuda()

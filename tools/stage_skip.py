@@ -10,10 +10,9 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CONFIGS = [
-    {}, {"SDSJ_SKIP_STAGES": str(1 << 6)}, {"SDSJ_SKIP_STAGES": str(1 << 7)}, {"SDSJ_SKIP_STAGES": str(1 << 12)},
-    {"SDSJ_SKIP_STAGES": str((1 << 6) | (1 << 7))},
-    {"SDSJ_WARM_BITS": "1000"}, {"SDSJ_WARM_BITS": "1500"}, {"SDSJ_WARM_BITS": "2500"}, {"SDSJ_WARM_BITS": "3000"},
-    {"SDSJ_LANES": "1"}, {"SDSJ_LANES": "2"}, {"SDSJ_LANES": "3"},
+    {}, {"SDSJ_LANE_MID": "5"}, {"SDSJ_LANE_MID": "6"}, {"SDSJ_LANE_MID": "7"}, {"SDSJ_LANE_MID": "8"},
+    {"SDSJ_LANES": "2", "SDSJ_LANE_MID": "6"}, {"SDSJ_LANES": "2", "SDSJ_LANE_MID": "8"},
+    {"SDSJ_SKIP_STAGES": str(1 << 6)}, {"SDSJ_SKIP_STAGES": str(1 << 7)}, {"SDSJ_SKIP_STAGES": str(1 << 12)},
 ]
 
 CHILD = r'''
