@@ -34,10 +34,14 @@
 
 namespace sdsj {
 
+#ifndef SDSJ_STATS
+#define SDSJ_STATS 0  // 1: per-image symbol / tick / lane-utilisation statistics (tools/entropy_stats.py builds)
+#endif
+constexpr bool kStats = SDSJ_STATS != 0;
+
 constexpr int kEntThreads = kDecodeThreads;
 constexpr int kLutEntries = 1 << 13;  // LDS lookup capacity: 4 tables x 2^11 or 8 x 2^10
 constexpr int kStageStride = 64;      // int16 per lane staging block (one 128-byte block)
-constexpr int kBudget0 = 64;          // first sync stage's symbol budget
 constexpr int kMaxTasks = kEntThreads;  // per round (more: picked up by the next round)
 // k_entsync is latency-bound (a few serial re-decodes per image): one wave per image keeps more
 // images in flight per CU than a 4-wave workgroup would (the LDS tables bound both)
@@ -446,7 +450,7 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           b.buf <<= tot;
           b.nb -= tot;
           b.pos += tot;
-          nsym++;
+          if (kStats) nsym++;
           if (next_z(z, sz, r)) {
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
             sdc = ctx_dc(K, blk);
@@ -476,7 +480,7 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           int s, r, val;
           const bool isdc = z == 0;
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
-          nsym++;
+          if (kStats) nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           if (next_z(z, s, r)) {
             add_dc(c, dcd, d0, d1, d2);
@@ -539,7 +543,7 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           int sy, r, val;
           const bool isdc = z == 0;
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, sy, r, val, bad);
-          nsym++;
+          if (kStats) nsym++;
           dcd = isdc ? val : dcd;
           if (next_z(z, sy, r)) {
             add_dc(c, dcd, d0, d1, d2);
@@ -590,126 +594,6 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
     S.new_dc[2] = d2;
   }
   return nsym;
-}
-
-// Records of the speculative pass, kRQ at a time in registers (filled with the bit queue).
-constexpr int kRQ = 6;
-
-__device__ __forceinline__ void rec_fill(const SyncRec* rec, int ri, int nrec, uint32_t* rp, uint32_t* rx) {
-  const uint2* r2 = reinterpret_cast<const uint2*>(rec);
-#pragma unroll
-  for (int k = 0; k < kRQ; k++) {
-    const int i = ri + k;
-    const uint2 v = r2[i < kRec ? i : kRec - 1];
-    rp[k] = i < nrec ? v.x : 0xFFFFFFFFu;  // past the last record: never reached
-    rx[k] = i < nrec ? v.y : 0u;           // dc (low 16 bits) | blk << 16
-  }
-}
-
-// Resumable re-decode of S (state in S.res_*), at most `budget` symbols.  Returns true when the
-// task is finished (merged with a record, or reached the subsequence end); new_exit_* / new_nblk /
-// new_dc then hold the result.  Otherwise the state is saved for the next stage.
-template <int LB>
-__device__ bool sync_step(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, const SyncRec* rec,
-                          int budget, int* nsym_out) {
-  const uint32_t end = S.end_bit;
-  const int nrec = S.nrec;
-  Bits b;
-  bits_init(b, src, S.res_p, S.lim_bit);
-  int blk = S.res_bz >> 8, z = S.res_bz & 0xFF;
-  int nblk = S.res_nblk, ri = S.res_ri;
-  int d0 = S.res_dc[0], d1 = S.res_dc[1], d2 = S.res_dc[2];
-  int q0 = S.res_q[0], q1 = S.res_q[1], q2 = S.res_q[2];  // speculative DC prefix up to record ri
-  int bad = 0, nsym = 0;
-  int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
-  uint32_t rp[kRQ], rx[kRQ];
-  int nr = 0, done_blk = 0;
-  uint32_t P = 0;
-  bool adv = false, merged = false;  // adv: records up to boundary P still to be passed
-  bool run = (b.pos < end || z != 0) && budget > 0;
-  while (__builtin_amdgcn_ballot_w64(run)) {
-    if (run) {
-      bits_fill(b);
-      rec_fill(rec, ri, nrec, rp, rx);
-      nr = kRQ;
-    }
-    for (;;) {
-      const bool dry = run && (adv ? nr == 0 : !bits_can(b));
-      if (__builtin_amdgcn_ballot_w64(dry) || !__builtin_amdgcn_ballot_w64(run)) break;
-      if (run) {
-        if (!adv) {
-          int s, r, val;
-          const bool isdc = z == 0;
-          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
-          nsym++;
-          add_dc(c, isdc ? val : 0, d0, d1, d2);
-          if (next_z(z, s, r)) {
-            done_blk = blk;
-            blk = blk + 1 == K.bpm ? 0 : blk + 1;
-            c = ctx_c(K, blk);
-            sdc = ctx_dc(K, blk);
-            sac = ctx_ac(K, blk);
-            nblk++;
-            adv = true;
-            P = b.pos;
-          }
-        }
-        // pass the records at or before P; a record at P of the same MCU block = merged paths
-        while (adv && nr > 0) {
-          const uint32_t Rp = rp[0], Rx = rx[0];
-          if (Rp > P) {
-            adv = false;
-            break;
-          }
-          const int rb = (int)(Rx >> 16) & 0xFF;
-          add_dc(ctx_c(K, rb), (int)(int16_t)(Rx & 0xFFFF), q0, q1, q2);
-          ri++;
-#pragma unroll
-          for (int k = 0; k + 1 < kRQ; k++) {
-            rp[k] = rp[k + 1];
-            rx[k] = rx[k + 1];
-          }
-          nr--;
-          if (Rp == P && rb == done_blk) {
-            merged = true;
-            adv = false;
-          }
-        }
-        run = !merged && (adv || ((b.pos < end || z != 0) && nsym < budget));
-      }
-    }
-  }
-  *nsym_out = nsym;
-  if (merged) {
-    // the remainder of the speculative result is exact
-    S.new_exit_p = S.spec_exit_p;
-    S.new_exit_bz = S.spec_exit_bz;
-    S.new_nblk = nblk + S.spec_nblk - ri;
-    S.new_dc[0] = d0 + S.spec_dc[0] - q0;
-    S.new_dc[1] = d1 + S.spec_dc[1] - q1;
-    S.new_dc[2] = d2 + S.spec_dc[2] - q2;
-    return true;
-  }
-  if (b.pos >= end && z == 0) {
-    S.new_exit_p = b.pos;
-    S.new_exit_bz = (uint16_t)((blk << 8) | z);
-    S.new_nblk = nblk;
-    S.new_dc[0] = d0;
-    S.new_dc[1] = d1;
-    S.new_dc[2] = d2;
-    return true;
-  }
-  S.res_p = b.pos;
-  S.res_bz = (uint16_t)((blk << 8) | z);
-  S.res_nblk = nblk;
-  S.res_ri = ri;
-  S.res_dc[0] = d0;
-  S.res_dc[1] = d1;
-  S.res_dc[2] = d2;
-  S.res_q[0] = q0;
-  S.res_q[1] = q1;
-  S.res_q[2] = q2;
-  return false;
 }
 
 template <int LB>
@@ -770,26 +654,28 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   unsigned long long nsym_spec = 0;
 
   // --- 1. speculative pass ---
-  if (t == 0) L.t0 = __builtin_amdgcn_s_memtime();
-  if ((t & 63) == 0) L.wmax[t >> 6] = 0;
+  if (kStats && t == 0) L.t0 = __builtin_amdgcn_s_memtime();
+  if (kStats && (t & 63) == 0) L.wmax[t >> 6] = 0;
   __syncthreads();
   // this workgroup's share of the subsequences (every group computes the same layout above)
   const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
   for (int j = j0 + t; j < j1; j += kEntThreads) {
     const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, (uint32_t)sv.lo[sub[j].seg] * 8u,
                                 (uint32_t)d->warm_bits);
-    nsym_spec += k;
-    atomicMax(&L.wmax[t >> 6], k);
+    if (kStats) {
+      nsym_spec += k;
+      atomicMax(&L.wmax[t >> 6], k);
+    }
   }
   __syncthreads();
-  if (t == 0) {
+  if (kStats && t == 0) {
     L.t1 = __builtin_amdgcn_s_memtime();
     for (int w = 0; w < kEntThreads / 64; w++) L.it[0] += 64ull * L.wmax[w];
   }
-  atomicAdd(&L.sym[0], nsym_spec);
+  if (kStats) atomicAdd(&L.sym[0], nsym_spec);
   __syncthreads();
   if (t == 0) d->nsub = nsub;
-  if (t == 0 && grp == 0) {  // statistics: the first group's share
+  if (kStats && t == 0 && grp == 0) {  // statistics: the first group's share
     d->sym_spec = (int64_t)L.sym[0];
     d->t_spec = (int64_t)(L.t1 - L.t0);
     d->it_spec = (int64_t)L.it[0];
@@ -813,7 +699,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
     L.stages = 0;
     L.sym[0] = L.sym[1] = 0;
     L.it[0] = L.it[1] = 0;
-    L.t1 = __builtin_amdgcn_s_memtime();
+    if (kStats) L.t1 = __builtin_amdgcn_s_memtime();
   }
   // any subsequence whose entry differs from its predecessor's exit?  Only then are the decode
   // tables built (most images: none after the warm-up)
@@ -846,12 +732,6 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
           SubState& S = sub[j];
           S.new_entry_p = ep;
           S.new_entry_bz = ebz;
-          S.res_p = ep;
-          S.res_bz = ebz;
-          S.res_nblk = 0;
-          S.res_ri = 0;
-          S.res_dc[0] = S.res_dc[1] = S.res_dc[2] = 0;
-          S.res_q[0] = S.res_q[1] = S.res_q[2] = 0;
         }
         ntask += tot;
       }
@@ -864,7 +744,8 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       }
       for (int i = t; i < ntask; i += NT) {
         const int j = L.u.task[0][i];
-        nsym_sync += sync_full<kSyncLB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec);
+        const int k = sync_full<kSyncLB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec);
+        if (kStats) nsym_sync += k;
       }
       __syncthreads();
       // commit every task of the round (entries first: they were read from cur_exit of j-1)
@@ -887,7 +768,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
     }
   }
   // --- 3. segmented exclusive scan of (blocks, dc0, dc1, dc2) ---
-  if (t == 0) L.t2 = __builtin_amdgcn_s_memtime();
+  if (kStats && t == 0) L.t2 = __builtin_amdgcn_s_memtime();
   {
     int carry[4] = {0, 0, 0, 0};
     for (int base = 0; base < nsub; base += NT) {
@@ -934,11 +815,13 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       __syncthreads();
     }
   }
-  atomicAdd(&L.sym[1], nsym_sync);
+  if (kStats) atomicAdd(&L.sym[1], nsym_sync);
   __syncthreads();
   if (t == 0) {
     d->sync_rounds = L.rounds;
     d->pad0 = L.stages;
+  }
+  if (kStats && t == 0) {
     d->sym_sync = (int64_t)L.sym[1];
     d->t_sync = (int64_t)(L.t2 - L.t1);
     d->t_scan = (int64_t)(__builtin_amdgcn_s_memtime() - L.t2);
@@ -975,7 +858,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     L.bad = 0;
     L.sym = 0;
     L.it = 0;
-    L.t0 = __builtin_amdgcn_s_memtime();
+    if (kStats) L.t0 = __builtin_amdgcn_s_memtime();
   }
   __syncthreads();
   const EntTables& T = L.T;
@@ -985,7 +868,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   const SubState* sub = reinterpret_cast<const SubState*>(scratch + d->off_sub);
   int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
   const int nsub = d->nsub;
-  const int64_t blocks_per_seg = d->restart_interval ? (int64_t)d->restart_interval * K.bpm : d->total_blocks;
+  const int blocks_per_seg = d->restart_interval ? d->restart_interval * K.bpm : (int)d->total_blocks;
   const int my_base = t * kStageStride, sink_base = kEntThreads * kStageStride;
   int bad = 0;
   unsigned long long nsym = 0, witers = 0;
@@ -996,16 +879,16 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     const bool active = j < j1;
     Bits b;
     int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, pc = 0, sdc = 0, sac = 0;
-    int64_t g = 0, gend = 0;
+    int g = 0, gend = 0;  // decode-order block indices (total_blocks < 2^24, setup_geometry)
     uint32_t end_bit = 0, lim = 0;
     int s_int = 0;
     bool writing = false, last_of_seg = false, run = false;
     if (active) {
       const SubState& S = sub[j];
       const int s = S.seg;
-      const int64_t g0 = (int64_t)s * blocks_per_seg;
+      const int g0 = s * blocks_per_seg;
       gend = g0 + blocks_per_seg;
-      if (gend > d->total_blocks) gend = d->total_blocks;
+      if (gend > (int)d->total_blocks) gend = (int)d->total_blocks;
       g = g0 + S.nblk_ex;
       p0 = S.dc_ex[0];
       p1 = S.dc_ex[1];
@@ -1031,14 +914,14 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       for (;;) {
 #pragma unroll
        for (int u = 0; u < kWriteGroup; u++) {
-        witers++;
+        if (kStats) witers++;
         bool ready = false;
         uint32_t gdone = 0;
         if (run) {
           int s, r, val, sb = 0;
           const bool isdc = z == 0;
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
-          nsym++;
+          if (kStats) nsym++;
           bad |= sb;
           // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
           pc += isdc ? val : 0;
@@ -1090,15 +973,17 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       }
     }
     if (active && last_of_seg) {
-      if (g < gend) sv.vend[s_int] = (int32_t)g;            // the rest of the interval stays zero
+      if (g < gend) sv.vend[s_int] = g;                     // the rest of the interval stays zero
       if (b.pos > lim) sv.flag[s_int] |= kSegIns;          // ran out of data (JWRN_HIT_MARKER)
     }
   }
   if (bad) atomicOr(&L.bad, 1);  // bad Huffman codes: libjpeg warns and decodes symbol 0 (statistics only)
-  atomicAdd(&L.sym, nsym);
-  if (lane == 0) atomicAdd(&L.it, 64ull * witers);
+  if (kStats) {
+    atomicAdd(&L.sym, nsym);
+    if (lane == 0) atomicAdd(&L.it, 64ull * witers);
+  }
   __syncthreads();
-  if (t == 0 && grp == 0) {  // statistics: the first group's share
+  if (kStats && t == 0 && grp == 0) {  // statistics: the first group's share
     d->sym_write = (int64_t)L.sym;
     d->it_write = (int64_t)L.it;
     d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - L.t0);

@@ -786,8 +786,8 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   if (img >= n) return;
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
-  __shared__ int ws[kIdctBlocks * kWsStride];
-  __shared__ int32_t qt[kMaxComp][64];
+  __shared__ alignas(16) int ws[kIdctBlocks * kWsStride];
+  __shared__ alignas(16) int32_t qt[kMaxComp][64];
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
   __shared__ int32_t gstart[kMaxComp + 1], ngx[kMaxComp], cbw[kMaxComp], ch_[kMaxComp], cv_[kMaxComp], cpitch[kMaxComp];
   __shared__ int32_t cgx0[kMaxComp], cby0[kMaxComp];  // first 8-block group column / block row needed
@@ -872,10 +872,14 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   auto process = [&](const uint4& raw, int c, int by, int bx, int g) {
     const bool valid = g >= 0;
     if (valid) {
-      // row r of the block, dequantised (DEQUANTIZE: coef * quantval)
-      int16_t vv[8];
-      *reinterpret_cast<uint4*>(vv) = zero_block(g) ? make_uint4(0, 0, 0, 0) : raw;
-      for (int k = 0; k < 8; k++) W[r * 8 + k] = (int)vv[k] * qt[c][r * 8 + k];
+      // row r of the block, dequantised (DEQUANTIZE: coef * quantval), stored as two 16-byte writes
+      const uint4 v = zero_block(g) ? make_uint4(0, 0, 0, 0) : raw;
+      const int4 q0 = *reinterpret_cast<const int4*>(&qt[c][r * 8]), q1 = *reinterpret_cast<const int4*>(&qt[c][r * 8 + 4]);
+      auto lo16 = [](uint32_t x) { return (int)(int16_t)(x & 0xFFFF); };
+      auto hi16 = [](uint32_t x) { return (int)(int16_t)(x >> 16); };
+      *reinterpret_cast<int4*>(W + r * 8) = make_int4(lo16(v.x) * q0.x, hi16(v.x) * q0.y, lo16(v.y) * q0.z, hi16(v.y) * q0.w);
+      *reinterpret_cast<int4*>(W + r * 8 + 4) =
+          make_int4(lo16(v.z) * q1.x, hi16(v.z) * q1.y, lo16(v.w) * q1.z, hi16(v.w) * q1.w);
     }
     wave_lds_sync();
     // pass 1: column r
@@ -897,9 +901,9 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
     wave_lds_sync();
     // pass 2: row r -> 8 bytes of plane row by * 8 + r
     if (valid) {
-      const int* w = W + r * 8;
+      const int4 w0 = *reinterpret_cast<const int4*>(W + r * 8), w1 = *reinterpret_cast<const int4*>(W + r * 8 + 4);
       int o[8];
-      islow_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+      islow_1d(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, o);
       uint32_t lo = 0, hi = 0;
       for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
       for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
