@@ -1,10 +1,13 @@
 #!/bin/bash
 # PMC passes (one counter group per rocprofv3 run, no tracing domains) over a short bench run;
 # tools/pmc_summary.py then folds the CSVs into gpurun_out/pmc.json (mean per dispatch per kernel).
+# SDSJ_LANES (default 1 here) is the engine's lane count for the whole run: at 1, one dispatch of a
+# kernel covers the whole batch, the unit bench.py's roofline prices.
 # usage: tools/pmc.sh [extra bench args]
 set -e
 export TMPDIR=/tmp
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --rows 20000 $*"
+export SDSJ_LANES=${SDSJ_LANES:-1}
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 --rows 20000 $*"
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU" \
@@ -12,6 +15,6 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   rm -rf gpurun_out/pmc_$i
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_$i -o p -- $B > gpurun_out/pmc_$i.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_$i -o p -- $B > gpurun_out/pmc_$i.log 2>&1
 done
-python3 tools/pmc_summary.py gpurun_out 4096 "$(python3 -c 'import bench; print(bench.engine_lanes(4096))')" > gpurun_out/pmc.json
+python3 tools/pmc_summary.py gpurun_out 4096 "$SDSJ_LANES" > gpurun_out/pmc.json

@@ -20,6 +20,7 @@ for path in glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv
 out = {k: {c: sum(v) / len(v) for c, v in sorted(cs.items())} for k, cs in sorted(acc.items())}
 batch = int(sys.argv[2]) if len(sys.argv) > 2 else None
 lanes = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+head = os.environ.get("SDSJ_HEAD", "")
 json.dump({"note": "rocprofv3 --pmc, mean per dispatch (bench.py --steps 2 --warmup 1); one dispatch = one lane "
-                   "of the batch (batch / lanes images)", "batch": batch, "lanes": lanes,
+                   "of the batch (batch / lanes images)", "batch": batch, "lanes": lanes, "head": head,
            "kernels": out}, sys.stdout, indent=1)
