@@ -230,11 +230,16 @@ enum Route : int32_t {
   kRtEnt10, kRtEnt11,             // entropy kernels by lookahead width
   kRtEnt11M,                      // LB = 11 images decoded by several workgroups (ent_groups > 1)
   kRtProg,                        // progressive images (k_prog)
+  kRtEnt11G,                      // (count only) (image, group) tasks of the kRtEnt11M images: group_tasks()
   kNumRoutes
 };
 constexpr int kRouteSlots = 32;  // counts [0, kNumRoutes), the rest zero
 static_assert(kNumRoutes <= kRouteSlots, "route counts must fit the count slots");
 SDSJ_HD inline const int32_t* route_list(const int32_t* routes, int cap, int r) { return routes + kRouteSlots + r * cap; }
+// After the lists: one entry (image << 3 | group) per workgroup task of a multi-group image, so the
+// spec / write passes give every (image, group) its own workgroup (count in routes[kRtEnt11G]).
+SDSJ_HD inline int32_t* group_tasks(int32_t* routes, int cap) { return routes + kRouteSlots + (int64_t)kNumRoutes * cap; }
+SDSJ_HD inline int64_t route_ints(int cap) { return kRouteSlots + (int64_t)(kNumRoutes + kMaxEntGroups) * cap; }
 SDSJ_HD inline int rs_route(int kt) { return kRt3 + (kt - 3) / 2; }
 // generic fused resample route of an image whose horizontal pass has kt taps (1: none)
 SDSJ_HD inline int gen_route(int kt) {

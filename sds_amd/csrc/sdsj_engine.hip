@@ -254,7 +254,7 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
       SDSJ_HIP(e, hipEventCreateWithFlags(&e->ev_join[k], hipEventDisableTiming));
     }
   const int64_t ob = out_bytes_per_image(op);
-  const size_t rsz = kRouteSlots + (size_t)kNumRoutes * e->max_batch;
+  const size_t rsz = (size_t)route_ints(e->max_batch);
   for (int k = 0; k < nl; k++) {
     const int i0 = (int)((int64_t)n * k / nl), i1 = (int)((int64_t)n * (k + 1) / nl);
     const Lane ln = k == 0 ? first
@@ -581,11 +581,11 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   if (e->lane_mid >= 0 && e->lane_mid < 2) e->lane_mid = 2;  // a lane's k_plan reads the previous lane's total
   if (hipMalloc(&e->d_total, sizeof(int64_t)) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_totals_x, sizeof(int64_t) * (kMaxLanes - 1)) != hipSuccess) return cleanup(SDSJ_ENOMEM);
-  if (hipMalloc(&e->d_routes_x, sizeof(int32_t) * (kMaxLanes - 1) * (kRouteSlots + (size_t)kNumRoutes * e->max_batch)) !=
+  if (hipMalloc(&e->d_routes_x, sizeof(int32_t) * (kMaxLanes - 1) * (size_t)route_ints(e->max_batch)) !=
       hipSuccess)
     return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_etab, enttab_bytes() * e->max_batch) != hipSuccess) return cleanup(SDSJ_ENOMEM);
-  if (hipMalloc(&e->d_routes, sizeof(int32_t) * (kRouteSlots + (size_t)kNumRoutes * e->max_batch)) != hipSuccess)
+  if (hipMalloc(&e->d_routes, sizeof(int32_t) * (size_t)route_ints(e->max_batch)) != hipSuccess)
     return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_lut, sizeof(float) * 256) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_counters, sizeof(unsigned long long) * SDSJ_NUM_COUNTERS) != hipSuccess) return cleanup(SDSJ_ENOMEM);

@@ -999,12 +999,18 @@ __device__ __forceinline__ void ent_phase(int img, int grp, ImgDesc* descs, cons
 
 // The entropy kernels take images from a route list.  MODE 0: one workgroup per list entry (grid =
 // batch size, surplus workgroups exit at once) -- the main route (LB = 11, one group per image).
-// MODE 1: a small grid strides over the list and runs each image's groups in turn (LB = 10, and the
-// sync pass of multi-group images).  MODE 2: grid.y = kMaxEntGroups, workgroup y takes group y of
-// each image it strides over (LB = 11 images with ent_groups > 1).  The sync pass is per image.
+// MODE 1: a small grid strides over the list and runs each image's groups in turn (LB = 10).  MODE 3:
+// one workgroup per (image, group) task of the LB = 11 images with ent_groups > 1 (grid = batch x
+// kMaxEntGroups, surplus workgroups exit at once).  The sync pass is per image (MODE 0 for them too).
 template <int LB, int PHASE, int RT, int MODE, int NTS = kSyncThreads>
 __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables, uint8_t* scratch, int32_t* routes,
                                          int cap) {
+  if (MODE == 3) {  // one workgroup per (image, group) task (k_plan's group_tasks list)
+    if ((int)blockIdx.x >= routes[kRtEnt11G]) return;
+    const int task = group_tasks(routes, cap)[blockIdx.x];
+    ent_phase<LB, PHASE, NTS>(task >> 3, task & 7, descs, tables, scratch);
+    return;
+  }
   const int cnt = routes[RT];
   const int32_t* list = route_list(routes, cap, RT);
   if (MODE == 0) {
@@ -1057,10 +1063,10 @@ hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* e
   const int g = n;  // one workgroup per image on the main route
   EntTables* tables = static_cast<EntTables*>(etab);
   hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
-  const int gs = g < 256 ? g : 256, gm = g < 192 ? g : 192;
+  const int gs = g < 256 ? g : 256;
   hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 2>), dim3(gm, kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables, scratch,
-                     routes, cap);
+  hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3>), dim3(g * kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables,
+                     scratch, routes, cap);
   hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
@@ -1071,7 +1077,7 @@ hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, i
   const int gs = g < 256 ? g : 256;
   hipLaunchKernelGGL((k_entsync<11, kRtEnt11, 0, kSyncThreads>), dim3(g), dim3(kSyncThreads), 0, s, descs, tables, scratch,
                      routes, cap);
-  hipLaunchKernelGGL((k_entsync<11, kRtEnt11M, 1, kEntThreads>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch,
+  hipLaunchKernelGGL((k_entsync<11, kRtEnt11M, 0, kEntThreads>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch,
                      routes, cap);
   hipLaunchKernelGGL((k_entsync<10, kRtEnt10, 1, kSyncThreads>), dim3(gs), dim3(kSyncThreads), 0, s, descs, tables, scratch,
                      routes, cap);
@@ -1082,10 +1088,10 @@ hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scr
                            hipStream_t s) {
   const int g = n;  // one workgroup per image on the main route
   const EntTables* tables = static_cast<const EntTables*>(etab);
-  const int gs = g < 256 ? g : 256, gm = g < 192 ? g : 192;
+  const int gs = g < 256 ? g : 256;
   hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 2>), dim3(gm, kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables, scratch,
-                     routes, cap);
+  hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(g * kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables,
+                     scratch, routes, cap);
   hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }

@@ -318,6 +318,11 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         const int re = d.progressive ? kRtProg : ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
         int32_t* lst = routes + kRouteSlots + re * cap;
         lst[atomicAdd(&rcnt[re], 1)] = i;
+        if (re == kRtEnt11M) {
+          int32_t* gt = group_tasks(routes, cap);
+          const int b = atomicAdd(&rcnt[kRtEnt11G], d.ent_groups);
+          for (int q = 0; q < d.ent_groups; q++) gt[b + q] = (i << 3) | q;
+        }
         if (d.geo != kGeoZeros) {
           const int rr = !d.fused ? kRtUnfused
                          : (d.rs_fast ? rs_route(d.rs_fast) : gen_route(d.need_h ? d.ksh : 1));
