@@ -28,8 +28,10 @@ constexpr int kWarmBits = 2000;       // speculative warm-up before each subsequ
 constexpr int kWarmDiv = 3;           // ... or sub_bits / kWarmDiv when that is larger
 // large images: ent_groups = ceil(bits / (kDecodeThreads x kGroupBits)) workgroups (<= kMaxEntGroups)
 // share the subsequences, so one lane's serial decode stays near kGroupBits
-constexpr int kGroupBits = 8192;
-constexpr int kMaxEntGroups = 8;
+constexpr int kGroupBits = 4096;
+constexpr int kMaxEntGroups = 16;
+constexpr int kGroupShift = 4;  // (image << kGroupShift) | group in the group-task list
+static_assert((1 << kGroupShift) >= kMaxEntGroups, "group index must fit the task encoding");
 constexpr int kUPad = 128;            // zero bytes after each unstuffed stream (bit-reader prefetch)
 constexpr int kMaxSpan = 960;         // source columns per fused-resample tile (LDS row width)
 constexpr int kRingDW = 3072;         // fused-resample ring (dwords): ring_rows x (3072 / ring_rows) columns
@@ -236,7 +238,7 @@ enum Route : int32_t {
 constexpr int kRouteSlots = 32;  // counts [0, kNumRoutes), the rest zero
 static_assert(kNumRoutes <= kRouteSlots, "route counts must fit the count slots");
 SDSJ_HD inline const int32_t* route_list(const int32_t* routes, int cap, int r) { return routes + kRouteSlots + r * cap; }
-// After the lists: one entry (image << 3 | group) per workgroup task of a multi-group image, so the
+// After the lists: one entry (image << kGroupShift | group) per workgroup task of a multi-group image, so the
 // spec / write passes give every (image, group) its own workgroup (count in routes[kRtEnt11G]).
 SDSJ_HD inline int32_t* group_tasks(int32_t* routes, int cap) { return routes + kRouteSlots + (int64_t)kNumRoutes * cap; }
 SDSJ_HD inline int64_t route_ints(int cap) { return kRouteSlots + (int64_t)(kNumRoutes + kMaxEntGroups) * cap; }

@@ -42,7 +42,8 @@ constexpr bool kStats = SDSJ_STATS != 0;
 constexpr int kEntThreads = kDecodeThreads;
 constexpr int kLutEntries = 1 << 13;  // LDS lookup capacity: 4 tables x 2^11 or 8 x 2^10
 constexpr int kStageStride = 64;      // int16 per lane staging block (one 128-byte block)
-constexpr int kMaxTasks = kEntThreads;  // per round (more: picked up by the next round)
+template <int NT>
+constexpr int max_tasks() { return 4 * NT; }  // sync tasks per round (more: picked up by the next round)
 // k_entsync is latency-bound (a few serial re-decodes per image): one wave per image keeps more
 // images in flight per CU than a 4-wave workgroup would (the LDS tables bound both)
 constexpr int kSyncThreads = 64;
@@ -398,7 +399,7 @@ struct LdsSyncT {
   TT T;
   int32_t tmp[NT];  // block_excl_scan scratch
   union {                    // sync rounds | final segmented scan (never live together)
-    int32_t task[1][kMaxTasks];
+    int32_t task[1][max_tasks<NT>()];
     struct {
       int32_t scan[4][NT];
       int32_t flag[NT];
@@ -727,7 +728,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
         }
         int tot;
         const int off = block_excl_scan<NT>(need ? 1 : 0, L.tmp, &tot);
-        if (need && ntask + off < kMaxTasks) {
+        if (need && ntask + off < max_tasks<NT>()) {
           L.u.task[0][ntask + off] = j;
           SubState& S = sub[j];
           S.new_entry_p = ep;
@@ -735,7 +736,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
         }
         ntask += tot;
       }
-      if (ntask > kMaxTasks) ntask = kMaxTasks;  // the rest are picked up by the next round
+      if (ntask > max_tasks<NT>()) ntask = max_tasks<NT>();  // the rest are picked up by the next round
       __syncthreads();
       if (ntask == 0) break;
       if (t == 0) {
@@ -1008,7 +1009,7 @@ __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables
   if (MODE == 3) {  // one workgroup per (image, group) task (k_plan's group_tasks list)
     if ((int)blockIdx.x >= routes[kRtEnt11G]) return;
     const int task = group_tasks(routes, cap)[blockIdx.x];
-    ent_phase<LB, PHASE, NTS>(task >> 3, task & 7, descs, tables, scratch);
+    ent_phase<LB, PHASE, NTS>(task >> kGroupShift, task & ((1 << kGroupShift) - 1), descs, tables, scratch);
     return;
   }
   const int cnt = routes[RT];

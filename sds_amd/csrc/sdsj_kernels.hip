@@ -321,7 +321,7 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         if (re == kRtEnt11M) {
           int32_t* gt = group_tasks(routes, cap);
           const int b = atomicAdd(&rcnt[kRtEnt11G], d.ent_groups);
-          for (int q = 0; q < d.ent_groups; q++) gt[b + q] = (i << 3) | q;
+          for (int q = 0; q < d.ent_groups; q++) gt[b + q] = (i << kGroupShift) | q;
         }
         if (d.geo != kGeoZeros) {
           const int rr = !d.fused ? kRtUnfused
