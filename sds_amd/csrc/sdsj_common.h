@@ -28,7 +28,7 @@ constexpr int kWarmBits = 2000;       // speculative warm-up before each subsequ
 constexpr int kWarmDiv = 3;           // ... or sub_bits / kWarmDiv when that is larger
 // large images: ent_groups = ceil(bits / (kDecodeThreads x kGroupBits)) workgroups (<= kMaxEntGroups)
 // share the subsequences, so one lane's serial decode stays near kGroupBits
-constexpr int kGroupBits = 4096;
+constexpr int kGroupBits = 8192;
 constexpr int kMaxEntGroups = 16;
 constexpr int kGroupShift = 4;  // (image << kGroupShift) | group in the group-task list
 static_assert((1 << kGroupShift) >= kMaxEntGroups, "group index must fit the task encoding");
