@@ -48,7 +48,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-ffp-contract=off", "-Wl,-z,defs", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
-           "-I", os.path.join(REPO, "include"), "-o", tmp] + sources()
+           "-I", os.path.join(REPO, "include"), "-o", tmp] + os.environ.get("SDSJ_CFLAGS", "").split() + sources()
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -33,6 +33,8 @@ constexpr int kMaxEntGroups = 16;
 constexpr int kGroupShift = 4;  // (image << kGroupShift) | group in the group-task list
 static_assert((1 << kGroupShift) >= kMaxEntGroups, "group index must fit the task encoding");
 constexpr int kUPad = 128;            // zero bytes after each unstuffed stream (bit-reader prefetch)
+constexpr int kUsTileBytes = 8192;    // unstuffing tile: 256 threads x 32 bytes
+constexpr int kUsSerialTiles = 64;    // images of at most this many tiles are unstuffed by one workgroup
 constexpr int kMaxSpan = 960;         // source columns per fused-resample tile (LDS row width)
 constexpr int kRingDW = 3072;         // fused-resample ring (dwords): ring_rows x (3072 / ring_rows) columns
 constexpr int kRingMaxRows = 16;      // vertical windows longer than this use the unfused path
@@ -149,6 +151,16 @@ struct ImgDesc {
   int32_t pad3;
   int64_t sos_pos;
   int64_t off_ptab;
+  // k_unstuff: per 8 KiB tile of the entropy-coded data, the counts its first pass found (UsTile)
+  int64_t off_tiles;
+  int32_t ntiles, pad5;
+};
+
+// One tile of k_unstuff's first pass: bytes it emits and split markers (RSTn, codes below SOF0) it
+// holds before the tile's end, where its data ends (first other marker or the end of the input; -1:
+// not in this tile) and that marker's code (-1: the end of the input).
+struct UsTile {
+  int32_t emit, split, end, code;
 };
 
 // Entropy decoder state of one subsequence (Weissenberger & Schmidt style self-synchronisation).
@@ -233,6 +245,7 @@ enum Route : int32_t {
   kRtEnt11M,                      // LB = 11 images decoded by several workgroups (ent_groups > 1)
   kRtProg,                        // progressive images (k_prog)
   kRtEnt11G,                      // (count only) (image, group) tasks of the kRtEnt11M images: group_tasks()
+  kRtUsSmall, kRtUsBig,           // unstuffing: k_us_serial / the tile-parallel passes (kUsSerialTiles)
   kNumRoutes
 };
 constexpr int kRouteSlots = 32;  // counts [0, kNumRoutes), the rest zero

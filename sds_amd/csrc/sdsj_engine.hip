@@ -204,7 +204,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   const int cap = e->max_batch;
   SDSJ_HIP(e, launch_plan(n, ln.descs, e->capacity, ln.base, ln.total, ln.routes, cap, s));
   mark(2);
-  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, s));
+  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, ln.routes, cap, s));
   SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, ln.descs, e->scratch, s));
   mark(3);
   // (after mark 3: the next lane may start while this lane's progressive images decode)
@@ -768,6 +768,7 @@ int sdsj_resize_frames_device(sdsj_engine* e, int n, const uint8_t* d_frames, in
       const int64_t o = need * k;
       d.off_ustream += o;
       d.off_seg += o;
+      d.off_tiles += o;
       d.off_sub += o;
       d.off_rec += o;
       d.off_ptab += o;

@@ -11,6 +11,7 @@ hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, cons
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* base, int64_t* total, int32_t* routes,
                        int cap, hipStream_t s);
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
+                          const int32_t* routes, int cap,
                           hipStream_t s);
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);

@@ -155,6 +155,8 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
   d->off_ustream = take(prog ? 32 : d->entropy_len + kUPad + 32);  // + the 16-byte granule of the final pad store
   d->ustream_cap = prog ? 0 : d->entropy_len + kUPad;
   d->off_seg = take(seg_bytes(d->nseg));
+  d->ntiles = prog ? 0 : (int32_t)((d->entropy_len + kUsTileBytes - 1) / kUsTileBytes);
+  d->off_tiles = take((int64_t)d->ntiles * sizeof(UsTile));
   d->off_sub = take((int64_t)d->nsub_cap * sizeof(SubState));
   d->off_rec = take((int64_t)d->nsub_cap * kRec * sizeof(SyncRec));
   d->off_ptab = take(prog ? (int64_t)sizeof(ProgTables) : 0);
@@ -296,6 +298,7 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
       } else {
         d.off_ustream += start;
         d.off_seg += start;
+        d.off_tiles += start;
         d.off_sub += start;
         d.off_rec += start;
         d.off_ptab += start;
@@ -315,6 +318,10 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
             for (int q = 0; q < ns; q++) seen |= keys[q] == key;
             if (!seen) keys[ns++] = key;
           }
+        if (!d.progressive) {  // unstuffing: one workgroup per small image, tile-parallel passes for the rest
+          const int ru = d.ntiles > kUsSerialTiles ? kRtUsBig : kRtUsSmall;
+          routes[kRouteSlots + ru * cap + atomicAdd(&rcnt[ru], 1)] = i;
+        }
         const int re = d.progressive ? kRtProg : ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
         int32_t* lst = routes + kRouteSlots + re * cap;
         lst[atomicAdd(&rcnt[re], 1)] = i;
@@ -379,15 +386,24 @@ __global__ void __launch_bounds__(256) k_finish(int n, const ImgDesc* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// k_unstuff: one 256-thread workgroup per image.  Removes FF00 stuffing and fill bytes, splits at
-// RSTn markers and stops at the first other marker (jdhuff.c jpeg_fill_bit_buffer semantics).
-// Tiles of 8 KiB: each thread classifies 32 consecutive bytes (read as realigned dwords), one
-// packed (emitted, RSTn) scan places them, the tile is assembled in LDS and leaves as aligned
-// 16-byte stores (the unaligned tail rides into the next tile).
+// Unstuffing: removes FF00 stuffing and fill bytes, splits at RSTn markers and stops at the first
+// other marker (jdhuff.c jpeg_fill_bit_buffer semantics).  The entropy-coded data is cut into 8 KiB
+// tiles; each thread classifies 32 consecutive bytes (read as realigned dwords).  Three passes over
+// the tiles of all images at once:
+//   k_us_count  per tile: bytes emitted and split markers before the tile's end marker
+//   k_us_scan   per image: exclusive prefixes over its tiles, the tile the scan ends in, lengths
+//   k_us_write  per tile: one packed (emitted, split) scan places the bytes, the tile is assembled
+//               in LDS and leaves as aligned 16-byte stores (byte stores for the two boundary chunks
+//               it shares with its neighbours)
 // ------------------------------------------------------------------------------------------
 constexpr int kUnstuffThreads = 256;
 constexpr int kUsBytes = 32;
 constexpr int kUsTile = kUnstuffThreads * kUsBytes;
+static_assert(kUsTile == kUsTileBytes, "tile table granularity");
+constexpr int kUsGrid = 16;  // virtual workgroups per kRtUsBig image in k_us_count / k_us_write
+constexpr int kUsLaunch = 1024;  // workgroups of the route-striding unstuff kernels
+constexpr int kUsNone = 0x7fffffff;
+constexpr int kUsSkip = 2, kUsFinal = 1;  // UsTile.code after k_us_scan
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
   const int lane = threadIdx.x & 63;
@@ -515,177 +531,399 @@ __device__ void finish_scan(ImgDesc* d, const SegView sv, const uint8_t* raw, in
   if (status != SDSJ_OK) d->status = status;
 }
 
-__global__ void __launch_bounds__(kUnstuffThreads) k_unstuff(int n, const uint8_t* __restrict__ blob,
-                                                             const int64_t* __restrict__ offsets,
-                                                             ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch) {
-  const int img = blockIdx.x;
-  if (img >= n) return;
-  ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK || d->progressive) return;  // progressive: k_prog reads the raw stream
-  __shared__ alignas(16) uint8_t buf[kUsTile + 32];  // [carried tail][this tile's output]
-  __shared__ int wsum[kUnstuffThreads / 64];
-  __shared__ int s_end, s_end_code, s_overflow;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint8_t* raw = blob + offsets[img];
-  const uint8_t* e = raw + d->entropy_off;
-  const int64_t L = d->entropy_len;
-  const uintptr_t e_end = (uintptr_t)(e + L);  // dwords starting below this lie in mapped pages
-  uint8_t* out = scratch + d->off_ustream;  // 256-byte aligned
-  const int nseg = d->nseg;
-  const SegView sv = seg_view(scratch + d->off_seg, nseg);
-  if (t == 0) {
-    s_overflow = 0;
-    s_end_code = -1;
+// Bytes [my0, my0 + 32) of the entropy-coded data classified as bit masks (bit k = byte k): FF bytes
+// are skipped (fill / stuffing prefix); a byte after FF is a stuffed zero (emitted as 0xFF) or a
+// marker code; markers split the data (RSTn, and codes below SOF0: the restart logic decides) or end
+// it (any other marker, or the end of the input).  u[1..8] hold the 32 bytes, u[0] the 4 before
+// (entropy_off >= 4, so they are header bytes of the same image).
+struct UsClass {
+  uint32_t u[9];
+  uint32_t emit, stuffed, split, endm, vmask;
+};
+__device__ __forceinline__ int us_byte(const UsClass& c, int k) {
+  uint32_t dw = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) dw = q == (k >> 2) ? c.u[1 + q] : dw;
+  return (int)(dw >> (8 * (k & 3))) & 0xFF;
+}
+// The ten dwords holding bytes [my0 - 4, my0 + 32), all loads issued together.  A dword past the
+// input reads the last one (same page): bytes past the input are never emitted (us_classify's vmask),
+// so their values do not matter.  The 4 bytes before the entropy-coded data are header bytes.
+struct UsRaw {
+  uint32_t v[10];
+};
+__device__ __forceinline__ void us_load(const uint8_t* e, int64_t L, int64_t my0, UsRaw& r) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(((uintptr_t)(e + my0) & ~(uintptr_t)3) - 4);
+  const uint32_t* last = reinterpret_cast<const uint32_t*>(((uintptr_t)(e + L) - 1) & ~(uintptr_t)3);
+#pragma unroll
+  for (int k = 0; k < 10; k++) r.v[k] = *(w + k < last ? w + k : last);
+}
+__device__ __forceinline__ void us_classify(const uint8_t* e, int64_t L, int64_t my0, const UsRaw& r, UsClass& c) {
+  const int sh = (int)((uintptr_t)(e + my0) & 3);
+#pragma unroll
+  for (int k = 0; k < 9; k++) c.u[k] = (uint32_t)((((uint64_t)r.v[k + 1] << 32) | r.v[k]) >> (8 * sh));
+  // per byte (SWAR, bit 7 of each byte lane): zero, 0xFF, and "a marker code that splits the data"
+  // (RSTn, or below SOF0), then packed to bit masks (bit k = byte k)
+  auto pack = [](uint32_t m) { return ((m >> 7) & 1) | ((m >> 14) & 2) | ((m >> 21) & 4) | ((m >> 28) & 8); };
+  auto zbytes = [](uint32_t x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u; };
+  uint32_t isff = 0, isz = 0, issp = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t x = c.u[1 + q];
+    const uint32_t ge_c0 = x & (x << 1) & 0x80808080u;               // top two bits set
+    const uint32_t rst = zbytes((x ^ 0xD0D0D0D0u) & 0xF8F8F8F8u);    // 0xD0..0xD7
+    isz |= pack(zbytes(x)) << (4 * q);
+    isff |= pack(zbytes(~x)) << (4 * q);
+    issp |= pack((~ge_c0 & 0x80808080u) | rst) << (4 * q);
   }
+  const uint32_t prevff = (isff << 1) | ((my0 > 0 && (c.u[0] >> 24) == 0xFF) ? 1u : 0u);
+  const int64_t nvalid = L - my0;
+  c.vmask = nvalid >= kUsBytes ? 0xFFFFFFFFu : (nvalid <= 0 ? 0u : ((1u << nvalid) - 1u));
+  const uint32_t marker = prevff & ~isz & ~isff & c.vmask;
+  c.stuffed = prevff & isz;
+  c.emit = ~isff & ~marker & c.vmask;
+  c.split = marker & issp;
+  c.endm = (marker & ~issp) | ~c.vmask;  // the first byte past the input ends the data as well
+}
 
-  int64_t out_pos = 0;  // bytes emitted so far; [out_pos & ~15, out_pos) sit in buf[0, carry)
-  int nmk = 0;          // split markers (RSTn, and codes below SOF0) met so far
-  int64_t end_raw = -1; // entropy-relative index of the last FF of the terminating marker
-  bool ended = false;
-  for (int64_t base = 0; base < L && !ended; base += kUsTile) {
-    if (t == 0) s_end = 0x7fffffff;
-    // bytes [my0 - 4, my0 + 32) as 9 realigned dwords u[0..8] (u[0] holds the 4 preceding bytes;
-    // entropy_off >= 4, so they are header bytes of the same image)
-    const int64_t my0 = base + (int64_t)t * kUsBytes;
-    const uintptr_t a = (uintptr_t)(e + my0);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>((a & ~(uintptr_t)3) - 4);
-    const int sh = (int)(a & 3);
-    uint32_t v[10];
+// Tile end: the first ending byte of the tile (kUsNone: none), from every thread's classification
+// (one barrier; wmin is free again after the caller's next barrier).
+__device__ __forceinline__ int us_my_end(const UsClass& c, int t) {
+  return c.endm ? t * kUsBytes + __builtin_ctz(c.endm) : kUsNone;
+}
+__device__ __forceinline__ int us_tile_end(int my_end, int t, int* wmin) {
+  int m = my_end;
 #pragma unroll
-    for (int k = 0; k < 10; k++) v[k] = (uintptr_t)(w + k) < e_end ? w[k] : 0u;
-    uint32_t u[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) u[k] = (uint32_t)((((uint64_t)v[k + 1] << 32) | v[k]) >> (8 * sh));
-    // classify the 32 bytes as bit masks (bit k = byte k): FF bytes are skipped (fill / stuffing
-    // prefix); a byte after FF is a stuffed zero (emitted as 0xFF) or a marker code; markers split
-    // the data (RSTn, and codes below SOF0: the restart logic decides) or end it (any other marker,
-    // or the end of the input)
-    uint32_t isff = 0, isz = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint32_t x = u[1 + q], y = ~x;
-      const uint32_t zz = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // zero bytes
-      const uint32_t zf = ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;  // 0xFF bytes
-      isz |= (((zz >> 7) & 1) | ((zz >> 14) & 2) | ((zz >> 21) & 4) | ((zz >> 28) & 8)) << (4 * q);
-      isff |= (((zf >> 7) & 1) | ((zf >> 14) & 2) | ((zf >> 21) & 4) | ((zf >> 28) & 8)) << (4 * q);
-    }
-    const uint32_t prevff = (isff << 1) | ((my0 > 0 && (u[0] >> 24) == 0xFF) ? 1u : 0u);
-    const int64_t nvalid = L - my0;
-    const uint32_t vmask = nvalid >= kUsBytes ? 0xFFFFFFFFu : (nvalid <= 0 ? 0u : ((1u << nvalid) - 1u));
-    const uint32_t marker = prevff & ~isz & ~isff & vmask;
-    const uint32_t stuffed = prevff & isz;
-    const uint32_t emit = ~isff & ~marker & vmask;
-    uint32_t split = 0, endm = ~vmask;  // the first byte past the input ends it as well
-    for (uint32_t mk = marker; mk;) {   // rare: one iteration per marker
-      const int k = __builtin_ctz(mk);
-      mk &= mk - 1;
-      uint32_t dw = 0;
-#pragma unroll
-      for (int q = 0; q < 8; q++) dw = q == (k >> 2) ? u[1 + q] : dw;
-      const int c = (int)(dw >> (8 * (k & 3))) & 0xFF;
-      if ((c >= 0xD0 && c <= 0xD7) || c < 0xC0) split |= 1u << k;
-      else endm |= 1u << k;
-    }
-    const int my_end = endm ? __builtin_ctz(endm) : kUsBytes;
-    __syncthreads();  // s_end initialised; buf tail of the previous tile settled
-    if (my_end < kUsBytes) atomicMin(&s_end, t * kUsBytes + my_end);
-    __syncthreads();
-    const int tile_end = s_end;
-    if (my_end < kUsBytes && tile_end == t * kUsBytes + my_end) {  // the earliest end: its marker code
-      uint32_t dw = 0;
-#pragma unroll
-      for (int q = 0; q < 8; q++) dw = q == (my_end >> 2) ? u[1 + q] : dw;
-      s_end_code = ((vmask >> my_end) & 1) ? (int)(dw >> (8 * (my_end & 3))) & 0xFF : -1;
-    }
-    int lim = tile_end - t * kUsBytes;
-    lim = lim < 0 ? 0 : (lim > kUsBytes ? kUsBytes : lim);
-    const uint32_t below = lim >= kUsBytes ? 0xFFFFFFFFu : ((1u << lim) - 1u);
-    const uint32_t em = emit & below, sp = split & below;
-    const int packed = __popc(em) | (__popc(sp) << 16);
-    const int incl = wave_incl_scan(packed);
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    int before = 0, total = 0;
-#pragma unroll
-    for (int q = 0; q < kUnstuffThreads / 64; q++) {
-      before += q < wv ? wsum[q] : 0;
-      total += wsum[q];
-    }
-    const int excl = before + incl - packed;
-    const int carry = (int)(out_pos & 15);
-    int pos = excl & 0xFFFF;
-#pragma unroll
-    for (int k = 0; k < kUsBytes; k++) {
-      // an emitted byte is itself, or 0xFF for the stuffed 0x00 of an FF00 pair
-      const uint32_t rawb = (u[1 + (k >> 2)] >> (8 * (k & 3))) & 0xFF;
-      if ((em >> k) & 1) buf[carry + pos++] = (uint8_t)(((stuffed >> k) & 1) ? 0xFF : rawb);
-    }
-    int r = nmk + (excl >> 16);
-    for (uint32_t mk = sp; mk; r++) {  // rare: the split markers, in order
-      const int k = __builtin_ctz(mk);
-      mk &= mk - 1;
-      uint32_t dw = 0;
-#pragma unroll
-      for (int q = 0; q < 8; q++) dw = q == (k >> 2) ? u[1 + q] : dw;
-      if (r < sv.cap) {
-        sv.mk_out[r] = (int32_t)(out_pos + (excl & 0xFFFF) + __popc(em & ((1u << k) - 1u)));
-        sv.mk_raw[r] = (int32_t)(my0 + k - 1);
-        sv.mk_code[r] = (int32_t)(dw >> (8 * (k & 3))) & 0xFF;
-      } else {
-        s_overflow = 1;
-      }
-    }
-    __syncthreads();
-    const int temit = total & 0xFFFF;
-    // full 16-byte chunks of [out_pos & ~15, out_pos + temit) leave; the tail is carried
-    const int have = carry + temit, full = have >> 4;
-    uint4* dst = reinterpret_cast<uint4*>(out + (out_pos & ~(int64_t)15));
-    const uint4* src = reinterpret_cast<const uint4*>(buf);
-    for (int i = t; i < full; i += kUnstuffThreads) dst[i] = src[i];
-    const int rem = have & 15;
-    uint8_t tail = t < rem ? buf[full * 16 + t] : 0;
-    __syncthreads();
-    if (t < rem) buf[t] = tail;
-    out_pos += temit;
-    nmk += total >> 16;
-    if (tile_end != 0x7fffffff) {
-      ended = true;
-      end_raw = base + tile_end - 1;
-    }
-  }
+  for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o, 64));
+  if ((t & 63) == 0) wmin[t >> 6] = m;
   __syncthreads();
-  // the carried tail, then zero padding so the bit reader can over-read safely
-  {
-    const int rem = (int)(out_pos & 15);
-    const int64_t a0 = out_pos & ~(int64_t)15;
-    const int nchunks = (rem + kUPad + 15) >> 4;
-    for (int i = t; i < nchunks; i += kUnstuffThreads) {
-      uint32_t wds[4];
+  int r = wmin[0];
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        uint32_t x = 0;
+  for (int q = 1; q < kUnstuffThreads / 64; q++) r = min(r, wmin[q]);
+  return r;
+}
+// The ending marker's code (-1: the end of the input), from the thread that holds it.
+__device__ __forceinline__ int us_end_code(const UsClass& c, int t, int tile_end) {
+  const int k = tile_end - t * kUsBytes;
+  return ((c.vmask >> k) & 1) ? us_byte(c, k) : -1;
+}
+
+__device__ __forceinline__ uint32_t us_below(int tile_end, int t) {
+  int lim = tile_end - t * kUsBytes;
+  lim = lim < 0 ? 0 : (lim > kUsBytes ? kUsBytes : lim);
+  return lim >= kUsBytes ? 0xFFFFFFFFu : ((1u << lim) - 1u);
+}
+
+// Places one tile's bytes at output offset obase and its split markers from entry sbase: one packed
+// (emitted, split) scan, assembly in LDS, aligned 16-byte stores (byte stores for the boundary chunks
+// shared with the neighbouring tiles).  The final tile is followed by kUPad zero bytes (the bit reader
+// over-reads) to a 16-byte end.  Returns the tile's packed total.  Block-uniform call; buf and wsum are
+// free again after the caller's next barrier.
+// buf: [16 + kUsTile + kUPad + 16] bytes; the last 16 take the skipped bytes' stores
+__device__ int us_place(const UsClass& c, int64_t my0, int t, int tile_end, int64_t obase, int sbase, bool final,
+                        uint8_t* out, const SegView& sv, uint8_t* buf, int* wsum) {
+  const int lane = t & 63, wv = t >> 6;
+  const uint32_t below = us_below(tile_end, t);
+  const uint32_t em = c.emit & below, sp = c.split & below;
+  const int packed = __popc(em) | (__popc(sp) << 16);
+  const int incl = wave_incl_scan(packed);
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int before = 0, total = 0;
 #pragma unroll
-        for (int bb = 0; bb < 4; bb++) {
-          const int o = i * 16 + q * 4 + bb;
-          x |= (uint32_t)(o < rem ? buf[o] : 0) << (8 * bb);
-        }
-        wds[q] = x;
-      }
-      reinterpret_cast<uint4*>(out + a0)[i] = make_uint4(wds[0], wds[1], wds[2], wds[3]);
+  for (int q = 0; q < kUnstuffThreads / 64; q++) {
+    before += q < wv ? wsum[q] : 0;
+    total += wsum[q];
+  }
+  const int excl = before + incl - packed;
+  const int head = (int)(obase & 15);  // buf[i] is output byte (obase & ~15) + i
+  // an emitted byte is itself, or 0xFF for the stuffed 0x00 of an FF00 pair; every byte is stored
+  // (branch-free), the skipped ones to a dummy slot past the tile
+  constexpr int kDummy = 16 + kUsTile + kUPad;
+  int pos = head + (excl & 0xFFFF);
+#pragma unroll
+  for (int q = 0; q < kUsBytes / 4; q++) {
+    const uint32_t sm = (c.stuffed >> (4 * q)) & 0xF;
+    const uint32_t wq = c.u[1 + q] | (((sm * 0x00204081u) & 0x01010101u) * 0xFFu);
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int k = 4 * q + b;
+      const int bit = (int)((em >> k) & 1);
+      buf[bit ? pos : kDummy] = (uint8_t)(wq >> (8 * b));
+      pos += bit;
     }
   }
+  int m = sbase + (excl >> 16);
+  for (uint32_t mk = sp; mk; m++) {  // rare: the split markers, in order
+    const int k = __builtin_ctz(mk);
+    mk &= mk - 1;
+    if (m < sv.cap) {  // (the image is marked corrupt otherwise)
+      sv.mk_out[m] = (int32_t)(obase + (excl & 0xFFFF) + __popc(em & ((1u << k) - 1u)));
+      sv.mk_raw[m] = (int32_t)(my0 + k - 1);
+      sv.mk_code[m] = us_byte(c, k);
+    }
+  }
+  const int len = head + (total & 0xFFFF);
+  const int stop = final ? ((len + kUPad + 15) & ~15) : len;
+  for (int i = len + t; i < stop; i += kUnstuffThreads) buf[i] = 0;
+  __syncthreads();
+  uint8_t* dst = out + (obase & ~(int64_t)15);
+  const int first_full = (head + 15) >> 4, end_full = stop >> 4;
+  for (int i = first_full + t; i < end_full; i += kUnstuffThreads)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(buf)[i];
+  if (end_full < first_full) {  // the tile's bytes lie inside one chunk
+    if (t >= head && t < stop) dst[t] = buf[t];
+  } else {
+    if (t < 16 && t >= head && first_full > 0) dst[t] = buf[t];              // chunk shared with the previous tile
+    if (t < (stop & 15)) dst[end_full * 16 + t] = buf[end_full * 16 + t];  // chunk shared with the next tile
+  }
+  return total;
+}
+
+// The scan's bookkeeping once its length is known: split-marker overflow, restart-interval ends; the
+// padding of an empty scan.
+__device__ void us_finish(ImgDesc* d, const SegView& sv, int t, int64_t ulen, int nsplit, int end_code,
+                          int64_t end_raw, uint8_t* out) {
+  if (t == 0) {
+    d->ulen = ulen;
+    d->useg_found = 1 + nsplit;
+    d->scan_end_code = end_code;
+    d->scan_end_raw = end_raw;
+    if (nsplit > sv.cap) d->status = SDSJ_CORRUPT;  // more split markers than slots
+  }
+  if (d->ntiles == 0)  // no entropy-coded data: an empty stream and its padding
+    for (int i = t; i < (kUPad >> 4); i += kUnstuffThreads) reinterpret_cast<uint4*>(out)[i] = make_uint4(0, 0, 0, 0);
+  const int nseg = d->nseg;
   const int64_t bps = d->restart_interval ? (int64_t)d->restart_interval * d->bpm : d->total_blocks;
   for (int k = t; k < nseg; k += kUnstuffThreads) {
     const int64_t ge = (int64_t)(k + 1) * bps;
     sv.vend[k] = (int32_t)(ge < d->total_blocks ? ge : d->total_blocks);
   }
-  __syncthreads();
-  if (t == 0) {
-    d->ulen = out_pos;
-    d->useg_found = 1 + nmk;
-    d->scan_end_code = ended ? s_end_code : -1;
-    d->scan_end_raw = end_raw;
-    if (s_overflow) d->status = SDSJ_CORRUPT;
+}
+
+// Images of at most kUsSerialTiles tiles (route kRtUsSmall): one workgroup per image, tile after tile.
+__global__ void __launch_bounds__(kUnstuffThreads) k_us_serial(const uint8_t* __restrict__ blob,
+                                                               const int64_t* __restrict__ offsets,
+                                                               ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                                               const int32_t* __restrict__ routes, int cap) {
+  __shared__ alignas(16) uint8_t buf[16 + kUsTile + kUPad + 16];
+  __shared__ int wsum[kUnstuffThreads / 64];
+  __shared__ int wmin[kUnstuffThreads / 64];
+  __shared__ int s_code;
+  const int t = threadIdx.x;
+  const int cnt = routes[kRtUsSmall];
+  const int32_t* lst = route_list(routes, cap, kRtUsSmall);
+  for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+    const int img = lst[q];
+    ImgDesc* d = &descs[img];
+    const uint8_t* e = blob + offsets[img] + d->entropy_off;
+    const int64_t L = d->entropy_len;
+    const int ntiles = d->ntiles;
+    uint8_t* out = scratch + d->off_ustream;  // 256-byte aligned
+    const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+    int64_t obase = 0, end_raw = -1;
+    int nsplit = 0, end_code = -1;
+    UsRaw raw;
+    if (ntiles > 0) us_load(e, L, t * kUsBytes, raw);
+#ifdef SDSJ_US_PROF
+    int64_t ph[4] = {0, 0, 0, 0};
+#endif
+    for (int j = 0; j < ntiles; j++) {
+#ifdef SDSJ_US_PROF
+      const int64_t c0 = clock64();
+#endif
+      const int64_t my0 = (int64_t)j * kUsTile + t * kUsBytes;
+      UsClass c;
+      us_classify(e, L, my0, raw, c);
+      if (j + 1 < ntiles) us_load(e, L, my0 + kUsTile, raw);  // the next tile's loads fly meanwhile
+#ifdef SDSJ_US_PROF
+      const int64_t c1 = clock64();
+#endif
+      const int my_end = us_my_end(c, t);
+      const int tile_end = us_tile_end(my_end, t, wmin);
+      const bool ends = tile_end != kUsNone;
+      if (ends && my_end == tile_end) s_code = us_end_code(c, t, tile_end);
+#ifdef SDSJ_US_PROF
+      const int64_t c2 = clock64();
+#endif
+      const int tot = us_place(c, my0, t, tile_end, obase, nsplit, ends || j == ntiles - 1, out, sv, buf, wsum);
+#ifdef SDSJ_US_PROF
+      const int64_t c3 = clock64();
+      ph[0] += c1 - c0;
+      ph[1] += c2 - c1;
+      ph[2] += c3 - c2;
+      ph[3] += 1;
+#endif
+      obase += tot & 0xFFFF;
+      nsplit += tot >> 16;
+      if (ends) {
+        end_code = s_code;  // (written before us_place's barriers)
+        end_raw = (int64_t)j * kUsTile + tile_end - 1;
+        break;
+      }
+    }
+    us_finish(d, sv, t, obase, nsplit, end_code, end_raw, out);
+#ifdef SDSJ_US_PROF
+    if (t == 0)
+      for (int k = 0; k < 4; k++) d->t_rs[k] = ph[k];
+#endif
+  }
+}
+
+// Larger images (route kRtUsBig): kUsGrid virtual workgroups per image stride over its tiles.
+// Pass 1 -- per tile: bytes emitted and split markers before the tile's end, the end and its code.
+__global__ void __launch_bounds__(kUnstuffThreads) k_us_count(const uint8_t* __restrict__ blob,
+                                                              const int64_t* __restrict__ offsets,
+                                                              ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                                              const int32_t* __restrict__ routes, int cap) {
+  __shared__ int wsum[kUnstuffThreads / 64];
+  __shared__ int wmin[kUnstuffThreads / 64];
+  __shared__ int s_code;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int cnt = routes[kRtUsBig];
+  const int32_t* lst = route_list(routes, cap, kRtUsBig);
+  for (int v = blockIdx.x; v < cnt * kUsGrid; v += gridDim.x) {
+    const int img = lst[v / kUsGrid];
+    const ImgDesc* d = &descs[img];
+    const int ntiles = d->ntiles;
+    const uint8_t* e = blob + offsets[img] + d->entropy_off;
+    const int64_t L = d->entropy_len;
+    UsTile* tiles = reinterpret_cast<UsTile*>(scratch + d->off_tiles);
+    for (int j = v % kUsGrid; j < ntiles; j += kUsGrid) {
+      const int64_t my0 = (int64_t)j * kUsTile + t * kUsBytes;
+      UsRaw raw;
+      UsClass c;
+      us_load(e, L, my0, raw);
+      us_classify(e, L, my0, raw, c);
+      const int my_end = us_my_end(c, t);
+      const int tile_end = us_tile_end(my_end, t, wmin);
+      if (tile_end != kUsNone && my_end == tile_end) s_code = us_end_code(c, t, tile_end);
+      const uint32_t below = us_below(tile_end, t);
+      int packed = __popc(c.emit & below) | (__popc(c.split & below) << 16);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) packed += __shfl_xor(packed, o, 64);
+      if (lane == 0) wsum[wv] = packed;
+      __syncthreads();
+      if (t == 0) {
+        int tot = 0;
+#pragma unroll
+        for (int q = 0; q < kUnstuffThreads / 64; q++) tot += wsum[q];
+        UsTile r;
+        r.emit = tot & 0xFFFF;
+        r.split = tot >> 16;
+        r.end = tile_end == kUsNone ? -1 : tile_end;
+        r.code = tile_end == kUsNone ? -1 : s_code;
+        tiles[j] = r;
+      }
+      __syncthreads();  // wsum, wmin and s_code read
+    }
+  }
+}
+
+// Pass 2 -- one workgroup per image: tile records -> {bytes before, split markers before, end,
+// kUsFinal / kUsSkip / 0}; the scan's length, split count and end marker.
+__global__ void __launch_bounds__(kUnstuffThreads) k_us_scan(ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                                             const int32_t* __restrict__ routes, int cap) {
+  __shared__ int wsum[3][kUnstuffThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int cnt = routes[kRtUsBig];
+  const int32_t* lst = route_list(routes, cap, kRtUsBig);
+  for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+    ImgDesc* d = &descs[lst[q]];
+    const int ntiles = d->ntiles;
+    const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+    UsTile* tiles = reinterpret_cast<UsTile*>(scratch + d->off_tiles);
+    int ebase = 0, sbase = 0, ended = 0;  // totals over the chunks before this one
+    int64_t ulen = 0, end_raw = -1;
+    int nsplit = 0, end_code = -1;
+    for (int j0 = 0; j0 < ntiles; j0 += kUnstuffThreads) {
+      const int j = j0 + t;
+      const UsTile r = j < ntiles ? tiles[j] : UsTile{0, 0, -1, -1};
+      const int hasend = r.end >= 0 ? 1 : 0;
+      const int ie = wave_incl_scan(r.emit), is = wave_incl_scan(r.split), ih = wave_incl_scan(hasend);
+      if (lane == 63) {
+        wsum[0][wv] = ie;
+        wsum[1][wv] = is;
+        wsum[2][wv] = ih;
+      }
+      __syncthreads();
+      int be = 0, bs = 0, bh = 0, te = 0, ts = 0, th = 0;
+#pragma unroll
+      for (int w = 0; w < kUnstuffThreads / 64; w++) {
+        be += w < wv ? wsum[0][w] : 0;
+        bs += w < wv ? wsum[1][w] : 0;
+        bh += w < wv ? wsum[2][w] : 0;
+        te += wsum[0][w];
+        ts += wsum[1][w];
+        th += wsum[2][w];
+      }
+      const int ends_before = ended + bh + ih - hasend;
+      if (j < ntiles) {
+        UsTile o;
+        o.emit = ebase + be + ie - r.emit;
+        o.split = sbase + bs + is - r.split;
+        o.end = r.end >= 0 ? r.end : kUsNone;
+        const bool final = ends_before == 0 && (hasend || j == ntiles - 1);
+        o.code = ends_before > 0 ? kUsSkip : (final ? kUsFinal : 0);
+        tiles[j] = o;
+        if (final) {  // (one thread of the image)
+          ulen = o.emit + r.emit;
+          nsplit = o.split + r.split;
+          end_code = hasend ? r.code : -1;
+          end_raw = hasend ? (int64_t)j * kUsTile + r.end - 1 : -1;
+          d->ulen = ulen;
+          d->useg_found = 1 + nsplit;
+          d->scan_end_code = end_code;
+          d->scan_end_raw = end_raw;
+          if (nsplit > sv.cap) d->status = SDSJ_CORRUPT;  // more split markers than slots
+        }
+      }
+      ebase += te;
+      sbase += ts;
+      ended += th;
+      __syncthreads();  // wsum read
+    }
+    const int nseg = d->nseg;
+    const int64_t bps = d->restart_interval ? (int64_t)d->restart_interval * d->bpm : d->total_blocks;
+    for (int k = t; k < nseg; k += kUnstuffThreads) {
+      const int64_t ge = (int64_t)(k + 1) * bps;
+      sv.vend[k] = (int32_t)(ge < d->total_blocks ? ge : d->total_blocks);
+    }
+  }
+}
+
+// Pass 3 -- per tile: places the bytes and markers at the offsets pass 2 found.
+__global__ void __launch_bounds__(kUnstuffThreads) k_us_write(const uint8_t* __restrict__ blob,
+                                                              const int64_t* __restrict__ offsets,
+                                                              ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                                              const int32_t* __restrict__ routes, int cap) {
+  __shared__ alignas(16) uint8_t buf[16 + kUsTile + kUPad + 16];
+  __shared__ int wsum[kUnstuffThreads / 64];
+  const int t = threadIdx.x;
+  const int cnt = routes[kRtUsBig];
+  const int32_t* lst = route_list(routes, cap, kRtUsBig);
+  for (int v = blockIdx.x; v < cnt * kUsGrid; v += gridDim.x) {
+    const int img = lst[v / kUsGrid];
+    const ImgDesc* d = &descs[img];
+    if (d->status != SDSJ_OK) continue;  // (split-marker overflow found by pass 2)
+    const int ntiles = d->ntiles;
+    const uint8_t* e = blob + offsets[img] + d->entropy_off;
+    const int64_t L = d->entropy_len;
+    uint8_t* out = scratch + d->off_ustream;
+    const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+    const UsTile* tiles = reinterpret_cast<const UsTile*>(scratch + d->off_tiles);
+    for (int j = v % kUsGrid; j < ntiles; j += kUsGrid) {
+      const UsTile r = tiles[j];
+      if (r.code == kUsSkip) break;  // the scan ended in an earlier tile (so it did for the later ones)
+      const int64_t my0 = (int64_t)j * kUsTile + t * kUsBytes;
+      UsRaw raw;
+      UsClass c;
+      us_load(e, L, my0, raw);
+      us_classify(e, L, my0, raw, c);
+      us_place(c, my0, t, r.end, r.emit, r.split, r.code == kUsFinal, out, sv, buf, wsum);
+      if (r.code == kUsFinal) break;
+      __syncthreads();  // buf and wsum reused
+    }
   }
 }
 
@@ -1236,8 +1474,13 @@ hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* b
   return hipGetLastError();
 }
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
-                          hipStream_t s) {
-  hipLaunchKernelGGL(k_unstuff, dim3(n), dim3(kUnstuffThreads), 0, s, n, blob, offsets, descs, scratch);
+                          const int32_t* routes, int cap, hipStream_t s) {
+  const int g = n < kUsLaunch ? n : kUsLaunch;
+  const int gt = n * kUsGrid < 4 * kUsLaunch ? n * kUsGrid : 4 * kUsLaunch;
+  hipLaunchKernelGGL(k_us_serial, dim3(g), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
+  hipLaunchKernelGGL(k_us_count, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
+  hipLaunchKernelGGL(k_us_scan, dim3(g), dim3(kUnstuffThreads), 0, s, descs, scratch, routes, cap);
+  hipLaunchKernelGGL(k_us_write, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
   return hipGetLastError();
 }
 hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,

@@ -158,6 +158,27 @@ def test_4k_vs_oracle(engine):
     np.testing.assert_array_equal(got[0].cpu().numpy(), O.pipeline(jpg, (512, 512), flip=True))
 
 
+@pytest.mark.parametrize("rst", [0, 3])
+def test_tile_parallel_unstuff_vs_oracle(engine, rst):
+    """Images of more than kUsSerialTiles (64) 8 KiB tiles take the tile-parallel unstuff passes: noise
+    content (dense FF00 stuffing across tile boundaries), restart markers split across tiles, and a copy
+    truncated mid-scan."""
+    from tests.golden.synth import encode_jpeg
+    rng = np.random.default_rng(40 + rst)
+    rgb = rng.integers(0, 256, (1024, 1536, 3), dtype=np.uint8)
+    kw = {"restart_marker_blocks": rst} if rst else {}
+    jpg = encode_jpeg(rgb, 95, **kw)
+    assert len(jpg) > 64 * 8192 + 4096
+    cut = jpg[: len(jpg) * 2 // 3]
+    res = (200, 300)
+    got, st = engine.decode_resize([jpg, cut, jpg], res)
+    for k, j in enumerate([jpg, cut, jpg]):
+        ost, ref = _oracle_result(j, res)
+        assert int(st[k]) == ost, f"sample {k}: gpu {int(st[k])} vs oracle {ost}"
+        if ost == O.OK:
+            np.testing.assert_array_equal(got[k].cpu().numpy(), ref, err_msg=f"sample {k}")
+
+
 def _oracle_result(jpg, res):
     try:
         return O.OK, O.pipeline(jpg, res)
