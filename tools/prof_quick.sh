@@ -7,7 +7,7 @@ tag=$1
 shift
 rm -rf gpurun_out/pq_$tag
 SDSJ_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pq_$tag -o run -- \
-  python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline "$@" > gpurun_out/pq_$tag.log 2>&1
+  python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline "$@" > gpurun_out/pq_$tag.log 2>&1 || echo "bench exited with $? (stats still read)"
 python3 - gpurun_out/pq_$tag/run_kernel_stats.csv <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
