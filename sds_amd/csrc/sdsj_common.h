@@ -153,7 +153,8 @@ struct ImgDesc {
   int64_t off_ptab;
   // k_unstuff: per 8 KiB tile of the entropy-coded data, the counts its first pass found (UsTile)
   int64_t off_tiles;
-  int32_t ntiles, pad5;
+  int32_t ntiles;
+  int32_t rs_lay;  // chroma layout of the specialised fused kernel (RsLay) when rs_fast > 0
 };
 
 // One tile of k_unstuff's first pass: bytes it emits and split markers (RSTn, codes below SOF0) it
@@ -240,7 +241,8 @@ enum Route : int32_t {
   kRtGen0,         // k_resample<0>: any horizontal tap count (coefficients from the table)
   kRtGen1,         // k_resample<1>: no horizontal pass
   kRtGen3, kRtGen5, kRtGen7, kRtGen9, kRtGen11,  // k_resample<KT>
-  kRt3, kRt5, kRt7, kRt9, kRt11,  // k_rs420<KT>
+  kRtF,                           // k_rs420<KT, LAY>: 4 layouts x 5 tap counts from here (rs_route)
+  kRtFLast = kRtF + 19,
   kRtEnt10, kRtEnt11,             // entropy kernels by lookahead width
   kRtEnt11M,                      // LB = 11 images decoded by several workgroups (ent_groups > 1)
   kRtProg,                        // progressive images (k_prog)
@@ -248,14 +250,17 @@ enum Route : int32_t {
   kRtUsSmall, kRtUsBig,           // unstuffing: k_us_serial / the tile-parallel passes (kUsSerialTiles)
   kNumRoutes
 };
-constexpr int kRouteSlots = 32;  // counts [0, kNumRoutes), the rest zero
+constexpr int kRouteSlots = 48;  // counts [0, kNumRoutes), the rest zero
 static_assert(kNumRoutes <= kRouteSlots, "route counts must fit the count slots");
 SDSJ_HD inline const int32_t* route_list(const int32_t* routes, int cap, int r) { return routes + kRouteSlots + r * cap; }
 // After the lists: one entry (image << kGroupShift | group) per workgroup task of a multi-group image, so the
 // spec / write passes give every (image, group) its own workgroup (count in routes[kRtEnt11G]).
 SDSJ_HD inline int32_t* group_tasks(int32_t* routes, int cap) { return routes + kRouteSlots + (int64_t)kNumRoutes * cap; }
 SDSJ_HD inline int64_t route_ints(int cap) { return kRouteSlots + (int64_t)(kNumRoutes + kMaxEntGroups) * cap; }
-SDSJ_HD inline int rs_route(int kt) { return kRt3 + (kt - 3) / 2; }
+// chroma layouts of the specialised fused resample (sdsj_resample420.hip)
+enum RsLay : int32_t { kRs420 = 0, kRs422 = 1, kRs444 = 2, kRsGray = 3 };
+SDSJ_HD inline int rs_route(int lay, int kt) { return kRtF + lay * 5 + (kt - 3) / 2; }
+constexpr int kRsfEntries = 512;  // workgroup columns of a specialised-resample launch (they stride over its list)
 // generic fused resample route of an image whose horizontal pass has kt taps (1: none)
 SDSJ_HD inline int gen_route(int kt) {
   return kt == 1 ? kRtGen1 : (kt >= 3 && kt <= 11 && (kt & 1) ? kRtGen3 + (kt - 3) / 2 : kRtGen0);

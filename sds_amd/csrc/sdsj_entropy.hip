@@ -226,9 +226,6 @@ __device__ void load_sync_tables(SyncTables& T, const EntTables* g) {
 constexpr int kQ = 8;
 constexpr int kSpecGroup = 4;   // symbols decoded between two wave-uniform refill checks (spec pass)
 constexpr int kWriteGroup = 4;  // (write pass)
-#ifndef SDSJ_FLUSH_LANE
-#define SDSJ_FLUSH_LANE 0
-#endif
 static_assert(kSpecGroup < kQ && kWriteGroup < kQ, "a fresh refill must pass the group check");
 
 template <int Q>
@@ -947,21 +944,6 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           }
           run = g < gend && (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
         }
-#if SDSJ_FLUSH_LANE
-        // a completed block leaves from its own lane: 8 x 16-byte LDS reads, stores and clears
-        if (ready) {
-          uint4* sp = reinterpret_cast<uint4*>(L.stage + my_base);
-          uint4 v[8];
-#pragma unroll
-          for (int k = 0; k < 8; k++) v[k] = sp[k];
-          uint4* dst = reinterpret_cast<uint4*>(coef + (int64_t)gdone * 64);
-#pragma unroll
-          for (int k = 0; k < 8; k++) {
-            dst[k] = v[k];
-            sp[k] = make_uint4(0, 0, 0, 0);
-          }
-        }
-#else
         // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
         const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
         if (m) {
@@ -970,7 +952,8 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
             const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
             L.flist[wv][idx] = ((uint32_t)t << 24) | gdone;
           }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          // (a wave's LDS accesses execute in issue order: the reads below see these writes, and the
+          // owner's next stage writes land after the clears -- no waits beyond the data dependences)
           __builtin_amdgcn_wave_barrier();
           for (int b0 = 0; b0 < cnt; b0 += 8) {
             const int bi = b0 + (lane >> 3);
@@ -982,10 +965,8 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
               *sp = make_uint4(0, 0, 0, 0);
             }
           }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_wave_barrier();
         }
-#endif
        }
         if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kWriteGroup + 1)) ||
             !__builtin_amdgcn_ballot_w64(run))

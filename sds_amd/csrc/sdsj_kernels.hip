@@ -116,14 +116,25 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
     }
   }
   if (frames) d->fused = 0;
-  // specialised fused kernel: 4:2:0 (h2v2 fancy chroma), horizontal and vertical passes, odd tap
-  // counts 3..11 (sdsj_resample420.hip); everything else takes the generic k_resample
+  // specialised fused kernels (sdsj_resample420.hip): 4:2:0 (h2v2 fancy chroma), 4:2:2 (h2v1 fancy
+  // chroma), 4:4:4 and grayscale, horizontal and vertical passes, odd tap counts 3..11; everything
+  // else takes the generic k_resample
   d->rs_fast = 0;
-  if (d->fused && d->ncomp == 3 && d->need_h && d->need_v && d->ksh >= 3 && d->ksh <= 11 && (d->ksh & 1) &&
-      d->ring_rows <= kRingMaxRows && d->comp[0].rh == 1 && d->comp[0].rv == 1 && d->comp[1].rh == 2 &&
-      d->comp[1].rv == 2 && d->comp[2].rh == 2 && d->comp[2].rv == 2 && d->comp[1].dw > 2 &&
-      d->comp[2].dw == d->comp[1].dw && d->comp[2].dh == d->comp[1].dh)
-    d->rs_fast = d->ksh;
+  d->rs_lay = kRs420;
+  if (d->fused && d->need_h && d->need_v && d->ksh >= 3 && d->ksh <= 11 && (d->ksh & 1) &&
+      d->ring_rows <= kRingMaxRows && d->comp[0].rh == 1 && d->comp[0].rv == 1) {
+    const CompDesc &c1 = d->comp[1], &c2 = d->comp[2];
+    const bool same = d->ncomp == 3 && c2.rh == c1.rh && c2.rv == c1.rv && c2.dw == c1.dw && c2.dh == c1.dh;
+    int lay = -1;
+    if (d->ncomp == 1) lay = kRsGray;
+    else if (same && c1.rh == 1 && c1.rv == 1) lay = kRs444;
+    else if (same && c1.rh == 2 && c1.rv == 1 && c1.dw > 2) lay = kRs422;
+    else if (same && c1.rh == 2 && c1.rv == 2 && c1.dw > 2) lay = kRs420;
+    if (lay >= 0) {
+      d->rs_fast = d->ksh;
+      d->rs_lay = lay;
+    }
+  }
   {
     const int64_t bits = d->entropy_len * 8, per_group = (int64_t)kDecodeThreads * kGroupBits;
     int64_t g = (bits + per_group - 1) / per_group;
@@ -332,7 +343,7 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         }
         if (d.geo != kGeoZeros) {
           const int rr = !d.fused ? kRtUnfused
-                         : (d.rs_fast ? rs_route(d.rs_fast) : gen_route(d.need_h ? d.ksh : 1));
+                         : (d.rs_fast ? rs_route(d.rs_lay, d.rs_fast) : gen_route(d.need_h ? d.ksh : 1));
           lst = routes + kRouteSlots + rr * cap;
           lst[atomicAdd(&rcnt[rr], 1)] = i;
         }

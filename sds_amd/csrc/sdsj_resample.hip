@@ -401,8 +401,10 @@ __global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* _
                                                          const int32_t* __restrict__ routes, int cap,
                                                          const float* __restrict__ lut) {
   constexpr int r = KT == 0 ? kRtGen0 : (KT == 1 ? kRtGen1 : kRtGen3 + (KT - 3) / 2);
-  if ((int)blockIdx.x >= routes[r]) return;  // one workgroup column per list entry
-  resample_image<KT>(route_list(routes, cap, r)[blockIdx.x], descs, op, strip_h, scratch, flip, out, lut);
+  const int cnt = routes[r];
+  const int32_t* lst = route_list(routes, cap, r);
+  for (int e = blockIdx.x; e < cnt; e += gridDim.x)  // a small grid strides over the route's list
+    resample_image<KT>(lst[e], descs, op, strip_h, scratch, flip, out, lut);
 }
 
 hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
@@ -411,7 +413,7 @@ hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const
   const int strip_h = n >= 512 ? kMaxStrip : 16;
   const int tiles = (op.out_w + kRsThreads - 1) / kRsThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
-  const dim3 grid(n, strips, tiles);
+  const dim3 grid(n < kRsfEntries ? n : kRsfEntries, strips, tiles);
   hipLaunchKernelGGL(k_resample<0>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
   hipLaunchKernelGGL(k_resample<1>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
   hipLaunchKernelGGL(k_resample<3>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);

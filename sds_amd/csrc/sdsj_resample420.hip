@@ -1,14 +1,19 @@
-// sdsj_resample420.hip -- the fused colour + resample kernel specialised for the dominant case:
-// 4:2:0 YCbCr (h2v2 fancy chroma upsampling), a horizontal and a vertical Pillow pass, KT taps
-// (odd, 3..11).  Same arithmetic and the same streaming structure as k_resample
-// (sdsj_resample.hip, whose header describes the phases and the reference lines), with the
-// per-image geometry fixed at compile time where it matters:
-//   * conversion is one flattened loop over (step row, pixel pair); each item loads 12 chroma
-//     bytes + 2 luma bytes from the staged rows and writes each channel's pair as one u16;
+// sdsj_resample420.hip -- the fused colour + resample kernels specialised by chroma layout:
+// 4:2:0 YCbCr (h2v2 fancy chroma), 4:2:2 (h2v1 fancy chroma), 4:4:4 and grayscale, with a
+// horizontal and a vertical Pillow pass of KT taps (odd, 3..11).  Same arithmetic and the same
+// streaming structure as k_resample (sdsj_resample.hip, whose header describes the phases and the
+// reference lines), with the per-image geometry fixed at compile time where it matters:
+//   * the plane rows of the next step travel through registers (loads issued a whole step ahead);
+//   * conversion is one flattened loop over (step row, 8-pixel group); each item reads its luma and
+//     chroma as aligned dwords from the staged rows and writes each channel's 8 pixels as 2 dwords
+//     (grayscale has no conversion: the horizontal taps read the staged luma rows, and one channel
+//     goes through the H and V passes and is written to all three outputs -- Image.convert('RGB') of
+//     an 'L' image repeats it);
 //   * staging offsets of the step's rows come from a small LDS table, not from uniform registers
 //     (keeps the scalar file from spilling);
-//   * the horizontal taps are KT exactly, coefficients in registers.
-// plan_image sets ImgDesc::rs_fast = KT for the images this kernel takes; k_resample skips them.
+//   * the horizontal taps are KT exactly, coefficients in registers, windows read as aligned dwords.
+// plan_image sets ImgDesc::rs_fast = KT and rs_lay for the images these kernels take; k_resample
+// skips them.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,19 +31,29 @@
 namespace sdsj {
 
 constexpr int kFThreads = 256;
-constexpr int kFRows = 4;                               // source rows per step
-constexpr int kFYDW = kMaxSpan / 4 + 2;                 // staged luma row (dwords)
-constexpr int kFCDW = kMaxSpan / 8 + 3;                 // staged chroma row (dwords)
-constexpr int kFStageDW = kFRows * kFYDW + 2 * kFRows * kFCDW;
-constexpr int kFRgbW = kMaxSpan + 32;                   // RGB row pitch (bytes, even)
+constexpr int kFRows = 4;                // source rows per step
+constexpr int kFYDW = kMaxSpan / 4 + 2;  // staged luma (full-width) row (dwords)
+constexpr int kFCDW = kMaxSpan / 8 + 3;  // staged half-width chroma row (dwords)
+constexpr int kFRgbW = kMaxSpan + 32;    // RGB row pitch (bytes, even)
 
+// Per layout: staged chroma row width (dwords), staged rows (luma + both chroma planes), RGB rows.
+template <int LAY>
+struct FGeo {
+  static constexpr int kCDW = LAY == kRs444 ? kFYDW : (LAY == kRsGray ? 0 : kFCDW);
+  static constexpr int kCRows = LAY == kRsGray ? 0 : kFRows;  // staged rows per chroma plane (<= 4)
+  static constexpr int kStageDW = kFRows * kFYDW + 2 * kCRows * kCDW;
+  static constexpr int kRgbRows = LAY == kRsGray ? 0 : kFRows;
+  static constexpr int kRows = kFRows + 2 * kCRows;  // staged rows per step at most
+};
+
+template <int LAY>
 struct LdsF {
-  uint32_t st[kFStageDW];                 // step's plane rows: 4 luma rows, then 4 Cb, 4 Cr rows
-  uint8_t rgb[kFRows][3][kFRgbW];         // converted rows, planar, column x at x - xb (xb even)
-  uint32_t ring[kRingDW];                 // per column: horizontal results of the last R rows
-  int32_t vb[kMaxStrip][2];               // strip rows: vertical window (first row, row count)
-  int32_t vw[kMaxStrip][kVTaps];          // strip rows: vertical weights
-  int32_t rinfo[kFRows][8];               // step row q: byte offsets of its Y, Cb i/f, Cr i/f rows
+  uint32_t st[FGeo<LAY>::kStageDW];                          // step's plane rows: 4 luma, then Cb, Cr
+  uint8_t rgb[FGeo<LAY>::kRgbRows > 0 ? FGeo<LAY>::kRgbRows : 1][3][kFRgbW];  // converted rows, planar
+  uint32_t ring[kRingDW];                                    // per column: H results of the last R rows
+  int32_t vb[kMaxStrip][2];                                  // strip rows: vertical window (first, count)
+  int32_t vw[kMaxStrip][kVTaps];                             // strip rows: vertical weights
+  int32_t rinfo[kFRows][8];                                  // step row q: byte offsets of its staged rows
 };
 
 // Pillow horizontal pass of one channel at one output column: KT taps from the byte window that
@@ -59,34 +74,37 @@ __device__ __forceinline__ int htaps(const uint32_t* w, int hsh, const int32_t* 
   return rs_clip8(acc);
 }
 
-template <int KT>
-__device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
-                            const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
-                            void* __restrict__ out, const float* __restrict__ lut);
+template <int KT, int LAY>
+__device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
+                          const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
+                          void* __restrict__ out, const float* __restrict__ lut);
 
-template <int KT>
+// Route (LAY, KT): a small grid strides over the route's list (an empty route costs one short launch).
+template <int KT, int LAY>
 __global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                       int strip_h, const uint8_t* __restrict__ scratch,
                                                       const uint8_t* __restrict__ flip, void* __restrict__ out,
                                                       const int32_t* __restrict__ routes, int cap,
                                                       const float* __restrict__ lut) {
-  const int r = rs_route(KT);  // one workgroup column per list entry; the surplus exits at once
-  if ((int)blockIdx.x >= routes[r]) return;
-  rs420_image<KT>(route_list(routes, cap, r)[blockIdx.x], descs, op, strip_h, scratch, flip, out, lut);
+  const int r = rs_route(LAY, KT);
+  const int cnt = routes[r];
+  const int32_t* lst = route_list(routes, cap, r);
+  for (int e = blockIdx.x; e < cnt; e += gridDim.x) rsf_image<KT, LAY>(lst[e], descs, op, strip_h, scratch, flip, out, lut);
 }
 
-// One image's share (strip blockIdx.y, column tiles from blockIdx.z) of the 4:2:0 fused resample.
-template <int KT>
-__device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
-                            const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
-                            void* __restrict__ out, const float* __restrict__ lut) {
+// One image's share (strip blockIdx.y, column tiles from blockIdx.z) of the fused resample.
+template <int KT, int LAY>
+__device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
+                          const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
+                          void* __restrict__ out, const float* __restrict__ lut) {
+  using G = FGeo<LAY>;
   const ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK || d->rs_fast != KT) return;
+  if (d->status != SDSJ_OK || d->rs_fast != KT || d->rs_lay != LAY) return;
   const int oh = op.out_h, ow = op.out_w;
   const int oy0 = blockIdx.y * strip_h;
   if (oy0 >= oh) return;
   const int oy1 = oy0 + strip_h < oh ? oy0 + strip_h : oh;
-  __shared__ LdsF L;
+  __shared__ LdsF<LAY> L;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t plane = (int64_t)oh * ow;
   OutMap om;
@@ -101,11 +119,11 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
   const int32_t* kv = bv + 2 * oh;
   const int ksv = d->ksv, cx0 = d->cx0, cy0 = d->cy0, tw = d->tile_w;
   const int rmask = d->ring_rows - 1, rstride = kRingDW / d->ring_rows;
-  const int dwc = d->comp[1].dw, dhc = d->comp[1].dh;
+  const int dwc = LAY == kRsGray ? 0 : d->comp[1].dw, dhc = LAY == kRsGray ? 0 : d->comp[1].dh;
   const uint8_t* pY = scratch + d->off_planes + d->comp[0].plane_off;
-  const uint8_t* pCb = scratch + d->off_planes + d->comp[1].plane_off;
-  const uint8_t* pCr = scratch + d->off_planes + d->comp[2].plane_off;
-  const int pitchY = d->comp[0].pitch, pitchC = d->comp[1].pitch;
+  const uint8_t* pCb = LAY == kRsGray ? pY : scratch + d->off_planes + d->comp[1].plane_off;
+  const uint8_t* pCr = LAY == kRsGray ? pY : scratch + d->off_planes + d->comp[2].plane_off;
+  const int pitchY = d->comp[0].pitch, pitchC = LAY == kRsGray ? 0 : d->comp[1].pitch;
   const int ntiles = (ow + tw - 1) / tw;
   const int r_lo = bv[2 * oy0], r_hi = bv[2 * (oy1 - 1)] + bv[2 * (oy1 - 1) + 1];
   // the strip's vertical windows and weights
@@ -117,19 +135,20 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
     }
     L.vw[b][k] = k < ksv ? kv[(int64_t)oy * ksv + k] : 0;
   }
-  const uint8_t* stb = reinterpret_cast<const uint8_t*>(L.st);
 
   for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
     const int ox0 = tile * tw, ox1 = ox0 + tw < ow ? ox0 + tw : ow;
     const int s_lo = bh[2 * ox0], s_hi = bh[2 * (ox1 - 1)] + bh[2 * (ox1 - 1) + 1];
     const int ax0 = cx0 + s_lo, ax1 = cx0 + s_hi;  // image columns of the tile
-    const int jb = (ax0 >> 1) & ~3;                // first chroma column of the first 4-pair group
-    const int xb = 2 * jb;                         // rgb row origin (8-aligned: dword writes)
-    const int ng = (((ax1 - 1) >> 1) - jb) / 4 + 1;  // 4-pair groups covering [ax0, ax1)
-    // staged columns: luma [xb, xb + 8 ng), chroma [jb - 4, jb + 4 ng + 4).  Bytes past a row end
-    // (or before the first one) come from neighbouring scratch and only feed pixels outside the tile.
+    // 8-pixel groups: luma columns [xb, xb + 8 ng) with xb 8-aligned (dword writes); half-width
+    // chroma columns [jb - 4, jb + 4 ng + 4) (the fancy upsampling reads one neighbour each side),
+    // full-width chroma (4:4:4) columns [xb, xb + 8 ng).  Bytes past a row end (or before the first
+    // one) come from neighbouring scratch and only feed pixels outside the tile.
+    const int jb = (ax0 >> 1) & ~3;
+    const int xb = 2 * jb;
+    const int ng = (ax1 - 1 - xb) / 8 + 1;
     const int jalY = xb, ndY = 2 * ng;
-    const int jalC = jb - 4, ndC = ng + 2;
+    const int jalC = LAY == kRs444 ? xb : jb - 4, ndC = LAY == kRs444 ? 2 * ng : ng + 2;
     const int xx = ox0 + t;
     const bool active = xx < ox1;
     int hm = 0, hc = 0;
@@ -140,7 +159,8 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
     int32_t cf[KT];
 #pragma unroll
     for (int j = 0; j < KT; j++) cf[j] = active && j < hc ? kh[(int64_t)xx * KT + j] : 0;
-    const uint32_t* hw = reinterpret_cast<const uint32_t*>(&L.rgb[0][0][0]) + (hm >> 2);
+    // H windows: the converted RGB rows, or (grayscale) the staged luma rows themselves
+    const uint32_t* hw = LAY == kRsGray ? L.st + (hm >> 2) : reinterpret_cast<const uint32_t*>(&L.rgb[0][0][0]) + (hm >> 2);
     const int hsh = hm & 3;
     uint32_t* ring = L.ring + t;
     const int ox = fl ? ow - 1 - xx : xx;
@@ -154,9 +174,9 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
         tm = now;
       }
     };
-    // Plane rows of a step (4 source rows): luma rows ya.., chroma rows ilo..ihi -- the rows the
-    // h2v2 fancy upsampling reads (row i = y >> 1 and its neighbour f = i -/+ 1 for even/odd y),
-    // clamped to the plane: at most 4 chroma rows per plane.
+    // Plane rows of a step (4 source rows): luma rows ya..; chroma rows ilo..ilo + nrc - 1 -- for
+    // 4:2:0 the rows the h2v2 fancy upsampling reads (row i = y >> 1 and its neighbour f = i -/+ 1
+    // for even/odd y, clamped: at most 4 per plane), otherwise the luma rows' own.
     struct Step {
       int ra, nr, ya, ilo, nrc;
     };
@@ -165,17 +185,22 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
       p.ra = ra;
       p.nr = r_hi - ra < kFRows ? r_hi - ra : kFRows;
       p.ya = cy0 + ra;
-      int ilo = ((p.ya + 1) >> 1) - 1, ihi = (p.ya + p.nr) >> 1;
-      ilo = ilo < 0 ? 0 : ilo;
-      ihi = ihi > dhc - 1 ? dhc - 1 : ihi;
-      p.ilo = ilo;
-      p.nrc = ihi - ilo + 1;
+      if (LAY == kRs420) {
+        int ilo = ((p.ya + 1) >> 1) - 1, ihi = (p.ya + p.nr) >> 1;
+        ilo = ilo < 0 ? 0 : ilo;
+        ihi = ihi > dhc - 1 ? dhc - 1 : ihi;
+        p.ilo = ilo;
+        p.nrc = ihi - ilo + 1;
+      } else {
+        p.ilo = p.ya;
+        p.nrc = LAY == kRsGray ? 0 : p.nr;
+      }
       return p;
     };
     // The next step's rows travel through registers (global loads issued before this step's
     // conversion, written to LDS after its H/V work), so their latency hides behind a whole step.
     // Wave wv holds staged rows wv, wv + 4, wv + 8 (<= 12 rows), 64 dwords per load.
-    constexpr int kPR = 3, kPC = (kMaxSpan / 4 + 2 + 63) / 64;
+    constexpr int kPR = (G::kRows + 3) / 4, kPC = (kMaxSpan / 4 + 2 + 63) / 64;
     uint32_t pre[kPR][kPC];
     auto row_src = [&](const Step& p, int row, const uint8_t*& g, int& nd, int& o) {
       if (row < p.nr) {
@@ -185,11 +210,11 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
       } else if (row < p.nr + p.nrc) {
         g = pCb + (int64_t)(p.ilo + row - p.nr) * pitchC + jalC;
         nd = ndC;
-        o = kFRows * kFYDW + (row - p.nr) * kFCDW;
+        o = kFRows * kFYDW + (row - p.nr) * G::kCDW;
       } else {
         g = pCr + (int64_t)(p.ilo + row - p.nr - p.nrc) * pitchC + jalC;
         nd = ndC;
-        o = kFRows * kFYDW + kFRows * kFCDW + (row - p.nr - p.nrc) * kFCDW;
+        o = kFRows * kFYDW + G::kCRows * G::kCDW + (row - p.nr - p.nrc) * G::kCDW;
       }
     };
     auto issue = [&](const Step& p) {
@@ -220,15 +245,21 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
             if (64 * h + lane < nd) L.st[o + 64 * h + lane] = pre[i][h];
         }
       }
-      if (t < p.nr) {
-        const int y = p.ya + t, i = y >> 1;
-        int f = (y & 1) ? i + 1 : i - 1;
-        f = f < 0 ? 0 : (f > dhc - 1 ? dhc - 1 : f);
+      if (LAY != kRsGray && t < p.nr) {
+        const int y = p.ya + t;
+        int i = y - p.ilo, f = i;  // staged chroma row of this luma row, and its vertical neighbour
+        if (LAY == kRs420) {
+          const int ci = y >> 1;
+          int cfr = (y & 1) ? ci + 1 : ci - 1;
+          cfr = cfr < 0 ? 0 : (cfr > dhc - 1 ? dhc - 1 : cfr);
+          i = ci - p.ilo;
+          f = cfr - p.ilo;
+        }
         L.rinfo[t][0] = 4 * (t * kFYDW) - jalY;
-        L.rinfo[t][1] = 4 * (kFRows * kFYDW + (i - p.ilo) * kFCDW) - jalC;
-        L.rinfo[t][2] = 4 * (kFRows * kFYDW + (f - p.ilo) * kFCDW) - jalC;
-        L.rinfo[t][3] = 4 * (kFRows * kFYDW + kFRows * kFCDW + (i - p.ilo) * kFCDW) - jalC;
-        L.rinfo[t][4] = 4 * (kFRows * kFYDW + kFRows * kFCDW + (f - p.ilo) * kFCDW) - jalC;
+        L.rinfo[t][1] = 4 * (kFRows * kFYDW + i * G::kCDW) - jalC;
+        L.rinfo[t][2] = 4 * (kFRows * kFYDW + f * G::kCDW) - jalC;
+        L.rinfo[t][3] = 4 * (kFRows * kFYDW + G::kCRows * G::kCDW + i * G::kCDW) - jalC;
+        L.rinfo[t][4] = 4 * (kFRows * kFYDW + G::kCRows * G::kCDW + f * G::kCDW) - jalC;
       }
     };
     Step cur = plan_step(r_lo);
@@ -241,65 +272,100 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
       const Step nxt = more ? plan_step(ra + kFRows) : cur;
       if (more) issue(nxt);
       mark(0);
-      // B. h2v2 fancy upsampling + ycc->rgb on 4 pixel pairs (8 pixels) per item: chroma columns
-      // jg - 4 .. jg + 7 and luma x .. x + 7 come in as aligned dwords (jg = jb + 4g)
-      for (int it = t; it < nr * ng; it += kFThreads) {
-        const int q = (it >= ng) + (it >= 2 * ng) + (it >= 3 * ng), gi = it - q * ng;
-        const int jg = jb + 4 * gi, x = 2 * jg;
-        const int oY = L.rinfo[q][0], oBi = L.rinfo[q][1], oBf = L.rinfo[q][2], oRi = L.rinfo[q][3],
-                  oRf = L.rinfo[q][4];
-        // column sums 3 * row_i + row_f for columns jg - 1 .. jg + 4 (edges repeat column 0 / dwc - 1)
-        int cb[6], cr[6];
-        {
+      if (LAY != kRsGray) {
+        // B. fancy upsampling + ycc->rgb on 8 pixels per item
+        for (int it = t; it < nr * ng; it += kFThreads) {
+          const int q = (it >= ng) + (it >= 2 * ng) + (it >= 3 * ng), gi = it - q * ng;
+          const int x = xb + 8 * gi, jg = x >> 1;
+          const int oY = L.rinfo[q][0], oBi = L.rinfo[q][1], oRi = L.rinfo[q][3];
           const uint32_t* sw = L.st;
-          const uint32_t bi0 = sw[(oBi + jg - 4) >> 2], bi1 = sw[(oBi + jg) >> 2], bi2 = sw[(oBi + jg + 4) >> 2];
-          const uint32_t bf0 = sw[(oBf + jg - 4) >> 2], bf1 = sw[(oBf + jg) >> 2], bf2 = sw[(oBf + jg + 4) >> 2];
-          const uint32_t ri0 = sw[(oRi + jg - 4) >> 2], ri1 = sw[(oRi + jg) >> 2], ri2 = sw[(oRi + jg + 4) >> 2];
-          const uint32_t rf0 = sw[(oRf + jg - 4) >> 2], rf1 = sw[(oRf + jg) >> 2], rf2 = sw[(oRf + jg + 4) >> 2];
-          cb[0] = (int)(bi0 >> 24) * 3 + (int)(bf0 >> 24);
-          cr[0] = (int)(ri0 >> 24) * 3 + (int)(rf0 >> 24);
+          const uint32_t y0 = sw[(oY + x) >> 2], y1 = sw[(oY + x + 4) >> 2];
+          uint32_t wr[2] = {0, 0}, wg[2] = {0, 0}, wb[2] = {0, 0};
+          if (LAY == kRs444) {
+            const uint32_t cbw[2] = {sw[(oBi + x) >> 2], sw[(oBi + x + 4) >> 2]};
+            const uint32_t crw[2] = {sw[(oRi + x) >> 2], sw[(oRi + x + 4) >> 2]};
 #pragma unroll
-          for (int k = 0; k < 4; k++) {
-            cb[1 + k] = (int)((bi1 >> (8 * k)) & 0xFF) * 3 + (int)((bf1 >> (8 * k)) & 0xFF);
-            cr[1 + k] = (int)((ri1 >> (8 * k)) & 0xFF) * 3 + (int)((rf1 >> (8 * k)) & 0xFF);
-          }
-          cb[5] = (int)(bi2 & 0xFF) * 3 + (int)(bf2 & 0xFF);
-          cr[5] = (int)(ri2 & 0xFF) * 3 + (int)(rf2 & 0xFF);
-          if (jg == 0) {
-            cb[0] = cb[1];
-            cr[0] = cr[1];
-          }
-#pragma unroll
-          for (int k = 0; k < 4; k++)  // right edge: column j + 1 past dwc - 1 repeats column j
-            if (jg + k + 1 > dwc - 1) {
-              cb[2 + k] = cb[1 + k];
-              cr[2 + k] = cr[1 + k];
+            for (int k = 0; k < 8; k++) {
+              const int sh = 8 * (k & 3);
+              const uint32_t yw = k < 4 ? y0 : y1;
+              int r, g, b;
+              ycc_px((int)((yw >> sh) & 0xFF), (int)((cbw[k >> 2] >> sh) & 0xFF) - 128,
+                     (int)((crw[k >> 2] >> sh) & 0xFF) - 128, r, g, b);
+              wr[k >> 2] |= (uint32_t)r << sh;
+              wg[k >> 2] |= (uint32_t)g << sh;
+              wb[k >> 2] |= (uint32_t)b << sh;
             }
-        }
-        const uint32_t y0 = L.st[(oY + x) >> 2], y1 = L.st[(oY + x + 4) >> 2];
-        uint32_t wr[2] = {0, 0}, wg[2] = {0, 0}, wb[2] = {0, 0};
+          } else {
+            // chroma column values for columns jg - 1 .. jg + 4: 4:2:0 the column sums
+            // 3 * row_i + row_f, 4:2:2 the row itself (edges repeat column 0 / dwc - 1)
+            int cb[6], cr[6];
+            {
+              const uint32_t bi0 = sw[(oBi + jg - 4) >> 2], bi1 = sw[(oBi + jg) >> 2], bi2 = sw[(oBi + jg + 4) >> 2];
+              const uint32_t ri0 = sw[(oRi + jg - 4) >> 2], ri1 = sw[(oRi + jg) >> 2], ri2 = sw[(oRi + jg + 4) >> 2];
+              if (LAY == kRs420) {
+                const int oBf = L.rinfo[q][2], oRf = L.rinfo[q][4];
+                const uint32_t bf0 = sw[(oBf + jg - 4) >> 2], bf1 = sw[(oBf + jg) >> 2], bf2 = sw[(oBf + jg + 4) >> 2];
+                const uint32_t rf0 = sw[(oRf + jg - 4) >> 2], rf1 = sw[(oRf + jg) >> 2], rf2 = sw[(oRf + jg + 4) >> 2];
+                cb[0] = (int)(bi0 >> 24) * 3 + (int)(bf0 >> 24);
+                cr[0] = (int)(ri0 >> 24) * 3 + (int)(rf0 >> 24);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int c0 = cb[1 + k], d0 = cr[1 + k];
-          const uint32_t yw = k < 2 ? y0 : y1;
-          const int ye = (int)((yw >> (16 * (k & 1))) & 0xFF), yo = (int)((yw >> (16 * (k & 1) + 8)) & 0xFF);
-          int r0, g0, b0, r1, g1, b1;
-          ycc_px(ye, ((c0 * 3 + cb[k] + 8) >> 4) - 128, ((d0 * 3 + cr[k] + 8) >> 4) - 128, r0, g0, b0);
-          ycc_px(yo, ((c0 * 3 + cb[2 + k] + 7) >> 4) - 128, ((d0 * 3 + cr[2 + k] + 7) >> 4) - 128, r1, g1, b1);
-          const int sh = 16 * (k & 1);
-          wr[k >> 1] |= (uint32_t)(r0 | (r1 << 8)) << sh;
-          wg[k >> 1] |= (uint32_t)(g0 | (g1 << 8)) << sh;
-          wb[k >> 1] |= (uint32_t)(b0 | (b1 << 8)) << sh;
+                for (int k = 0; k < 4; k++) {
+                  cb[1 + k] = (int)((bi1 >> (8 * k)) & 0xFF) * 3 + (int)((bf1 >> (8 * k)) & 0xFF);
+                  cr[1 + k] = (int)((ri1 >> (8 * k)) & 0xFF) * 3 + (int)((rf1 >> (8 * k)) & 0xFF);
+                }
+                cb[5] = (int)(bi2 & 0xFF) * 3 + (int)(bf2 & 0xFF);
+                cr[5] = (int)(ri2 & 0xFF) * 3 + (int)(rf2 & 0xFF);
+              } else {
+                cb[0] = (int)(bi0 >> 24);
+                cr[0] = (int)(ri0 >> 24);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                  cb[1 + k] = (int)((bi1 >> (8 * k)) & 0xFF);
+                  cr[1 + k] = (int)((ri1 >> (8 * k)) & 0xFF);
+                }
+                cb[5] = (int)(bi2 & 0xFF);
+                cr[5] = (int)(ri2 & 0xFF);
+              }
+              if (jg == 0) {
+                cb[0] = cb[1];
+                cr[0] = cr[1];
+              }
+#pragma unroll
+              for (int k = 0; k < 4; k++)  // right edge: column j + 1 past dwc - 1 repeats column j
+                if (jg + k + 1 > dwc - 1) {
+                  cb[2 + k] = cb[1 + k];
+                  cr[2 + k] = cr[1 + k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const int c0 = cb[1 + k], d0 = cr[1 + k];
+              const uint32_t yw = k < 2 ? y0 : y1;
+              const int ye = (int)((yw >> (16 * (k & 1))) & 0xFF), yo = (int)((yw >> (16 * (k & 1) + 8)) & 0xFF);
+              int r0, g0, b0, r1, g1, b1;
+              if (LAY == kRs420) {  // jdsample.c h2v2_fancy_upsample
+                ycc_px(ye, ((c0 * 3 + cb[k] + 8) >> 4) - 128, ((d0 * 3 + cr[k] + 8) >> 4) - 128, r0, g0, b0);
+                ycc_px(yo, ((c0 * 3 + cb[2 + k] + 7) >> 4) - 128, ((d0 * 3 + cr[2 + k] + 7) >> 4) - 128, r1, g1, b1);
+              } else {  // jdsample.c h2v1_fancy_upsample
+                ycc_px(ye, ((c0 * 3 + cb[k] + 1) >> 2) - 128, ((d0 * 3 + cr[k] + 1) >> 2) - 128, r0, g0, b0);
+                ycc_px(yo, ((c0 * 3 + cb[2 + k] + 2) >> 2) - 128, ((d0 * 3 + cr[2 + k] + 2) >> 2) - 128, r1, g1, b1);
+              }
+              const int sh = 16 * (k & 1);
+              wr[k >> 1] |= (uint32_t)(r0 | (r1 << 8)) << sh;
+              wg[k >> 1] |= (uint32_t)(g0 | (g1 << 8)) << sh;
+              wb[k >> 1] |= (uint32_t)(b0 | (b1 << 8)) << sh;
+            }
+          }
+          uint32_t* o = reinterpret_cast<uint32_t*>(&L.rgb[q][0][x - xb]);
+          o[0] = wr[0];
+          o[1] = wr[1];
+          o[kFRgbW / 4] = wg[0];
+          o[kFRgbW / 4 + 1] = wg[1];
+          o[kFRgbW / 2] = wb[0];
+          o[kFRgbW / 2 + 1] = wb[1];
         }
-        uint32_t* o = reinterpret_cast<uint32_t*>(&L.rgb[q][0][x - xb]);
-        o[0] = wr[0];
-        o[1] = wr[1];
-        o[kFRgbW / 4] = wg[0];
-        o[kFRgbW / 4 + 1] = wg[1];
-        o[kFRgbW / 2] = wb[0];
-        o[kFRgbW / 2 + 1] = wb[1];
+        __syncthreads();
       }
-      __syncthreads();
       mark(1);
       if (active) {
 #pragma unroll
@@ -307,38 +373,53 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
           if (q >= nr) break;
           // H. KT taps of step row q -> ring slot.  Each channel's window comes in as aligned dwords
           // (unaligned sub-dword LDS reads are slow) and is realigned with v_alignbyte.
-          const int s0 = htaps<KT>(hw + q * 3 * (kFRgbW / 4), hsh, cf);
-          const int s1 = htaps<KT>(hw + (q * 3 + 1) * (kFRgbW / 4), hsh, cf);
-          const int s2 = htaps<KT>(hw + (q * 3 + 2) * (kFRgbW / 4), hsh, cf);
           const int r = ra + q;
-          ring[(r & rmask) * rstride] = pack3(s0, s1, s2);
+          if (LAY == kRsGray) {
+            ring[(r & rmask) * rstride] = (uint32_t)htaps<KT>(hw + q * kFYDW, hsh, cf);
+          } else {
+            const int s0 = htaps<KT>(hw + q * 3 * (kFRgbW / 4), hsh, cf);
+            const int s1 = htaps<KT>(hw + (q * 3 + 1) * (kFRgbW / 4), hsh, cf);
+            const int s2 = htaps<KT>(hw + (q * 3 + 2) * (kFRgbW / 4), hsh, cf);
+            ring[(r & rmask) * rstride] = pack3(s0, s1, s2);
+          }
           // V. output rows whose window ends at row r
           while (!(SDSJ_RS_EXP & 2) && nb < oy1) {
             const int vmin = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][0]);
             const int vcnt = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][1]);
             if (vmin + vcnt > r + 1) break;
-            int32_t v0 = 1 << 21, v1 = 1 << 21, v2 = 1 << 21;
             const int32_t* wk = L.vw[nb - oy0];
-            for (int k = 0; k < vcnt; k++) {
-              const uint32_t h = ring[((vmin + k) & rmask) * rstride];
-              const int32_t w = wk[k];
-              v0 += tap((int32_t)(h & 0xFF), w);
-              v1 += tap((int32_t)((h >> 8) & 0xFF), w);
-              v2 += tap((int32_t)(h >> 16), w);
+            if (LAY == kRsGray) {
+              int32_t v0 = 1 << 21;
+              for (int k = 0; k < vcnt; k++) v0 += tap((int32_t)ring[((vmin + k) & rmask) * rstride], wk[k]);
+              const int c = rs_clip8(v0);
+              if (SDSJ_RS_EXP & 1)
+                asm volatile("" ::"v"(c));
+              else
+                put3(out, om, lut, (int64_t)nb * ow + ox, c, c, c);
+            } else {
+              int32_t v0 = 1 << 21, v1 = 1 << 21, v2 = 1 << 21;
+              for (int k = 0; k < vcnt; k++) {
+                const uint32_t h = ring[((vmin + k) & rmask) * rstride];
+                const int32_t w = wk[k];
+                v0 += tap((int32_t)(h & 0xFF), w);
+                v1 += tap((int32_t)((h >> 8) & 0xFF), w);
+                v2 += tap((int32_t)(h >> 16), w);
+              }
+              if (SDSJ_RS_EXP & 1)
+                asm volatile("" ::"v"(v0), "v"(v1), "v"(v2));
+              else
+                put3(out, om, lut, (int64_t)nb * ow + ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
             }
-            if (SDSJ_RS_EXP & 1)
-              asm volatile("" ::"v"(v0), "v"(v1), "v"(v2));
-            else
-              put3(out, om, lut, (int64_t)nb * ow + ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
             nb++;
           }
         }
       }
+      if (LAY == kRsGray) __syncthreads();  // the H pass read the staged rows themselves
       if (more) {
         commit(nxt);
         cur = nxt;
       }
-      __syncthreads();  // next step's rows staged; this step's H reads of rgb are done
+      __syncthreads();  // next step's rows staged; this step's H reads are done
       mark(2);
     }
     if (SDSJ_RS_TIMING && lane == 0)
@@ -348,17 +429,27 @@ __device__ void rs420_image(int img, const ImgDesc* __restrict__ descs, const sd
   }
 }
 
+template <int LAY>
+static void launch_lay(const dim3& grid, int n, const ImgDesc* descs, const sdsj_op& op, int strip_h,
+                       const uint8_t* scratch, const uint8_t* flip, void* out, const int32_t* routes, int cap,
+                       const float* lut, hipStream_t s) {
+  hipLaunchKernelGGL((k_rs420<3, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL((k_rs420<5, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL((k_rs420<7, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL((k_rs420<9, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  hipLaunchKernelGGL((k_rs420<11, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+}
+
 hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
                               const uint8_t* flip, void* out, const int32_t* routes, int cap, const float* lut,
                               hipStream_t s) {
   const int tiles = (op.out_w + kFThreads - 1) / kFThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
-  const dim3 grid(n, strips, tiles);
-  hipLaunchKernelGGL(k_rs420<3>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_rs420<5>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_rs420<7>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_rs420<9>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_rs420<11>, grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  const dim3 grid(n < kRsfEntries ? n : kRsfEntries, strips, tiles);
+  launch_lay<kRs420>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
+  launch_lay<kRs422>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
+  launch_lay<kRs444>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
+  launch_lay<kRsGray>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
   return hipGetLastError();
 }
 

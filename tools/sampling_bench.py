@@ -18,9 +18,12 @@ def main():
     from sds_amd.engine import JpegEngine
     from tests.golden.synth import encode_jpeg, synth_rgb
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    only = sys.argv[2] if len(sys.argv) > 2 else None  # one sampling (profiling runs)
     eng = JpegEngine(max_batch=n, scratch_bytes=int(n * 7e6) + (256 << 20))
     for name, kw in (("4:2:0", dict(subsampling=2)), ("4:2:2", dict(subsampling=1)), ("4:4:4", dict(subsampling=0)),
                      ("gray", None)):
+        if only and name != only:
+            continue
         pool = []
         for i in range(64):
             rgb = synth_rgb(np.random.default_rng(1234 + i), 640, 480)

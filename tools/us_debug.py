@@ -61,12 +61,6 @@ def main():
                       f"end {d.scan_end_code}/{d.scan_end_raw} ref {end} ntiles {d.ntiles} tiles {tiles[:4]} "
                       f"nseg {d.nseg} first diffs {diff[:8]} pad_nonzero {sum(1 for x in got[d.ulen:d.ulen + 128] if x)}",
                       flush=True)
-                t_, k_ = d.pad3 & 0xFFFF, d.pad3 >> 16
-                words = [(x >> (32 * h)) & 0xFFFFFFFF for x in d.t_rs for h in (0, 1)]
-                seen = b"".join(int(w).to_bytes(4, "little") for w in words)
-                my0 = t_ * 32
-                print(f"    debug: thread {t_} split bit {k_} emit {d.pad5 & 0xFFFFFFFF:08x} seen[-4:28] {seen.hex()} "
-                      f"true {bytes(ent[max(my0 - 4, 0):my0 + 28]).hex()}", flush=True)
 
 
 if __name__ == "__main__":
