@@ -260,7 +260,7 @@ SDSJ_HD inline int64_t route_ints(int cap) { return kRouteSlots + (int64_t)(kNum
 // chroma layouts of the specialised fused resample (sdsj_resample420.hip)
 enum RsLay : int32_t { kRs420 = 0, kRs422 = 1, kRs444 = 2, kRsGray = 3 };
 SDSJ_HD inline int rs_route(int lay, int kt) { return kRtF + lay * 5 + (kt - 3) / 2; }
-constexpr int kRsfEntries = 512;  // workgroup columns of a specialised-resample launch (they stride over its list)
+constexpr int kRsfEntries = 4096;  // workgroup columns of a specialised-resample launch (they stride over its list)
 // generic fused resample route of an image whose horizontal pass has kt taps (1: none)
 SDSJ_HD inline int gen_route(int kt) {
   return kt == 1 ? kRtGen1 : (kt >= 3 && kt <= 11 && (kt & 1) ? kRtGen3 + (kt - 3) / 2 : kRtGen0);
