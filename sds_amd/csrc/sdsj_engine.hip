@@ -239,7 +239,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
 // stream waits for every lane at the end.  Scratch is taken by the lanes in image order (lane k + 1's
 // k_plan starts from lane k's total), so per-image results and capacity failures are those of a
 // single lane.
-constexpr int kLaneMin = 256;
+constexpr int kLaneMin = 128;
 
 int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_offsets, const int32_t* d_lengths,
               const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status, hipStream_t s) {

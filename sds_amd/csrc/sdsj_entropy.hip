@@ -351,7 +351,11 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   int l = e & 15;
   s = (e >> 4) & 15;
   r = (e >> 8) & 15;
+#ifdef SDSJ_EXP_NOLONG
+  if (l == 0) { l = 16; s = 0; r = 0; }  // (timing experiment: wrong output)
+#else
   if (l == 0) long_code<LB>(T, slot, isdc, hi, l, s, r, bad);
+#endif
   const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - s) & 31);
   val = s == 0 ? 0 : (x < (1u << (s - 1)) ? (int)x - (1 << s) + 1 : (int)x);
   const int tot = l + s;
@@ -361,11 +365,14 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
 }
 
 // decode_mcu's k loop: DC -> k = 1; AC value -> k += r + 1; ZRL -> k += 16; EOB -> done.
-// Returns true when the block is complete (z wraps to 0).
+// Returns true when the block is complete (z wraps to 0).  Branch-free: the step is r + 1 for a DC
+// symbol (r = 0), an AC value or ZRL (r = 15), and 64 for EOB.
 __device__ __forceinline__ bool next_z(int& z, int s, int r) {
-  const int zn = z == 0 ? 1 : (s ? z + r + 1 : (r == 15 ? z + 16 : 64));
-  z = zn >= 64 ? 0 : zn;
-  return zn >= 64;
+  const int m = (s != 0) | (r == 15) | (z == 0);
+  const int zn = z + 64 - m * (63 - r);
+  const bool done = zn >= 64;
+  z = done ? 0 : zn;
+  return done;
 }
 
 __device__ __forceinline__ void add_dc(int c, int v, int& d0, int& d1, int& d2) {
@@ -483,16 +490,16 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
-          if (next_z(z, s, r)) {
-            add_dc(c, dcd, d0, d1, d2);
-            if (nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
-            nrec++;
-            nblk++;
-            blk = blk + 1 == K.bpm ? 0 : blk + 1;
-            c = ctx_c(K, blk);
-            sdc = ctx_dc(K, blk);
-            sac = ctx_ac(K, blk);
-          }
+          const bool done = next_z(z, s, r);
+          if (done && nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
+          // block end without branches: the sums, counters and the next block's context by selects
+          add_dc(c, done ? dcd : 0, d0, d1, d2);
+          nrec += done ? 1 : 0;
+          nblk += done ? 1 : 0;
+          blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
+          c = ctx_c(K, blk);
+          sdc = ctx_dc(K, blk);
+          sac = ctx_ac(K, blk);
           run = b.pos < end || z != 0;
         }
       }

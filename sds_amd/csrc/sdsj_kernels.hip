@@ -366,33 +366,45 @@ __global__ void __launch_bounds__(256) k_finish(int n, const ImgDesc* __restrict
                                                 void* __restrict__ out, int32_t* __restrict__ status,
                                                 const float* __restrict__ lut, const int32_t* __restrict__ lengths,
                                                 unsigned long long* __restrict__ counters) {
-  const int img = blockIdx.x;
-  if (img >= n) return;
-  const ImgDesc* d = &descs[img];
-  const int st = d->status;
+  // one thread per image for its status and counters (summed in LDS, one atomic per counter and
+  // workgroup); the workgroup then zero-fills its failed / empty-crop images together
+  __shared__ unsigned long long acc[SDSJ_NUM_COUNTERS];
+  __shared__ int zlist[256];
+  __shared__ int nz;
+  const int t = threadIdx.x, img = blockIdx.x * 256 + t;
+  if (t < SDSJ_NUM_COUNTERS) acc[t] = 0;
+  if (t == 0) nz = 0;
+  __syncthreads();
   const int64_t plane = (int64_t)op.out_h * op.out_w, total = plane * 3;
-  if (threadIdx.x == 0) {
+  if (img < n) {
+    const ImgDesc* d = &descs[img];
+    const int st = d->status;
     status[img] = st;
     if (counters) {
       const int k = st == SDSJ_OK ? SDSJ_CTR_OK
                     : st == SDSJ_UNSUPPORTED ? SDSJ_CTR_UNSUPPORTED
                     : st == SDSJ_CORRUPT ? SDSJ_CTR_CORRUPT
                     : st == SDSJ_ECAPACITY ? SDSJ_CTR_CAPACITY : SDSJ_CTR_OTHER;
-      atomicAdd(&counters[lengths ? SDSJ_CTR_IMAGES : SDSJ_CTR_FRAMES], 1ull);
-      atomicAdd(&counters[k], 1ull);
-      if (lengths) atomicAdd(&counters[SDSJ_CTR_BYTES_IN], (unsigned long long)(uint32_t)lengths[img]);
-      atomicAdd(&counters[SDSJ_CTR_BYTES_OUT], (unsigned long long)(total * (op.out_dtype == SDSJ_DTYPE_F32 ? 4 : 1)));
-      if (lengths && st == SDSJ_OK && d->progressive) atomicAdd(&counters[SDSJ_CTR_PROGRESSIVE], 1ull);
+      atomicAdd(&acc[lengths ? SDSJ_CTR_IMAGES : SDSJ_CTR_FRAMES], 1ull);
+      atomicAdd(&acc[k], 1ull);
+      if (lengths) atomicAdd(&acc[SDSJ_CTR_BYTES_IN], (unsigned long long)(uint32_t)lengths[img]);
+      atomicAdd(&acc[SDSJ_CTR_BYTES_OUT], (unsigned long long)(total * (op.out_dtype == SDSJ_DTYPE_F32 ? 4 : 1)));
+      if (lengths && st == SDSJ_OK && d->progressive) atomicAdd(&acc[SDSJ_CTR_PROGRESSIVE], 1ull);
     }
+    if (!(st == SDSJ_OK && d->geo != kGeoZeros)) zlist[atomicAdd(&nz, 1)] = img;
   }
-  if (st == SDSJ_OK && d->geo != kGeoZeros) return;
-  if (op.out_dtype == SDSJ_DTYPE_F32) {
-    float* o = reinterpret_cast<float*>(out) + img * total;
-    const float z = lut[0];
-    for (int64_t i = threadIdx.x; i < total; i += blockDim.x) o[i] = z;
-  } else {
-    uint8_t* o = reinterpret_cast<uint8_t*>(out) + img * total;
-    for (int64_t i = threadIdx.x; i < total; i += blockDim.x) o[i] = 0;
+  __syncthreads();
+  if (counters && t < SDSJ_NUM_COUNTERS && acc[t]) atomicAdd(&counters[t], acc[t]);
+  for (int q = 0; q < nz; q++) {
+    const int64_t zi = zlist[q];
+    if (op.out_dtype == SDSJ_DTYPE_F32) {
+      float* o = reinterpret_cast<float*>(out) + zi * total;
+      const float z = lut[0];
+      for (int64_t i = t; i < total; i += blockDim.x) o[i] = z;
+    } else {
+      uint8_t* o = reinterpret_cast<uint8_t*>(out) + zi * total;
+      for (int64_t i = t; i < total; i += blockDim.x) o[i] = 0;
+    }
   }
 }
 
@@ -1496,7 +1508,8 @@ hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, Im
 }
 hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
                          const int32_t* lengths, unsigned long long* counters, hipStream_t s) {
-  hipLaunchKernelGGL(k_finish, dim3(n), dim3(256), 0, s, n, descs, op, out, status, lut, lengths, counters);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_finish, dim3((n + 255) / 256), dim3(256), 0, s, n, descs, op, out, status, lut, lengths, counters);
   return hipGetLastError();
 }
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
