@@ -356,8 +356,11 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
 #else
   if (l == 0) long_code<LB>(T, slot, isdc, hi, l, s, r, bad);
 #endif
+  // HUFF_EXTEND without branches: x < 2^(s-1) -> x - (2^s - 1); s = 0 -> 0
   const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - s) & 31);
-  val = s == 0 ? 0 : (x < (1u << (s - 1)) ? (int)x - (1 << s) + 1 : (int)x);
+  const uint32_t half = (1u << s) >> 1;
+  const int ext = x < half ? (int)x - (int)((1u << s) - 1u) : (int)x;
+  val = s != 0 ? ext : 0;
   const int tot = l + s;
   b.buf <<= tot;
   b.nb -= tot;
@@ -933,23 +936,25 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           bad |= sb;
           // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
           pc += isdc ? val : 0;
-          const int wpos = isdc ? 0 : (int)T.nat[z + r];
-          L.stage[((writing && (isdc || s)) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
-          if (next_z(z, s, r)) {
-            ready = writing;
-            gdone = (uint32_t)g;
-            p0 = c == 0 ? pc : p0;  // the component's predictor back, the next block's out
-            p1 = c == 1 ? pc : p1;
-            p2 = c == 2 ? pc : p2;
-            blk = blk + 1 == K.bpm ? 0 : blk + 1;
-            c = ctx_c(K, blk);
-            pc = c == 0 ? p0 : (c == 1 ? p1 : p2);
-            sdc = ctx_dc(K, blk);
-            sac = ctx_ac(K, blk);
-            g++;
-            writing = true;
-          }
-          run = g < gend && (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
+          const int wpos = T.nat[z + r];  // (natural_order[0] = 0 for the DC symbol)
+          L.stage[((writing & (isdc | (s != 0))) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
+          // block end by selects (no branches): the component's predictor back, the next block's out
+          const bool done = next_z(z, s, r);
+          ready = done & writing;
+          gdone = (uint32_t)g;
+          p0 = (done & (c == 0)) ? pc : p0;
+          p1 = (done & (c == 1)) ? pc : p1;
+          p2 = (done & (c == 2)) ? pc : p2;
+          blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
+          c = ctx_c(K, blk);
+          pc = done ? (c == 0 ? p0 : (c == 1 ? p1 : p2)) : pc;
+          sdc = ctx_dc(K, blk);
+          sac = ctx_ac(K, blk);
+          g += done ? 1 : 0;
+          writing = writing | done;
+          const bool more_last = !((z == 0) & (blk == 0) & (b.pos > lim));
+          const bool more_mid = (b.pos < end_bit) | (z != 0);
+          run = (g < gend) & (last_of_seg ? more_last : more_mid);
         }
         // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
         const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
