@@ -223,10 +223,26 @@ __device__ void load_sync_tables(SyncTables& T, const EntTables* g) {
 // global loads.  (CDNA counts loads and stores on one vmcnt: a load waited on inside the loop
 // would also wait for every coefficient/record store issued since.)
 // ------------------------------------------------------------------------------------------
-constexpr int kQ = 8;
-constexpr int kSpecGroup = 4;   // symbols decoded between two wave-uniform refill checks (spec pass)
-constexpr int kWriteGroup = 4;  // (write pass)
+#ifndef SDSJ_Q
+#define SDSJ_Q 8
+#endif
+constexpr int kQ = SDSJ_Q;
+#ifndef SDSJ_SPEC_GROUP
+#define SDSJ_SPEC_GROUP 4
+#endif
+#ifndef SDSJ_WRITE_GROUP
+#define SDSJ_WRITE_GROUP 4
+#endif
+constexpr int kSpecGroup = SDSJ_SPEC_GROUP;    // symbols decoded between two wave-uniform refill checks (spec pass)
+constexpr int kWriteGroup = SDSJ_WRITE_GROUP;  // (write pass)
 static_assert(kSpecGroup < kQ && kWriteGroup < kQ, "a fresh refill must pass the group check");
+// A symbol takes at most 27 bits (16-bit code + 11 extra bits; a bad code 17): a group of G symbols
+// has a word to pull before each of them when nb + 32 nq >= 27 (G - 1) + 32 at its start.
+#ifndef SDSJ_REFILL_SLACK
+#define SDSJ_REFILL_SLACK 0
+#endif
+constexpr int kRefillSpec = SDSJ_REFILL_SLACK ? 32 * (kSpecGroup + 1) : 27 * (kSpecGroup - 1) + 32;
+constexpr int kRefillWrite = SDSJ_REFILL_SLACK ? 32 * (kWriteGroup + 1) : 27 * (kWriteGroup - 1) + 32;
 
 template <int Q>
 struct BitsQ {
@@ -475,7 +491,7 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           }
         }
       }
-      if (__builtin_amdgcn_ballot_w64(warmup && b.nb + 32 * b.nq < 32 * (kSpecGroup + 1)) ||
+      if (__builtin_amdgcn_ballot_w64(warmup && b.nb + 32 * b.nq < kRefillSpec) ||
           !__builtin_amdgcn_ballot_w64(warmup))
         break;
     }
@@ -507,7 +523,7 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
         }
       }
       // leave to refill when a running lane may not hold kSpecGroup more symbols (<= 32 bits each)
-      if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kSpecGroup + 1)) ||
+      if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < kRefillSpec) ||
           !__builtin_amdgcn_ballot_w64(run))
         break;
     }
@@ -591,7 +607,7 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           next_chk = lo < nrec ? b.pos + kMergeBits : 0xFFFFFFFFu;
         }
       }
-      if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kSpecGroup + 1)) ||
+      if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < kRefillSpec) ||
           !__builtin_amdgcn_ballot_w64(run))
         break;
     }
@@ -980,7 +996,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           __builtin_amdgcn_wave_barrier();
         }
        }
-        if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < 32 * (kWriteGroup + 1)) ||
+        if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < kRefillWrite) ||
             !__builtin_amdgcn_ballot_w64(run))
           break;
       }
