@@ -24,7 +24,9 @@ constexpr int kMaxBlocksPerMcu = 10;  // D_MAX_BLOCKS_IN_MCU
 constexpr int kRec = 64;              // block-boundary records kept per subsequence by k_entsync
 constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
-constexpr int kWarmBits = 2000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
+constexpr int kWarmBits = 3000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
+constexpr int kWarmBitsSmall = 4500;  // ... for lanes of fewer than kWarmSmallLane images (the sync pass is
+constexpr int kWarmSmallLane = 512;   //     hidden by less concurrent work there, so it pays to shorten it)
 constexpr int kWarmDiv = 3;           // ... or sub_bits / kWarmDiv when that is larger
 // large images: ent_groups = ceil(bits / (kDecodeThreads x kGroupBits)) workgroups (<= kMaxEntGroups)
 // share the subsequences, so one lane's serial decode stays near kGroupBits

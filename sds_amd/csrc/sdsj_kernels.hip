@@ -54,6 +54,11 @@ __device__ __host__ inline void resample_bounds(int in_size, int out_size, doubl
 
 // frames = true: raw RGB frames (sdsj_resize_frames_device): the unfused passes read the frame rows
 // in place (off_rgb / rgb_pitch are set by the caller), no entropy / plane / RGB-row scratch.
+__device__ __host__ inline int warm_for(int sub_bits, int floor_bits) {
+  const int w = sub_bits / kWarmDiv > floor_bits ? sub_bits / kWarmDiv : floor_bits;
+  return sub_bits * 3 / 2 < w ? sub_bits * 3 / 2 : w;
+}
+
 __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, bool frames = false) {
   // Geometry: functional.py:78-80 shortcut, :118-147 crop, Pillow ImagingResampleInner.
   const int W = d->width, H = d->height;
@@ -144,12 +149,10 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
     d->sub_bits = (int32_t)align_up((bits + lanes - 1) / lanes, 32);
   }
   if (d->sub_bits < kMinSubBits) d->sub_bits = kMinSubBits;
-  // warm-up: kWarmBits, or sub_bits / kWarmDiv for long subsequences (large images: a few percent
-  // more speculative work removes nearly every sync task, each of which is a serial re-decode)
-  {
-    const int64_t w = d->sub_bits / kWarmDiv > kWarmBits ? d->sub_bits / kWarmDiv : kWarmBits;
-    d->warm_bits = (int)(d->sub_bits * 3 / 2 < w ? d->sub_bits * 3 / 2 : w);
-  }
+  // warm-up: kWarmBits (k_parse may raise the floor for small lanes), or sub_bits / kWarmDiv for long
+  // subsequences (large images: a few percent more speculative work removes nearly every sync task,
+  // each of which is a serial re-decode)
+  d->warm_bits = warm_for(d->sub_bits, kWarmBits);
   d->nsub_cap = (int32_t)((d->entropy_len * 8 + d->sub_bits - 1) / d->sub_bits) + d->nseg + 1;
   const bool prog = d->progressive && !frames;  // k_prog decodes it: no unstuffed stream, no subsequences
   if (prog) {
@@ -238,7 +241,8 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
     int status = parse_headers(rd, len, &sd, &st, sink);
     if (status == SDSJ_OK) status = setup_geometry(&sd, &st);
     if (status == SDSJ_OK) plan_image(&sd, op);
-    if (warm_bits >= 0) sd.warm_bits = warm_bits;
+    if (warm_bits >= 0) sd.warm_bits = warm_bits;                                 // override (experiments)
+    else if (n < kWarmSmallLane) sd.warm_bits = warm_for(sd.sub_bits, kWarmBitsSmall);  // small lane
     sd.status = status;
     for (int k = 0; k < 4; k++) sd.t_rs[k] = 0;
     s_status = status;
