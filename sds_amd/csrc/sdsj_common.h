@@ -200,7 +200,7 @@ struct ProgTables {
 };
 
 // One block boundary met by the speculative decode (for early sync detection).
-struct SyncRec {
+struct alignas(8) SyncRec {
   uint32_t p;       // bit position after the block's last symbol
   int16_t dc;       // DC difference decoded for that block
   uint8_t blk;      // MCU block index of the completed block

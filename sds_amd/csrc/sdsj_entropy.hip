@@ -510,7 +510,9 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           const bool done = next_z(z, s, r);
-          if (done && nrec < kRec) rec[nrec] = SyncRec{b.pos, (int16_t)dcd, (uint8_t)blk, 0};
+          if (done && nrec < kRec)  // one 8-byte store (SyncRec: p, dc, blk, pad)
+            reinterpret_cast<uint2*>(rec)[nrec] =
+                make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
           // block end without branches: the sums, counters and the next block's context by selects
           add_dc(c, done ? dcd : 0, d0, d1, d2);
           nrec += done ? 1 : 0;
@@ -866,6 +868,9 @@ struct LdsWrite {
   uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
   int32_t bad;
   unsigned long long sym;
+#ifdef SDSJ_EXP_LDSPAD
+  uint8_t pad_exp[SDSJ_EXP_LDSPAD];  // (occupancy experiment)
+#endif
 };
 
 template <int LB>
