@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sdsj_common.h"
 #include "sdsj_kernels.h"
 
@@ -53,6 +55,7 @@ constexpr int kMaxSlots = 2 * kMaxComp;  // a DC and an AC table per component a
 // Per-image decode tables in LDS.
 // ------------------------------------------------------------------------------------------
 struct EntTables {
+  static constexpr bool kTwoLevel = false;
   uint16_t lut[kLutEntries];
   int32_t maxcode[kMaxSlots][18];
   int32_t valoff[kMaxSlots][18];
@@ -183,6 +186,7 @@ __device__ __forceinline__ int load_tables(EntTables& T, const EntTables* g) {
 // lanes per image are latency-bound, and more images in flight hide that latency.
 constexpr int kSyncLB = 9;
 struct SyncTables {
+  static constexpr bool kTwoLevel = false;
   uint16_t lut[kMaxSlots << kSyncLB];
   int32_t maxcode[kMaxSlots][18];
   int32_t valoff[kMaxSlots][18];
@@ -356,6 +360,39 @@ __device__ __forceinline__ void long_code(const TT& T, int slot, bool isdc, uint
   }
 }
 
+// The write pass's tables for LB = 11 images (at most 4 slots), compact enough for 4 workgroups per
+// CU: a 9-bit first level and, for each 9-bit prefix of a longer code, a 4-entry second level holding
+// the LB = 11 table's entries for the next 2 bits (codes of 10 and 11 bits).  Longer codes (entry 0
+// at both levels) take the canonical search as before.  First-level entry of such a prefix:
+// (second-level subtable + 1) << 4 with length 0 (0: no subtable left -- the canonical search).
+constexpr int kW1 = 9;
+constexpr int kW2Cap = 256;  // second-level entries (64 subtables; a standard table needs ~8)
+struct WriteTables {
+  static constexpr bool kTwoLevel = true;
+  uint16_t lut[4 << kW1];
+  uint16_t l2[kW2Cap];
+  int32_t maxcode[4][18];
+  int32_t valoff[4][18];
+  uint8_t vals[4][256];
+  uint8_t nat[80];
+  uint32_t pk_dc[2], pk_ac[2], pk_c;
+  uint32_t pad[3];
+};
+
+template <int LB, class TT>
+__device__ __forceinline__ uint32_t lookup(const TT& T, int slot, uint32_t hi) {
+  if constexpr (TT::kTwoLevel) {
+    uint32_t e = T.lut[(slot << kW1) + (hi >> (32 - kW1))];
+    if ((e & 15) == 0) {  // code longer than 9 bits
+      const uint32_t sub = e >> 4;
+      e = sub ? T.l2[((sub - 1) << 2) + ((hi >> (32 - kW1 - 2)) & 3)] : 0u;
+    }
+    return e;
+  } else {
+    return T.lut[(slot << LB) + (hi >> (32 - LB))];
+  }
+}
+
 // One symbol (jdhuff.c HUFF_DECODE + get_bits + HUFF_EXTEND): DC -> category s, r = 0;
 // AC -> (r, s).  val = the extended value (0 when s = 0).
 template <int LB, class TT, int Q>
@@ -363,14 +400,16 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
                                            int& bad) {
   bits_pull(b);
   const uint32_t hi = (uint32_t)(b.buf >> 32);
-  const uint32_t e = T.lut[(slot << LB) + (hi >> (32 - LB))];
+  const uint32_t e = lookup<LB>(T, slot, hi);
   int l = e & 15;
   s = (e >> 4) & 15;
   r = (e >> 8) & 15;
 #ifdef SDSJ_EXP_NOLONG
   if (l == 0) { l = 16; s = 0; r = 0; }  // (timing experiment: wrong output)
 #else
-  if (l == 0) long_code<LB>(T, slot, isdc, hi, l, s, r, bad);
+  // (two-level tables: a prefix without a second level -- more long prefixes than kW2Cap / 4 -- may
+  // hold 10- and 11-bit codes too, so their search starts past the first level's width)
+  if (l == 0) long_code<TT::kTwoLevel ? kW1 : LB>(T, slot, isdc, hi, l, s, r, bad);
 #endif
   // HUFF_EXTEND without branches: x < 2^(s-1) -> x - (2^s - 1); s = 0 -> 0
   const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - s) & 31);
@@ -861,9 +900,10 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
 // ------------------------------------------------------------------------------------------
 // k_entwrite
 // ------------------------------------------------------------------------------------------
-struct LdsWrite {
+template <class TT>
+struct LdsWriteT {
   unsigned long long t0, it;
-  EntTables T;
+  TT T;
   alignas(16) int16_t stage[(kEntThreads + 1) * kStageStride];  // + one shared sink block
   uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
   int32_t bad;
@@ -873,14 +913,72 @@ struct LdsWrite {
 #endif
 };
 
+// The compact two-level tables from the image's LB = 11 tables (HBM).  The staging area serves as
+// the scan's scratch before it is cleared.
+__device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tmp) {
+  const int t = threadIdx.x;
+  const int ns = g->nslots;
+  if (!variant_owns<11>(ns)) return ns;
+  // which 9-bit prefixes lead to longer codes: 8 consecutive prefixes per thread, one block scan
+  constexpr int kPer = (4 << kW1) / kEntThreads;
+  int cnt = 0;
+  uint32_t longmask = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int i = t * kPer + j, q = i >> kW1, k = i & ((1 << kW1) - 1);
+    const uint32_t e = q < ns ? g->lut[(q << 11) + (k << 2)] : 0u;
+    const int l = e & 15;
+    const bool lng = q < ns && (l == 0 || l > kW1);
+    longmask |= lng ? 1u << j : 0u;
+    cnt += lng ? 1 : 0;
+  }
+  int total;
+  int base = block_excl_scan<kEntThreads>(cnt, tmp, &total);
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int i = t * kPer + j, q = i >> kW1, k = i & ((1 << kW1) - 1);
+    uint32_t e = q < ns ? g->lut[(q << 11) + (k << 2)] : 0u;
+    if ((longmask >> j) & 1) {
+      const int sub = base++;
+      if (sub < kW2Cap / 4) {
+        for (int m = 0; m < 4; m++) W.l2[sub * 4 + m] = g->lut[(q << 11) + (k << 2) + m];
+        e = (uint32_t)(sub + 1) << 4;
+      } else {
+        e = 0;  // no second level left: the canonical search
+      }
+    }
+    W.lut[i] = (uint16_t)e;
+  }
+  for (int i = t; i < 4 * 18; i += kEntThreads) {
+    W.maxcode[i / 18][i % 18] = g->maxcode[i / 18][i % 18];
+    W.valoff[i / 18][i % 18] = g->valoff[i / 18][i % 18];
+  }
+  const uint32_t* gv = reinterpret_cast<const uint32_t*>(g->vals);
+  uint32_t* wvls = reinterpret_cast<uint32_t*>(W.vals);
+  for (int i = t; i < 4 * 64; i += kEntThreads) wvls[i] = gv[i];
+  for (int i = t; i < 80; i += kEntThreads) W.nat[i] = g->nat[i];
+  if (t == 0) {
+    W.pk_dc[0] = g->pk_dc[0];
+    W.pk_dc[1] = g->pk_dc[1];
+    W.pk_ac[0] = g->pk_ac[0];
+    W.pk_ac[1] = g->pk_ac[1];
+    W.pk_c = g->pk_c;
+  }
+  __syncthreads();
+  return ns;
+}
+
 template <int LB>
 __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                                uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
-  __shared__ LdsWrite L;
+  using TT = std::conditional_t<LB == 11, WriteTables, EntTables>;
+  __shared__ LdsWriteT<TT> L;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int ns = load_tables<LB>(L.T, &tables[img]);
+  int ns;
+  if constexpr (LB == 11) ns = load_write_tables(L.T, &tables[img], reinterpret_cast<int32_t*>(L.stage));
+  else ns = load_tables<LB>(L.T, &tables[img]);
   if (!variant_owns<LB>(ns)) return;
   {
     uint4* z4 = reinterpret_cast<uint4*>(L.stage);
@@ -893,7 +991,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     if (kStats) L.t0 = __builtin_amdgcn_s_memtime();
   }
   __syncthreads();
-  const EntTables& T = L.T;
+  const TT& T = L.T;
   const BlkCtx K = make_ctx(T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
