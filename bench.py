@@ -44,7 +44,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 PMC_JSON = os.path.join(REPO, "profiles", "pmc_latest.json")  # tools/pmc.sh + tools/pmc_summary.py output
 BOX_CPU_SHARE = 16  # host CPUs a one-GPU box allots (nproc there shows the whole machine)
 # engine stage -> kernels launched in it (rocprofv3 kernel names contain these)
-STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_unstuff", "k_scanmap"],
+STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_us_", "k_scanmap"],
                  "prog": ["k_prog"], "entspec": ["k_enttab", "k_entspec"], "entsync": ["k_entsync"],
                  "entwrite": ["k_entwrite"], "idct": ["k_idct"],
                  "color": ["k_color"], "coeffs": ["k_coeffs"], "hpass": ["k_hpass"], "vpass": ["k_vpass"],

@@ -48,7 +48,7 @@ struct sdsj_engine {
   int32_t* d_routes = nullptr;  // per-variant image lists built by k_plan (sdsj_common.h Route)
   // lanes 2.. of a chunk (run_chunk): route lists and scratch totals, streams and events
   int lanes = 4;     // SDSJ_LANES (experiments)
-  int lane_mid = 3;  // lane k + 1 starts at lane k's mark lane_mid (>= 2: k_plan done; -1: its spec pass)
+  int lane_mid = 2;  // lane k + 1 starts at lane k's mark lane_mid (>= 2: k_plan done; -1: its spec pass)
   int64_t* d_totals_x = nullptr;
   int32_t* d_routes_x = nullptr;
   hipStream_t aux[kMaxLanes - 1] = {};
