@@ -231,6 +231,9 @@ __device__ void load_sync_tables(SyncTables& T, const EntTables* g) {
 #define SDSJ_Q 8
 #endif
 constexpr int kQ = SDSJ_Q;
+#ifndef SDSJ_SPEC_WAVES
+#define SDSJ_SPEC_WAVES 7  // k_entspec<11> occupancy target (waves per SIMD; 8 spills 7 VGPRs and measured no faster)
+#endif
 #ifndef SDSJ_SPEC_GROUP
 #define SDSJ_SPEC_GROUP 4
 #endif
@@ -304,6 +307,7 @@ __device__ __forceinline__ bool bits_can(const BitsQ<Q>& b) { return b.nb > 32 |
 
 template <int Q>
 __device__ __forceinline__ void bits_pull(BitsQ<Q>& b) {
+#ifdef SDSJ_PULL_BRANCH
   if (b.nb <= 32) {
     b.buf |= (uint64_t)b.q[0] << (32 - b.nb);
     b.nb += 32;
@@ -312,6 +316,17 @@ __device__ __forceinline__ void bits_pull(BitsQ<Q>& b) {
     b.nq--;
     b.wi++;
   }
+#else
+  // branch-free: a divergent branch here made the compiler copy the whole queue around it on every
+  // symbol (phi copies on both paths); selects shift it in place
+  const bool need = b.nb <= 32;
+  b.buf |= need ? (uint64_t)b.q[0] << ((32 - b.nb) & 63) : 0ull;
+  b.nb += need ? 32 : 0;
+#pragma unroll
+  for (int k = 0; k + 1 < Q; k++) b.q[k] = need ? b.q[k + 1] : b.q[k];
+  b.nq -= need ? 1 : 0;
+  b.wi += need ? 1u : 0u;
+#endif
 }
 
 // MCU position -> table slots and component, from packed per-image registers.
@@ -664,12 +679,22 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   return nsym;
 }
 
+// The speculative pass's LDS: tables, the layout scan's scratch, statistics -- not the sync kernel's
+// task / scan arrays (5 KB that cost it two workgroups per CU)
+struct LdsSpec {
+  EntTables T;
+  int32_t tmp[kEntThreads];
+  int32_t nsub;
+  unsigned long long sym[1], it[1], t0, t1;
+  int32_t wmax[kEntThreads / 64];
+};
+
 template <int LB>
 __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                               uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
-  __shared__ LdsSync L;
+  __shared__ LdsSpec L;
   const int t = threadIdx.x;
   const int ns = load_tables<LB>(L.T, &tables[img]);
   if (!variant_owns<LB>(ns)) return;
@@ -1168,7 +1193,7 @@ __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables
 // k_entspec: subsequence layout + speculative pass (warm-up, records); k_entsync: sync rounds +
 // segmented scan, decode tables built only when some entry disagrees with its predecessor's exit.
 template <int LB, int RT, int MODE>
-__global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(5)))
+__global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(LB == 11 ? SDSJ_SPEC_WAVES : 5)))
 k_entspec(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, uint8_t* __restrict__ scratch,
           int32_t* __restrict__ routes, int cap) {
   ent_feed<LB, 0, RT, MODE>(descs, tables, scratch, routes, cap);
