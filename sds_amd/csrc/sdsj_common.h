@@ -25,12 +25,15 @@ constexpr int kRec = 64;              // block-boundary records kept per subsequ
 constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
 constexpr int kWarmBits = 3000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
-constexpr int kWarmBitsSmall = 4500;  // ... for lanes of fewer than kWarmSmallLane images (the sync pass is
+constexpr int kWarmBitsSmall = 4000;  // ... for lanes of fewer than kWarmSmallLane images (the sync pass is
 constexpr int kWarmSmallLane = 512;   //     hidden by less concurrent work there, so it pays to shorten it)
 constexpr int kWarmDiv = 3;           // ... or sub_bits / kWarmDiv when that is larger
 // large images: ent_groups = ceil(bits / (kDecodeThreads x kGroupBits)) workgroups (<= kMaxEntGroups)
 // share the subsequences, so one lane's serial decode stays near kGroupBits
-constexpr int kGroupBits = 8192;
+#ifndef SDSJ_GROUP_BITS
+#define SDSJ_GROUP_BITS 8192
+#endif
+constexpr int kGroupBits = SDSJ_GROUP_BITS;
 constexpr int kMaxEntGroups = 16;
 constexpr int kGroupShift = 4;  // (image << kGroupShift) | group in the group-task list
 static_assert((1 << kGroupShift) >= kMaxEntGroups, "group index must fit the task encoding");
