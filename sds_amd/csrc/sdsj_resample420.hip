@@ -28,6 +28,10 @@
 #define SDSJ_RS_EXP 0  // experiments (tools/rs_timing.py): 1 = no output stores, 2 = no vertical gather
 #endif
 
+#ifndef SDSJ_VUNROLL
+#define SDSJ_VUNROLL 1  // (0: the vertical taps as a runtime loop, for A/B runs)
+#endif
+
 namespace sdsj {
 
 constexpr int kFThreads = 256;
@@ -388,9 +392,17 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
             const int vcnt = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][1]);
             if (vmin + vcnt > r + 1) break;
             const int32_t* wk = L.vw[nb - oy0];
+            // ksv <= KT (square crops): KT taps unrolled, so their ring and weight reads issue together
+            // (the weights past the window are zero, k_coeffs; ring rows past it are finite values)
+            const bool unr = SDSJ_VUNROLL && ksv <= KT;
             if (LAY == kRsGray) {
               int32_t v0 = 1 << 21;
-              for (int k = 0; k < vcnt; k++) v0 += tap((int32_t)ring[((vmin + k) & rmask) * rstride], wk[k]);
+              if (unr) {
+#pragma unroll
+                for (int k = 0; k < KT; k++) v0 += tap((int32_t)ring[((vmin + k) & rmask) * rstride], wk[k]);
+              } else {
+                for (int k = 0; k < vcnt; k++) v0 += tap((int32_t)ring[((vmin + k) & rmask) * rstride], wk[k]);
+              }
               const int c = rs_clip8(v0);
               if (SDSJ_RS_EXP & 1)
                 asm volatile("" ::"v"(c));
@@ -398,12 +410,18 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
                 put3(out, om, lut, (int64_t)nb * ow + ox, c, c, c);
             } else {
               int32_t v0 = 1 << 21, v1 = 1 << 21, v2 = 1 << 21;
-              for (int k = 0; k < vcnt; k++) {
+              auto vtap = [&](int k) {
                 const uint32_t h = ring[((vmin + k) & rmask) * rstride];
                 const int32_t w = wk[k];
                 v0 += tap((int32_t)(h & 0xFF), w);
                 v1 += tap((int32_t)((h >> 8) & 0xFF), w);
                 v2 += tap((int32_t)(h >> 16), w);
+              };
+              if (unr) {
+#pragma unroll
+                for (int k = 0; k < KT; k++) vtap(k);
+              } else {
+                for (int k = 0; k < vcnt; k++) vtap(k);
               }
               if (SDSJ_RS_EXP & 1)
                 asm volatile("" ::"v"(v0), "v"(v1), "v"(v2));
