@@ -14,6 +14,11 @@ R*N_r-row index (sds/index.py:227-246 INTER_NODE slicing), no collective on the 
 ("scaling": "weak"); the process group (RCCL) only carries the barriers and the max-over-ranks of
 the timed region.
 
+``--workload mixed512`` is configs[2] (mixed VGA..4K -> 512 + hflip + float32 normalise, device-
+resident); ``--workload e2e512`` is configs[4]: each rank's rows as JPEG files in a local cache
+directory -> pinned slots -> H2D -> decode + resize 512 -> D2H into pinned host memory, two batches
+in flight, reported next to the device-resident rate of the same rows (``device_resident_value``).
+
 Prints ONE JSON line (rank 0).  ``roofline`` prices the dominant kernel: algorithmic bytes per
 launch (compressed bytes in + output bytes out) / that kernel's mean duration,
 measured with HIP events on its launch stream in a single-lane pass after the timed region (one
@@ -219,7 +224,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["vga256", "mixed512"], default="vga256",
+    ap.add_argument("--workload", choices=["vga256", "mixed512", "e2e512"], default="vga256",
                     help="vga256 = configs[1] (the headline metric); mixed512 = configs[2]: VGA..4K -> centre crop + "
                          "resize 512 + hflip(p=0.5) + CHW float normalise")
     ap.add_argument("--batch", type=int, default=None)
@@ -235,7 +240,9 @@ def main():
     ap.add_argument("--engine", choices=["hip", "stub"], default="hip", help="stub: CPU stand-in (launcher tests)")
     args = ap.parse_args()
     mixed = args.workload == "mixed512"
+    e2e = args.workload == "e2e512"
     defaults = {"batch": 512, "rows": 16384, "pool": 96, "res": 512} if mixed else \
+        {"batch": 1024, "rows": 16384, "pool": 256, "res": 512} if e2e else \
         {"batch": 4096, "rows": 100_000, "pool": 1024, "res": 256}
     for k, v in defaults.items():
         if getattr(args, k) is None:
@@ -314,7 +321,7 @@ def main():
     flips = torch.from_numpy((np.random.default_rng(99 + rank).random(nrows) < 0.5).astype(np.uint8)).to(dev)
     cursor = [0]
 
-    def step():
+    def dev_step():
         s = cursor[0]
         if s + B > nrows:
             s = 0
@@ -322,10 +329,54 @@ def main():
                                  status=status, normalize=mixed, flip=flips[s:s + B] if mixed else None)
         cursor[0] = s + B
 
+    step = dev_step
+    cache_dir = None
+    if e2e:
+        # configs[4]: the rank's rows as files in a local cache directory (what sds/downloader.py leaves
+        # for LoadFromDiskTransform, presets.py:613-626) -> pinned slot -> H2D -> decode + resize -> D2H
+        # into pinned host memory.  One step submits batch k and completes batch k - 1 (its D2H on a
+        # second stream), so batch k's file reads and H2D overlap batch k - 1's decode.
+        cache_dir = tempfile.mkdtemp(prefix=f"sdsj_cache_r{rank}_")
+        fpaths = []
+        for k, p in enumerate(period):
+            fpaths.append(os.path.join(cache_dir, f"{r0 + k:08d}.jpg"))
+            with open(fpaths[-1], "wb") as f:
+                f.write(pool[p])
+        row_paths = [fpaths[j % len(period)] for j in range(nrows)]
+        outs = [out, torch.empty_like(out)]
+        hosts = [torch.empty(out.shape, dtype=out.dtype, pin_memory=True) for _ in range(2)]
+        d2h = torch.cuda.Stream(dev)
+        pipe = {"k": 0, "prev": None, "bad": 0, "done": 0}
+
+        def complete_prev():
+            prev = pipe["prev"]
+            o, st = eng.wait(prev)
+            pipe["bad"] += int((st != 0).sum())
+            pipe["done"] += len(st)
+            with torch.cuda.stream(d2h):
+                hosts[prev].copy_(o, non_blocking=True)
+            pipe["prev"] = None
+
+        def e2e_step():
+            s = cursor[0]
+            if s + B > nrows:
+                s = 0
+            slot = pipe["k"] % 2
+            torch.cuda.current_stream(dev).wait_stream(d2h)  # slot's previous output has left for the host
+            eng.submit(slot, row_paths[s:s + B], (args.res, args.res), files=True, out=outs[slot])
+            if pipe["prev"] is not None:
+                complete_prev()
+            pipe["prev"], pipe["k"] = slot, pipe["k"] + 1
+            cursor[0] = s + B
+
+        step = e2e_step
+
     # correctness gate before timing: the first batch's statuses are all OK
     step()
+    if e2e:
+        complete_prev()
     sync()
-    n_bad = int((status != 0).sum().item())
+    n_bad = pipe["bad"] if e2e else int((status != 0).sum().item())
     if n_bad:
         raise SystemExit(f"rank {rank}: {n_bad} samples failed to decode")
     for _ in range(args.warmup):
@@ -343,7 +394,13 @@ def main():
     sync()
     t1 = time.perf_counter()
     barrier()
-    n_bad = int((status != 0).sum().item())  # the last timed batch decoded completely as well
+    if e2e:  # every batch completed in the pipeline decoded completely; the last one is drained here
+        complete_prev()
+        sync()
+        n_bad = pipe["bad"]
+        shutil.rmtree(cache_dir, ignore_errors=True)
+    else:
+        n_bad = int((status != 0).sum().item())  # the last timed batch decoded completely as well
     if n_bad:
         raise SystemExit(f"rank {rank}: {n_bad} samples of the last timed batch failed to decode")
     my_elapsed = t1 - t0
@@ -359,6 +416,19 @@ def main():
         world_seen = 1
     imgs = B * args.steps * world
     value = imgs / elapsed
+    step = dev_step  # the pixel check and the roofline run the device-resident path on the same rows
+    dev_value = None
+    if e2e:  # configs[4] asks for the rate next to the device-resident one: same rows, batch, output
+        for _ in range(args.warmup):
+            step()
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync()
+        dev_value = B * args.steps * world / max_over_ranks(time.perf_counter() - t0,
+                                                            device=None if stub or args.backend == "gloo" else dev)
 
     # pixel check after timing: the batch holding pool image 0 at its start row, against PIL (the
     # reference's arithmetic) -- and for configs[1] also the reference-generated golden digest
@@ -373,7 +443,7 @@ def main():
         ref = _pil_pipeline(pool[0], args.res, flip=fl, normalize=mixed)
         ok = int(status[k0].item()) == 0 and torch.equal(got, ref.contiguous())
         pixel_check = {"row": r0 + k0, "pool_image": 0, "equal_to_pil": bool(ok)}
-        if not mixed:
+        if not mixed and args.res == 256:  # (the golden digests are of the 256x256 output)
             from tests import goldens as G
             meta = G.load_json("g2_synth.json")
             if meta.get("seed") == 1234 and (meta.get("w"), meta.get("h"), meta.get("quality")) == (640, 480, 90):
@@ -435,11 +505,16 @@ def main():
         workload = (f"configs[2]: synthetic mixed VGA..4K q90 4:2:0 baseline JPEGs resident in HBM -> centre crop + "
                     f"bilinear resize {args.res}x{args.res} + hflip (p=0.5, seeded) + float32 CHW x/127.5-1"
                     if mixed else
+                    f"configs[4]: synthetic 640x480 q90 JPEG files in a local cache directory per rank -> pinned "
+                    f"slot -> H2D -> centre crop + bilinear resize {args.res}x{args.res} uint8 CHW -> D2H into "
+                    f"pinned host memory (two slots in flight)"
+                    if e2e else
                     ("configs[3]: " if world > 1 else "configs[1]: ") +
                     "synthetic 640x480 q90 4:2:0 baseline JPEGs resident in HBM -> "
                     f"centre crop + bilinear resize {args.res}x{args.res} uint8 CHW")
         line = {
             "metric": ("images/s device-resident JPEG decode+crop+resize@512+hflip+normalise (mixed VGA..4K)" if mixed
+                       else "images/s end-to-end JPEG files -> H2D -> decode+resize@512 -> D2H (PCIe-inclusive)" if e2e
                        else "images/s device-resident JPEG decode+resize@256, 1/2/4/8 MI355X; %HBM roofline"),
             "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -465,6 +540,10 @@ def main():
             "pixel_check": pixel_check,
             "cpu_baseline": cpu,
         }
+        if e2e:
+            line["device_resident_value"] = round(dev_value, 1)
+            line["e2e_over_device_resident"] = round(value / dev_value, 4)
+            line["roofline"]["note"] = "device-resident kernels of the same rows (the PCIe legs are not kernels)"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
