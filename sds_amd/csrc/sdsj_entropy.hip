@@ -249,6 +249,11 @@ static_assert(kSpecGroup < kQ && kWriteGroup < kQ, "a fresh refill must pass the
 #define SDSJ_REFILL_SLACK 0
 #endif
 constexpr int kRefillSpec = SDSJ_REFILL_SLACK ? 32 * (kSpecGroup + 1) : 27 * (kSpecGroup - 1) + 32;
+#ifndef SDSJ_REC_STORE
+#define SDSJ_REC_STORE kRec
+#endif
+constexpr int kRecStore = SDSJ_REC_STORE;  // records the speculative pass keeps (<= kRec; experiments)
+static_assert(kRecStore <= kRec, "records fit their scratch");
 constexpr int kRefillWrite = SDSJ_REFILL_SLACK ? 32 * (kWriteGroup + 1) : 27 * (kWriteGroup - 1) + 32;
 
 template <int Q>
@@ -564,7 +569,7 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           const bool done = next_z(z, s, r);
-          if (done && nrec < kRec)  // one 8-byte store (SyncRec: p, dc, blk, pad)
+          if (done && nrec < kRecStore)  // one 8-byte store (SyncRec: p, dc, blk, pad)
             reinterpret_cast<uint2*>(rec)[nrec] =
                 make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
           // block end without branches: the sums, counters and the next block's context by selects
@@ -592,7 +597,7 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
   S.spec_dc[0] = S.cur_dc[0] = d0;
   S.spec_dc[1] = S.cur_dc[1] = d1;
   S.spec_dc[2] = S.cur_dc[2] = d2;
-  S.nrec = nrec < kRec ? nrec : kRec;
+  S.nrec = nrec < kRecStore ? nrec : kRecStore;
   return nsym;
 }
 
