@@ -259,7 +259,10 @@ def main():
         int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus and "RANK" in os.environ and args.gpus > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    dev = torch.device("cpu") if stub else torch.device("cuda", local_rank)
+    # one GPU per rank; more ranks than GPUs (a rehearsal on a smaller box, --backend gloo) share them
+    # round-robin (torch.cuda.device_count() does not initialise the GPU)
+    ndev = 0 if stub else torch.cuda.device_count()
+    dev = torch.device("cpu") if stub else torch.device("cuda", local_rank % max(1, ndev))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if stub:
@@ -524,7 +527,8 @@ def main():
                        "batch_per_gpu": B, "mean_jpeg_bytes": round(mean_in, 1),
                        "parallelism": f"index-sharded x{world}, no collective on the data path"},
             "per_rank_images_per_s": [round(B * args.steps / t, 1) for t in per_rank],
-            "process_group": {"backend": args.backend if world > 1 else None, "world_size": world_seen},
+            "process_group": {"backend": args.backend if world > 1 else None, "world_size": world_seen,
+                              "gpus_visible": ndev if not stub else 0},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": (traffic or {}).get("bytes_per_launch"),
