@@ -25,7 +25,7 @@ def _run(gpus):
 def test_two_rank_launch_reports_the_whole_job():
     line = _run(2)
     assert line["n_gpus"] == 2
-    assert line["process_group"] == {"backend": "gloo", "world_size": 2}
+    assert line["process_group"] == {"backend": "gloo", "world_size": 2, "gpus_visible": 0}
     assert len(line["per_rank_images_per_s"]) == 2
     assert line["config"]["global_batch"] == 32 and line["config"]["rows_per_gpu"] == 64
     # value = all ranks' images over the slowest rank's time
