@@ -241,9 +241,12 @@ def main():
     args = ap.parse_args()
     mixed = args.workload == "mixed512"
     e2e = args.workload == "e2e512"
-    defaults = {"batch": 512, "rows": 16384, "pool": 96, "res": 512} if mixed else \
+    # batches: one engine call per step, whose lanes drain at its end (the caller's stream orders the
+    # next call after it), so larger batches amortise that (configs[1]: 455k images/s at 4096, 476k
+    # at 16384; configs[2]: 45.0k at 512, 59.8k at 2048 -- DESIGN.md §5)
+    defaults = {"batch": 2048, "rows": 16384, "pool": 96, "res": 512} if mixed else \
         {"batch": 1024, "rows": 16384, "pool": 256, "res": 512} if e2e else \
-        {"batch": 4096, "rows": 100_000, "pool": 1024, "res": 256}
+        {"batch": 16384, "rows": 100_000, "pool": 1024, "res": 256}
     for k, v in defaults.items():
         if getattr(args, k) is None:
             setattr(args, k, v)
@@ -315,9 +318,14 @@ def main():
         eng = StubEngine()
     else:
         from sds_amd.engine import JpegEngine
-        # device scratch from host planning (sdsj_plan_need): a batch holds at most B of the largest
-        needs = [JpegEngine.scratch_need([p], (args.res, args.res), normalize=mixed) for p in pool]
-        eng = JpegEngine(dev, max_batch=B, scratch_bytes=B * max(needs) + (64 << 20))
+        # device scratch from host planning (sdsj_plan_need): the largest sum over any B consecutive
+        # rows (the rows repeat this rank's pool period, so every batch is such a window)
+        need_of = {p: JpegEngine.scratch_need([pool[p]], (args.res, args.res), normalize=mixed) for p in set(period)}
+        cyc = np.array([need_of[p] for p in period], np.int64)
+        full, rem = divmod(B, len(cyc))
+        ext = np.concatenate([[0], np.cumsum(np.concatenate([cyc, cyc]))])
+        win = int(max(ext[k + rem] - ext[k] for k in range(len(cyc)))) if rem else 0
+        eng = JpegEngine(dev, max_batch=B, scratch_bytes=full * int(cyc.sum()) + win + (64 << 20))
     out = torch.empty((B, 3, args.res, args.res), dtype=torch.float32 if mixed else torch.uint8, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
     # hflip flags for every row, seeded (the user HorizontalFlipTransform, p = 0.5)

@@ -7,7 +7,8 @@
 set -e
 export TMPDIR=/tmp
 export SDSJ_LANES=${SDSJ_LANES:-1}
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 --rows 20000 $*"
+BATCH=${BATCH:-16384}  # bench.py's default configs[1] batch (the PMC summary is per dispatch of one lane)
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 --rows 20000 --batch $BATCH $*"
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU" \
@@ -17,4 +18,4 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   rm -rf gpurun_out/pmc_$i
   timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_$i -o p -- $B > gpurun_out/pmc_$i.log 2>&1
 done
-python3 tools/pmc_summary.py gpurun_out 4096 "$SDSJ_LANES" > gpurun_out/pmc.json
+python3 tools/pmc_summary.py gpurun_out "$BATCH" "$SDSJ_LANES" > gpurun_out/pmc.json
