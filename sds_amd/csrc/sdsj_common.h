@@ -43,6 +43,10 @@ constexpr int kUsSerialTiles = 64;    // images of at most this many tiles are u
 constexpr int kMaxSpan = 960;         // source columns per fused-resample tile (LDS row width)
 constexpr int kRingDW = 3072;         // fused-resample ring (dwords): ring_rows x (3072 / ring_rows) columns
 constexpr int kRingMaxRows = 16;      // vertical windows longer than this use the unfused path
+#ifndef SDSJ_VTAPS_F
+#define SDSJ_VTAPS_F 16
+#endif
+constexpr int kVTapsF = SDSJ_VTAPS_F;  // vertical taps the specialised fused kernels (k_rs420) stage; more: k_resample
 
 // Raw DHT content (bits[1..16], huffval) -- jdmarker.c get_dht.
 struct HuffSpec {

@@ -8,7 +8,7 @@
 namespace sdsj {
 
 constexpr int kMaxStrip = 64;  // output rows per fused-resample workgroup (strip) at most
-constexpr int kVTaps = 16;     // vertical taps staged in LDS (= the largest ring)
+constexpr int kVTaps = 16;     // vertical taps staged in LDS (= the largest ring); k_rs420: kVTapsF (sdsj_common.h)
 
 __device__ __forceinline__ int rs_clip8(int32_t v) {
   v >>= 22;

@@ -35,7 +35,10 @@
 namespace sdsj {
 
 constexpr int kFThreads = 256;
-constexpr int kFRows = 4;                // source rows per step
+#ifndef SDSJ_FROWS
+#define SDSJ_FROWS 4
+#endif
+constexpr int kFRows = SDSJ_FROWS;       // source rows per step
 constexpr int kFYDW = kMaxSpan / 4 + 2;  // staged luma (full-width) row (dwords)
 constexpr int kFCDW = kMaxSpan / 8 + 3;  // staged half-width chroma row (dwords)
 constexpr int kFRgbW = kMaxSpan + 32;    // RGB row pitch (bytes, even)
@@ -44,7 +47,9 @@ constexpr int kFRgbW = kMaxSpan + 32;    // RGB row pitch (bytes, even)
 template <int LAY>
 struct FGeo {
   static constexpr int kCDW = LAY == kRs444 ? kFYDW : (LAY == kRsGray ? 0 : kFCDW);
-  static constexpr int kCRows = LAY == kRsGray ? 0 : kFRows;  // staged rows per chroma plane (<= 4)
+  // staged rows per chroma plane: 4:2:0 reads rows y >> 1 and their vertical neighbours, at most
+  // kFRows / 2 + 2 of them for kFRows luma rows; the other layouts the luma rows' own
+  static constexpr int kCRows = LAY == kRsGray ? 0 : (LAY == kRs420 ? kFRows / 2 + 2 : kFRows);
   static constexpr int kStageDW = kFRows * kFYDW + 2 * kCRows * kCDW;
   static constexpr int kRgbRows = LAY == kRsGray ? 0 : kFRows;
   static constexpr int kRows = kFRows + 2 * kCRows;  // staged rows per step at most
@@ -56,7 +61,7 @@ struct LdsF {
   uint8_t rgb[FGeo<LAY>::kRgbRows > 0 ? FGeo<LAY>::kRgbRows : 1][3][kFRgbW];  // converted rows, planar
   uint32_t ring[kRingDW];                                    // per column: H results of the last R rows
   int32_t vb[kMaxStrip][2];                                  // strip rows: vertical window (first, count)
-  int32_t vw[kMaxStrip][kVTaps];                             // strip rows: vertical weights
+  int32_t vw[kMaxStrip][kVTapsF];                            // strip rows: vertical weights
   int32_t rinfo[kFRows][8];                                  // step row q: byte offsets of its staged rows
 };
 
@@ -84,8 +89,13 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
                           void* __restrict__ out, const float* __restrict__ lut);
 
 // Route (LAY, KT): a small grid strides over the route's list (an empty route costs one short launch).
+#ifdef SDSJ_RS_WAVES  // occupancy target (waves per SIMD); the 9- and 11-tap kernels at most 5 (their windows spill at 6)
+#define SDSJ_RS_OCC __attribute__((amdgpu_waves_per_eu(KT <= 7 ? SDSJ_RS_WAVES : (SDSJ_RS_WAVES > 5 ? 5 : SDSJ_RS_WAVES))))
+#else
+#define SDSJ_RS_OCC
+#endif
 template <int KT, int LAY>
-__global__ void __launch_bounds__(kFThreads) k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+__global__ void __launch_bounds__(kFThreads) SDSJ_RS_OCC k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                       int strip_h, const uint8_t* __restrict__ scratch,
                                                       const uint8_t* __restrict__ flip, void* __restrict__ out,
                                                       const int32_t* __restrict__ routes, int cap,
@@ -131,8 +141,8 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
   const int ntiles = (ow + tw - 1) / tw;
   const int r_lo = bv[2 * oy0], r_hi = bv[2 * (oy1 - 1)] + bv[2 * (oy1 - 1) + 1];
   // the strip's vertical windows and weights
-  for (int i = t; i < (oy1 - oy0) * kVTaps; i += kFThreads) {
-    const int b = i / kVTaps, k = i % kVTaps, oy = oy0 + b;
+  for (int i = t; i < (oy1 - oy0) * kVTapsF; i += kFThreads) {
+    const int b = i / kVTapsF, k = i % kVTapsF, oy = oy0 + b;
     if (k == 0) {
       L.vb[b][0] = bv[2 * oy];
       L.vb[b][1] = bv[2 * oy + 1];
