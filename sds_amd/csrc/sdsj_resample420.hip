@@ -289,7 +289,10 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
       if (LAY != kRsGray) {
         // B. fancy upsampling + ycc->rgb on 8 pixels per item
         for (int it = t; it < nr * ng; it += kFThreads) {
-          const int q = (it >= ng) + (it >= 2 * ng) + (it >= 3 * ng), gi = it - q * ng;
+          int q = 0;  // step row of the item (it / ng without a division)
+#pragma unroll
+          for (int k = 1; k < kFRows; k++) q += it >= k * ng ? 1 : 0;
+          const int gi = it - q * ng;
           const int x = xb + 8 * gi, jg = x >> 1;
           const int oY = L.rinfo[q][0], oBi = L.rinfo[q][1], oRi = L.rinfo[q][3];
           const uint32_t* sw = L.st;
