@@ -16,6 +16,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <thread>
 #include <vector>
@@ -184,7 +185,7 @@ struct Lane {
 // after_spec (optional) is recorded once the lane's speculative entropy pass is queued.
 int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const int64_t* d_offsets,
              const int32_t* d_lengths, const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status,
-             hipStream_t s, hipEvent_t after_spec) {
+             hipStream_t s, hipEvent_t after_spec, uint64_t rm) {
   std::vector<hipEvent_t>* evs = nullptr;
   if (e->timing) {
     if (e->ev_used == e->ev_sets.size()) {
@@ -204,29 +205,30 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   const int cap = e->max_batch;
   SDSJ_HIP(e, launch_plan(n, ln.descs, e->capacity, ln.base, ln.total, ln.routes, cap, s));
   mark(2);
-  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, ln.routes, cap, s));
+  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, ln.routes, cap, s, rm));
   SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, ln.descs, e->scratch, s));
   mark(3);
   // (after mark 3: the next lane may start while this lane's progressive images decode)
-  SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s));
+  SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s, rm));
   mark(4);
-  if (!(e->skip >> 4 & 1)) SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s));
+  if (!(e->skip >> 4 & 1)) SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(5);
-  if (!(e->skip >> 5 & 1)) SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
+  if (!(e->skip >> 5 & 1)) SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(6);
-  if (!(e->skip >> 6 & 1)) SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s));
+  if (!(e->skip >> 6 & 1)) SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(7);
   if (!(e->skip >> 7 & 1)) SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
   mark(8);
-  SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s));
+  SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s, rm));
   mark(9);
   SDSJ_HIP(e, launch_coeffs(n, ln.descs, op, e->scratch, s));
   mark(10);
-  SDSJ_HIP(e, launch_hpass(n, ln.descs, op, e->scratch, ln.routes, cap, s));
+  SDSJ_HIP(e, launch_hpass(n, ln.descs, op, e->scratch, ln.routes, cap, s, rm));
   mark(11);
-  SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s));
+  SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s, rm));
   mark(12);
-  if (!(e->skip >> 12 & 1)) SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s));
+  if (!(e->skip >> 12 & 1))
+    SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s, rm));
   SDSJ_HIP(e, launch_finish(n, ln.descs, op, d_out, d_status, e->d_lut, d_lengths, e->d_counters, s));
   mark(13);
   return SDSJ_OK;
@@ -241,12 +243,14 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
 // single lane.
 constexpr int kLaneMin = 128;
 
+// rm: the routes the chunk's images may take (host planning), or kAllRoutes
 int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_offsets, const int32_t* d_lengths,
-              const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status, hipStream_t s) {
+              const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status, hipStream_t s,
+              uint64_t rm = kAllRoutes) {
   int nl = std::min(std::max(e->lanes, 1), kMaxLanes);
   while (nl > 1 && n < nl * kLaneMin) nl--;
   const Lane first{e->descs, e->tables, e->d_etab, e->d_routes, e->d_total, nullptr};
-  if (nl == 1) return run_lane(e, first, n, d_blob, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr);
+  if (nl == 1) return run_lane(e, first, n, d_blob, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr, rm);
   for (int k = 0; k + 1 < nl; k++)
     if (!e->aux[k]) {
       SDSJ_HIP(e, hipStreamCreateWithFlags(&e->aux[k], hipStreamNonBlocking));
@@ -266,7 +270,7 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
     if (k > 0) SDSJ_HIP(e, hipStreamWaitEvent(ls, e->ev_mid[k - 1], 0));
     int st = run_lane(e, ln, i1 - i0, d_blob, d_offsets + i0, d_lengths + i0, op, d_flip ? d_flip + i0 : nullptr,
                       static_cast<uint8_t*>(d_out) + i0 * ob, d_status + i0, ls,
-                      k + 1 < nl ? e->ev_mid[k] : nullptr);
+                      k + 1 < nl ? e->ev_mid[k] : nullptr, rm);
     if (st != SDSJ_OK) return st;
   }
   for (int k = 0; k + 1 < nl; k++) {
@@ -371,13 +375,18 @@ int slot_reserve(sdsj_engine* e, Slot& sl, int n, size_t bytes) {
 // behind that copy, status D2H into pinned memory, completion event.
 int slot_launch(sdsj_engine* e, Slot& sl, int n, size_t bytes, const sdsj_op& op, void* out, hipStream_t s) {
   std::vector<int64_t> needs(n, 0);
+  std::atomic<uint64_t> rmask{0};  // the routes the batch takes (launchers skip the others)
   parallel_for(n, [&](int i0, int i1) {
+    uint64_t rm = 0;
     for (int i = i0; i < i1; i++) {
       if (sl.h_pre[i] != SDSJ_OK) continue;
       int st = SDSJ_OK;
-      const int64_t ni = host_plan_need(sl.h_stage + sl.h_offsets[i], sl.h_lengths[i], op, &st);
+      uint64_t r = 0;
+      const int64_t ni = host_plan_need(sl.h_stage + sl.h_offsets[i], sl.h_lengths[i], op, &st, &r);
       if (st == SDSJ_OK) needs[i] = align_up(ni, 256);
+      rm |= r;
     }
+    rmask.fetch_or(rm);
   });
   int64_t need = 0;
   for (int i = 0; i < n; i++) need += needs[i];
@@ -394,7 +403,7 @@ int slot_launch(sdsj_engine* e, Slot& sl, int n, size_t bytes, const sdsj_op& op
   SDSJ_HIP(e, hipMemcpyAsync(sl.d_flip, sl.h_flip, n, hipMemcpyHostToDevice, cs));
   SDSJ_HIP(e, hipEventRecord(sl.ev_h2d, cs));
   SDSJ_HIP(e, hipStreamWaitEvent(s, sl.ev_h2d, 0));
-  const int rc = run_chunk(e, n, sl.d_blob, sl.d_offsets, sl.d_lengths, op, sl.d_flip, out, sl.d_status, s);
+  const int rc = run_chunk(e, n, sl.d_blob, sl.d_offsets, sl.d_lengths, op, sl.d_flip, out, sl.d_status, s, rmask.load());
   if (rc != SDSJ_OK) return rc;
   SDSJ_HIP(e, hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
   SDSJ_HIP(e, hipEventRecord(sl.ev_done, s));
@@ -686,11 +695,14 @@ int sdsj_decode_resize_batch(sdsj_engine* e, int n, const uint8_t* const* jpg, c
     int m = std::min(e->max_batch, n - c0);
     // host planning: exact scratch need of this chunk (same code as k_parse / k_plan)
     int64_t need = 0, bytes = 0;
+    uint64_t rm = 0;  // the routes the chunk takes (launchers skip the others)
     for (int i = 0; i < m; i++) {
       int st = SDSJ_OK;
       if (len[c0 + i] > (size_t)INT32_MAX) return fail(e, SDSJ_EINVAL, "sample larger than 2 GiB");
-      int64_t ni = host_plan_need(jpg[c0 + i], (int64_t)len[c0 + i], *op, &st);
+      uint64_t r = 0;
+      int64_t ni = host_plan_need(jpg[c0 + i], (int64_t)len[c0 + i], *op, &st, &r);
       if (st == SDSJ_OK) need += align_up(ni, 256);
+      rm |= r;
       bytes += align_up((int64_t)len[c0 + i], 16);
     }
     if (need > e->capacity) {
@@ -726,7 +738,7 @@ int sdsj_decode_resize_batch(sdsj_engine* e, int n, const uint8_t* const* jpg, c
     SDSJ_HIP(e, hipMemcpyAsync(e->d_lengths, e->h_lengths, sizeof(int32_t) * m, hipMemcpyHostToDevice, s));
     SDSJ_HIP(e, hipMemcpyAsync(e->d_flip, e->h_flip, m, hipMemcpyHostToDevice, s));
     rc = run_chunk(e, m, e->d_blob, e->d_offsets, e->d_lengths, *op, e->d_flip,
-                   reinterpret_cast<uint8_t*>(out) + c0 * ob, e->d_status, s);
+                   reinterpret_cast<uint8_t*>(out) + c0 * ob, e->d_status, s, rm);
     if (rc != SDSJ_OK) return rc;
     SDSJ_HIP(e, hipMemcpyAsync(e->h_status, e->d_status, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s));
     SDSJ_HIP(e, hipStreamSynchronize(s));

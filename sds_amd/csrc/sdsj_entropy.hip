@@ -1236,40 +1236,51 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ 
 size_t enttab_bytes() { return sizeof(EntTables); }
 
 hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s) {
+                          int cap, hipStream_t s, uint64_t rm) {
   const int g = n;  // one workgroup per image on the main route
   EntTables* tables = static_cast<EntTables*>(etab);
-  hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
   const int gs = g < 256 ? g : 256;
-  hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3>), dim3(g * kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables,
-                     scratch, routes, cap);
-  hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  if (route_on(rm, kRtEnt11) || route_on(rm, kRtEnt11M) || route_on(rm, kRtEnt10))
+    hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
+  if (route_on(rm, kRtEnt11))
+    hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  if (route_on(rm, kRtEnt11M))
+    hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3>), dim3(g * kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables,
+                       scratch, routes, cap);
+  if (route_on(rm, kRtEnt10))
+    hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 
-hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, int32_t* routes, int cap, hipStream_t s) {
+hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, int32_t* routes, int cap, hipStream_t s,
+                          uint64_t rm) {
   const int g = n;
   EntTables* tables = static_cast<EntTables*>(etab);
   const int gs = g < 256 ? g : 256;
-  hipLaunchKernelGGL((k_entsync<11, kRtEnt11, 0, kSyncThreads>), dim3(g), dim3(kSyncThreads), 0, s, descs, tables, scratch,
-                     routes, cap);
-  hipLaunchKernelGGL((k_entsync<11, kRtEnt11M, 0, kEntThreads>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch,
-                     routes, cap);
-  hipLaunchKernelGGL((k_entsync<10, kRtEnt10, 1, kSyncThreads>), dim3(gs), dim3(kSyncThreads), 0, s, descs, tables, scratch,
-                     routes, cap);
+  if (route_on(rm, kRtEnt11))
+    hipLaunchKernelGGL((k_entsync<11, kRtEnt11, 0, kSyncThreads>), dim3(g), dim3(kSyncThreads), 0, s, descs, tables,
+                       scratch, routes, cap);
+  if (route_on(rm, kRtEnt11M))
+    hipLaunchKernelGGL((k_entsync<11, kRtEnt11M, 0, kEntThreads>), dim3(g), dim3(kEntThreads), 0, s, descs, tables,
+                       scratch, routes, cap);
+  if (route_on(rm, kRtEnt10))
+    hipLaunchKernelGGL((k_entsync<10, kRtEnt10, 1, kSyncThreads>), dim3(gs), dim3(kSyncThreads), 0, s, descs, tables,
+                       scratch, routes, cap);
   return hipGetLastError();
 }
 
 hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
-                           hipStream_t s) {
+                           hipStream_t s, uint64_t rm) {
   const int g = n;  // one workgroup per image on the main route
   const EntTables* tables = static_cast<const EntTables*>(etab);
   const int gs = g < 256 ? g : 256;
-  hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
-  hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(g * kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables,
-                     scratch, routes, cap);
-  hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  if (route_on(rm, kRtEnt11))
+    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  if (route_on(rm, kRtEnt11M))
+    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(g * kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables,
+                       scratch, routes, cap);
+  if (route_on(rm, kRtEnt10))
+    hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 

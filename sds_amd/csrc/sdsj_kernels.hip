@@ -284,6 +284,25 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
 // ------------------------------------------------------------------------------------------
 // k_plan: one workgroup; exclusive scan of per-image scratch needs -> absolute offsets.
 // ------------------------------------------------------------------------------------------
+// The routes of one planned image (k_plan's lists; host planning's route masks): unstuffing (-1 for
+// progressive images), entropy variant by the Huffman tables in use (slots as load_tables counts
+// them), resample variant as plan_image chose it (-1 for an empty crop).
+SDSJ_HD inline void image_routes(const ImgDesc& d, int* ru, int* re, int* rr) {
+  int keys[2 * kMaxComp], ns = 0;
+  for (int c = 0; c < d.ncomp; c++)
+    for (int k = 0; k < 2; k++) {
+      const int key = k ? (4 | d.comp[c].ta) : d.comp[c].td;
+      bool seen = false;
+      for (int q = 0; q < ns; q++) seen |= keys[q] == key;
+      if (!seen) keys[ns++] = key;
+    }
+  *ru = d.progressive ? -1 : (d.ntiles > kUsSerialTiles ? kRtUsBig : kRtUsSmall);
+  *re = d.progressive ? kRtProg : ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
+  *rr = d.geo == kGeoZeros ? -1
+        : !d.fused ? kRtUnfused
+                   : (d.rs_fast ? rs_route(d.rs_lay, d.rs_fast) : gen_route(d.need_h ? d.ksh : 1));
+}
+
 __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ descs, int64_t capacity,
                                                const int64_t* __restrict__ base, int64_t* __restrict__ total_out,
                                                int32_t* __restrict__ routes, int cap) {
@@ -323,21 +342,11 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
         d.off_tmp += start;
         d.off_kh += start;
         d.off_kv += start;
-        // routes: entropy variant by the Huffman tables in use (slots as load_tables counts them),
-        // resample variant as plan_image chose it
-        int keys[2 * kMaxComp], ns = 0;
-        for (int c = 0; c < d.ncomp; c++)
-          for (int k = 0; k < 2; k++) {
-            const int key = k ? (4 | d.comp[c].ta) : d.comp[c].td;
-            bool seen = false;
-            for (int q = 0; q < ns; q++) seen |= keys[q] == key;
-            if (!seen) keys[ns++] = key;
-          }
-        if (!d.progressive) {  // unstuffing: one workgroup per small image, tile-parallel passes for the rest
-          const int ru = d.ntiles > kUsSerialTiles ? kRtUsBig : kRtUsSmall;
-          routes[kRouteSlots + ru * cap + atomicAdd(&rcnt[ru], 1)] = i;
-        }
-        const int re = d.progressive ? kRtProg : ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
+        // routes (image_routes): unstuffing -- one workgroup per small image, tile-parallel passes for
+        // the rest --, entropy variant, resample variant
+        int ru, re, rr;
+        image_routes(d, &ru, &re, &rr);
+        if (ru >= 0) routes[kRouteSlots + ru * cap + atomicAdd(&rcnt[ru], 1)] = i;
         int32_t* lst = routes + kRouteSlots + re * cap;
         lst[atomicAdd(&rcnt[re], 1)] = i;
         if (re == kRtEnt11M) {
@@ -345,9 +354,7 @@ __global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ desc
           const int b = atomicAdd(&rcnt[kRtEnt11G], d.ent_groups);
           for (int q = 0; q < d.ent_groups; q++) gt[b + q] = (i << kGroupShift) | q;
         }
-        if (d.geo != kGeoZeros) {
-          const int rr = !d.fused ? kRtUnfused
-                         : (d.rs_fast ? rs_route(d.rs_lay, d.rs_fast) : gen_route(d.need_h ? d.ksh : 1));
+        if (rr >= 0) {
           lst = routes + kRouteSlots + rr * cap;
           lst[atomicAdd(&rcnt[rr], 1)] = i;
         }
@@ -1501,13 +1508,16 @@ hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* b
   return hipGetLastError();
 }
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
-                          const int32_t* routes, int cap, hipStream_t s) {
+                          const int32_t* routes, int cap, hipStream_t s, uint64_t rm) {
   const int g = n < kUsLaunch ? n : kUsLaunch;
   const int gt = n * kUsGrid < 4 * kUsLaunch ? n * kUsGrid : 4 * kUsLaunch;
-  hipLaunchKernelGGL(k_us_serial, dim3(g), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
-  hipLaunchKernelGGL(k_us_count, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
-  hipLaunchKernelGGL(k_us_scan, dim3(g), dim3(kUnstuffThreads), 0, s, descs, scratch, routes, cap);
-  hipLaunchKernelGGL(k_us_write, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
+  if (route_on(rm, kRtUsSmall))
+    hipLaunchKernelGGL(k_us_serial, dim3(g), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
+  if (route_on(rm, kRtUsBig)) {
+    hipLaunchKernelGGL(k_us_count, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
+    hipLaunchKernelGGL(k_us_scan, dim3(g), dim3(kUnstuffThreads), 0, s, descs, scratch, routes, cap);
+    hipLaunchKernelGGL(k_us_write, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
+  }
   return hipGetLastError();
 }
 hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
@@ -1525,7 +1535,9 @@ hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uin
   hipLaunchKernelGGL(k_idct, dim3(kIdctGrid, n), dim3(kIdctThreads), 0, s, n, descs, tables, scratch);
   return hipGetLastError();
 }
-hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s) {
+hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,
+                        uint64_t rm) {
+  if (!route_on(rm, kRtUnfused)) return hipSuccess;
   hipLaunchKernelGGL(k_color, dim3(64, n < 64 ? n : 64), dim3(256), 0, s, n, descs, scratch, routes, cap);
   return hipGetLastError();
 }
@@ -1535,12 +1547,14 @@ hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t
   return hipGetLastError();
 }
 hipError_t launch_hpass(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, const int32_t* routes, int cap,
-                        hipStream_t s) {
+                        hipStream_t s, uint64_t rm) {
+  if (!route_on(rm, kRtUnfused)) return hipSuccess;
   hipLaunchKernelGGL(k_hpass, dim3(32, n < 64 ? n : 64), dim3(256), 0, s, n, descs, op, scratch, routes, cap);
   return hipGetLastError();
 }
 hipError_t launch_vpass(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
-                        void* out, const int32_t* routes, int cap, const float* lut, hipStream_t s) {
+                        void* out, const int32_t* routes, int cap, const float* lut, hipStream_t s, uint64_t rm) {
+  if (!route_on(rm, kRtUnfused)) return hipSuccess;
   hipLaunchKernelGGL(k_vpass, dim3(32, n < 64 ? n : 64), dim3(256), 0, s, n, descs, op, scratch, flip, out, routes, cap, lut);
   return hipGetLastError();
 }
@@ -1562,7 +1576,7 @@ int64_t host_plan_frame(ImgDesc* d, int width, int height, const sdsj_op& op) {
   return plan_image(d, op, true);
 }
 
-int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status) {
+int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status, uint64_t* routes) {
   ImgDesc d;
   static thread_local ImgTables t;
   HostReader rd{jpg};
@@ -1571,6 +1585,14 @@ int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* st
   int64_t need = 0;
   if (st == SDSJ_OK) need = plan_image(&d, op);
   *status = st;
+  if (routes) {
+    *routes = kAllRoutes;
+    if (st == SDSJ_OK) {
+      int ru, re, rr;
+      image_routes(d, &ru, &re, &rr);
+      *routes = (ru >= 0 ? 1ull << ru : 0) | (1ull << re) | (rr >= 0 ? 1ull << rr : 0);
+    }
+  }
   return need;
 }
 }  // namespace sdsj

@@ -728,7 +728,9 @@ __global__ void __launch_bounds__(kProgLanes) k_prog(ImgDesc* __restrict__ descs
 }
 
 hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* blob, const int64_t* offsets,
-                       const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s) {
+                       const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,
+                       uint64_t rm) {
+  if (!route_on(rm, kRtProg)) return hipSuccess;
   hipLaunchKernelGGL(k_prog_zero, dim3(n, 16), dim3(256), 0, s, descs, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog, dim3((n + kProgLanes - 1) / kProgLanes), dim3(kProgLanes), 0, s, descs, tables, blob,
                      offsets, lengths, scratch, routes, cap);

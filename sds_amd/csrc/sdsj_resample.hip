@@ -408,23 +408,24 @@ __global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* _
 }
 
 hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
-                           void* out, int32_t* status, const int32_t* routes, int cap, const float* lut, hipStream_t s) {
+                           void* out, int32_t* status, const int32_t* routes, int cap, const float* lut, hipStream_t s,
+                           uint64_t rm) {
   // strips of output rows: tall for big batches (less window overlap), short for small ones
   const int strip_h = n >= 512 ? kMaxStrip : 16;
   const int tiles = (op.out_w + kRsThreads - 1) / kRsThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
   const dim3 grid(n < kRsfEntries ? n : kRsfEntries, strips, tiles);
-  hipLaunchKernelGGL(k_resample<0>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_resample<1>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_resample<3>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_resample<5>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_resample<7>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_resample<9>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL(k_resample<11>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen0)) hipLaunchKernelGGL(k_resample<0>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen1)) hipLaunchKernelGGL(k_resample<1>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen3)) hipLaunchKernelGGL(k_resample<3>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen5)) hipLaunchKernelGGL(k_resample<5>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen7)) hipLaunchKernelGGL(k_resample<7>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen9)) hipLaunchKernelGGL(k_resample<9>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen11)) hipLaunchKernelGGL(k_resample<11>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   (void)status;  // published by k_finish after every resample variant
-  return launch_resample420(n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
+  return launch_resample420(n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
 }
 
 }  // namespace sdsj

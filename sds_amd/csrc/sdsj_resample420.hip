@@ -463,24 +463,29 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
 template <int LAY>
 static void launch_lay(const dim3& grid, int n, const ImgDesc* descs, const sdsj_op& op, int strip_h,
                        const uint8_t* scratch, const uint8_t* flip, void* out, const int32_t* routes, int cap,
-                       const float* lut, hipStream_t s) {
-  hipLaunchKernelGGL((k_rs420<3, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL((k_rs420<5, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL((k_rs420<7, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL((k_rs420<9, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  hipLaunchKernelGGL((k_rs420<11, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+                       const float* lut, hipStream_t s, uint64_t rm) {
+  if (route_on(rm, rs_route(LAY, 3)))
+    hipLaunchKernelGGL((k_rs420<3, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, rs_route(LAY, 5)))
+    hipLaunchKernelGGL((k_rs420<5, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, rs_route(LAY, 7)))
+    hipLaunchKernelGGL((k_rs420<7, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, rs_route(LAY, 9)))
+    hipLaunchKernelGGL((k_rs420<9, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, rs_route(LAY, 11)))
+    hipLaunchKernelGGL((k_rs420<11, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
 }
 
 hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
                               const uint8_t* flip, void* out, const int32_t* routes, int cap, const float* lut,
-                              hipStream_t s) {
+                              hipStream_t s, uint64_t rm) {
   const int tiles = (op.out_w + kFThreads - 1) / kFThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
   const dim3 grid(n < kRsfEntries ? n : kRsfEntries, strips, tiles);
-  launch_lay<kRs420>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
-  launch_lay<kRs422>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
-  launch_lay<kRs444>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
-  launch_lay<kRsGray>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s);
+  launch_lay<kRs420>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
+  launch_lay<kRs422>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
+  launch_lay<kRs444>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
+  launch_lay<kRsGray>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
   return hipGetLastError();
 }
 
