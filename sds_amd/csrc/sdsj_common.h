@@ -164,6 +164,7 @@ struct ImgDesc {
   int64_t off_tiles;
   int32_t ntiles;
   int32_t rs_lay;  // chroma layout of the specialised fused kernel (RsLay) when rs_fast > 0
+  int64_t plan_base;  // k_plan_scan: the image's first scratch byte (the offsets above are relative until k_plan_apply)
 };
 
 // One tile of k_unstuff's first pass: bytes it emits and split markers (RSTn, codes below SOF0) it

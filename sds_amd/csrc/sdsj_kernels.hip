@@ -303,70 +303,87 @@ SDSJ_HD inline void image_routes(const ImgDesc& d, int* ru, int* re, int* rr) {
                    : (d.rs_fast ? rs_route(d.rs_lay, d.rs_fast) : gen_route(d.need_h ? d.ksh : 1));
 }
 
-__global__ void __launch_bounds__(1024) k_plan(int n, ImgDesc* __restrict__ descs, int64_t capacity,
-                                               const int64_t* __restrict__ base, int64_t* __restrict__ total_out,
-                                               int32_t* __restrict__ routes, int cap) {
+// k_plan, in two kernels.  k_plan_scan (one workgroup): exclusive scan of the images' scratch needs
+// from the previous lane's total (each image's plan_base, the lane's total), route counters zeroed.
+// k_plan_apply (one thread per image): capacity check, the image's scratch offsets, its route-list
+// entries -- counted per workgroup in LDS, one global atomic per route and workgroup (the lists'
+// order is the workgroups' arrival order; every image still lands in exactly its lists).
+__global__ void __launch_bounds__(1024) k_plan_scan(int n, ImgDesc* __restrict__ descs, const int64_t* __restrict__ base,
+                                                    int64_t* __restrict__ total_out, int32_t* __restrict__ routes) {
   __shared__ int64_t part[1024];
   __shared__ int64_t carry;
-  __shared__ int rcnt[kNumRoutes];
-  if (threadIdx.x == 0) carry = base ? *base : 0;  // a second lane allocates after the first
-  if (threadIdx.x < kNumRoutes) rcnt[threadIdx.x] = 0;
+  const int t = threadIdx.x;
+  if (t == 0) carry = base ? *base : 0;  // a second lane allocates after the first
+  if (t < kRouteSlots) routes[t] = 0;    // route counts, then work counters
   __syncthreads();
-  for (int base = 0; base < n; base += 1024) {
-    int i = base + threadIdx.x;
+  for (int b0 = 0; b0 < n; b0 += 1024) {
+    const int i = b0 + t;
     int64_t need = 0;
     if (i < n && descs[i].status == SDSJ_OK) need = descs[i].need;
-    part[threadIdx.x] = need;
+    part[t] = need;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {
-      int64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      const int64_t v = t >= off ? part[t - off] : 0;
       __syncthreads();
-      part[threadIdx.x] += v;
+      part[t] += v;
       __syncthreads();
     }
-    int64_t start = carry + part[threadIdx.x] - need;
-    if (i < n && descs[i].status == SDSJ_OK) {
-      ImgDesc& d = descs[i];
-      if (start + need > capacity) {
-        d.status = SDSJ_ECAPACITY;
-      } else {
-        d.off_ustream += start;
-        d.off_seg += start;
-        d.off_tiles += start;
-        d.off_sub += start;
-        d.off_rec += start;
-        d.off_ptab += start;
-        d.off_coef += start;
-        d.off_planes += start;
-        d.off_rgb += start;
-        d.off_tmp += start;
-        d.off_kh += start;
-        d.off_kv += start;
-        // routes (image_routes): unstuffing -- one workgroup per small image, tile-parallel passes for
-        // the rest --, entropy variant, resample variant
-        int ru, re, rr;
-        image_routes(d, &ru, &re, &rr);
-        if (ru >= 0) routes[kRouteSlots + ru * cap + atomicAdd(&rcnt[ru], 1)] = i;
-        int32_t* lst = routes + kRouteSlots + re * cap;
-        lst[atomicAdd(&rcnt[re], 1)] = i;
-        if (re == kRtEnt11M) {
-          int32_t* gt = group_tasks(routes, cap);
-          const int b = atomicAdd(&rcnt[kRtEnt11G], d.ent_groups);
-          for (int q = 0; q < d.ent_groups; q++) gt[b + q] = (i << kGroupShift) | q;
-        }
-        if (rr >= 0) {
-          lst = routes + kRouteSlots + rr * cap;
-          lst[atomicAdd(&rcnt[rr], 1)] = i;
-        }
-      }
-    }
+    if (i < n) descs[i].plan_base = carry + part[t] - need;
     __syncthreads();
-    if (threadIdx.x == 1023) carry += part[1023];
+    if (t == 1023) carry += part[1023];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *total_out = carry;
-  if (threadIdx.x < kNumRoutes) routes[threadIdx.x] = rcnt[threadIdx.x];
-  else if (threadIdx.x < kRouteSlots) routes[threadIdx.x] = 0;  // work counters
+  if (t == 0) *total_out = carry;
+}
+
+constexpr int kPlanThreads = 256;
+__global__ void __launch_bounds__(kPlanThreads) k_plan_apply(int n, ImgDesc* __restrict__ descs, int64_t capacity,
+                                                             int32_t* __restrict__ routes, int cap) {
+  __shared__ int lcnt[kNumRoutes], gbase[kNumRoutes];
+  const int t = threadIdx.x, i = blockIdx.x * kPlanThreads + t;
+  if (t < kNumRoutes) lcnt[t] = 0;
+  __syncthreads();
+  int ru = -1, re = -1, rr = -1, iu = 0, ie = 0, ir = 0, ig = 0, ng = 0;
+  if (i < n && descs[i].status == SDSJ_OK) {
+    ImgDesc& d = descs[i];
+    const int64_t start = d.plan_base;
+    if (start + d.need > capacity) {
+      d.status = SDSJ_ECAPACITY;
+    } else {
+      d.off_ustream += start;
+      d.off_seg += start;
+      d.off_tiles += start;
+      d.off_sub += start;
+      d.off_rec += start;
+      d.off_ptab += start;
+      d.off_coef += start;
+      d.off_planes += start;
+      d.off_rgb += start;
+      d.off_tmp += start;
+      d.off_kh += start;
+      d.off_kv += start;
+      // routes (image_routes): unstuffing -- one workgroup per small image, tile-parallel passes for
+      // the rest --, entropy variant, resample variant
+      image_routes(d, &ru, &re, &rr);
+      if (ru >= 0) iu = atomicAdd(&lcnt[ru], 1);
+      ie = atomicAdd(&lcnt[re], 1);
+      if (re == kRtEnt11M) {
+        ng = d.ent_groups;
+        ig = atomicAdd(&lcnt[kRtEnt11G], ng);
+      }
+      if (rr >= 0) ir = atomicAdd(&lcnt[rr], 1);
+    }
+  }
+  __syncthreads();
+  if (t < kNumRoutes) gbase[t] = lcnt[t] ? atomicAdd(&routes[t], lcnt[t]) : 0;
+  __syncthreads();
+  if (ru >= 0) routes[kRouteSlots + ru * cap + gbase[ru] + iu] = i;
+  if (re >= 0) routes[kRouteSlots + re * cap + gbase[re] + ie] = i;
+  if (ng) {
+    int32_t* gt = group_tasks(routes, cap);
+    for (int q = 0; q < ng; q++) gt[gbase[kRtEnt11G] + ig + q] = (i << kGroupShift) | q;
+  }
+  if (rr >= 0) routes[kRouteSlots + rr * cap + gbase[rr] + ir] = i;
 }
 
 // k_finish: publishes every sample's status and writes the zeros of failed samples and of empty
@@ -1504,7 +1521,10 @@ hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, cons
 }
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* base, int64_t* total, int32_t* routes,
                        int cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_plan, dim3(1), dim3(1024), 0, s, n, descs, capacity, base, total, routes, cap);
+  hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, n, descs, base, total, routes);
+  if (n > 0)
+    hipLaunchKernelGGL(k_plan_apply, dim3((n + kPlanThreads - 1) / kPlanThreads), dim3(kPlanThreads), 0, s, n, descs,
+                       capacity, routes, cap);
   return hipGetLastError();
 }
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,

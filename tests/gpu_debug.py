@@ -38,7 +38,7 @@ class ImgDescC(ctypes.Structure):
                 ("warm_bits", i32), ("scan_end_code", i32), ("scan_end_raw", i64),
                 ("rgb_pitch", i32), ("ent_groups", i32),
                 ("progressive", i32), ("pad3", i32), ("sos_pos", i64), ("off_ptab", i64),
-                ("off_tiles", i64), ("ntiles", i32), ("rs_lay", i32)]
+                ("off_tiles", i64), ("ntiles", i32), ("rs_lay", i32), ("plan_base", i64)]
 
 
 def _memcpy_d2h(ptr: int, nbytes: int) -> np.ndarray:
