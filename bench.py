@@ -39,6 +39,7 @@ import subprocess
 import sys
 import tempfile
 import time
+from typing import Optional
 
 import numpy as np
 
@@ -47,7 +48,6 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 PMC_JSON = os.path.join(REPO, "profiles", "pmc_latest.json")  # tools/pmc.sh + tools/pmc_summary.py output
-BOX_CPU_SHARE = 16  # host CPUs a one-GPU box allots (nproc there shows the whole machine)
 # engine stage -> kernels launched in it (rocprofv3 kernel names contain these)
 STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_us_", "k_scanmap"],
                  "prog": ["k_prog"], "entspec": ["k_enttab", "k_entspec"], "entsync": ["k_entsync"],
@@ -77,6 +77,43 @@ def pmc_traffic(stage: str, batch: int, lanes: int):
         if hit else None
 
 
+def pmc_counters(stage: str, batch: int, lanes: int) -> Optional[dict]:
+    """Per-launch PMC counters of `stage` (summed over its kernels) from the committed summary, if it
+    was collected at this batch and lane count."""
+    try:
+        with open(PMC_JSON) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if pmc.get("batch") != batch or pmc.get("lanes", 1) != lanes:
+        return None
+    tot: dict = {}
+    for name, ctr in pmc.get("kernels", {}).items():
+        if any(k in name for k in STAGE_KERNELS.get(stage, [])):
+            for k, v in ctr.items():
+                tot[k] = tot.get(k, 0.0) + v
+    return tot or None
+
+
+def measured_limiter(stage: str, batch: int, launch_ms: float, traffic: Optional[dict]) -> dict:
+    """Which roof the dominant kernel is nearest, from its measured counters: HBM (implementation bytes
+    per launch / launch time / peak) or VALU issue (wave-level VALU instructions x 2 cycles -- a wave64
+    VALU op holds its SIMD 2 cycles when two or more waves share it -- / (1,024 SIMDs x 2.4 GHz x launch
+    time)).  Neither near 1 = latency-bound (dependent LDS lookups / VALU chains)."""
+    ctr = pmc_counters(stage, batch, 1)
+    out = {"source": os.path.relpath(PMC_JSON, REPO) if ctr else None}
+    if not ctr or launch_ms <= 0:
+        out["verdict"] = "unmeasured (no PMC summary at this batch)"
+        return out
+    sec = launch_ms * 1e-3
+    hbm = (traffic or {}).get("bytes_per_launch", 0) / sec / (HBM_PEAK_GBS * 1e9) if traffic else None
+    valu = ctr.get("SQ_INSTS_VALU", 0.0) * 2 / (1024 * 2.4e9 * sec)
+    out.update({"hbm_traffic_frac": round(hbm, 4) if hbm is not None else None, "valu_issue_frac": round(valu, 4)})
+    best = max([("hbm", hbm or 0.0), ("valu_issue", valu)], key=lambda kv: kv[1])
+    out["verdict"] = best[0] if best[1] >= 0.7 else f"latency (nearest roof: {best[0]} at {best[1]:.2f})"
+    return out
+
+
 def _make_pool_image(i: int) -> bytes:
     from tests.golden.synth import encode_jpeg, synth_rgb
     return encode_jpeg(synth_rgb(np.random.default_rng(1234 + i), 640, 480), 90)
@@ -91,11 +128,21 @@ def _make_mixed_image(i: int) -> bytes:
     return encode_jpeg(synth_rgb(rng, w, h), 90)
 
 
+def _pool_map(fn, items, workers: int, chunksize: int = 1) -> list:
+    """map over spawn-started worker processes that are closed and joined (they exit normally; the
+    Pool context manager would terminate them, and SIGTERM handlers fire inside profiled runs)."""
+    p = mp.get_context("spawn").Pool(workers)
+    try:
+        return p.map(fn, items, chunksize=chunksize)
+    finally:
+        p.close()
+        p.join()
+
+
 def make_pool(n: int, workers: int, maker=_make_pool_image) -> list[bytes]:
     if workers <= 1:
         return [maker(i) for i in range(n)]
-    with mp.get_context("spawn").Pool(workers) as p:
-        return p.map(maker, range(n), chunksize=4)
+    return _pool_map(maker, range(n), workers, chunksize=4)
 
 
 # ---------------------------------------------------------------- CPU baseline (reference ops)
@@ -144,8 +191,7 @@ def cpu_baseline(paths: list[str], procs: int, seconds: float, res: int = 256, m
     if procs <= 1:
         n, dt = _cpu_worker((paths, seconds, res, mixed))
         return n / dt
-    with mp.get_context("spawn").Pool(procs) as p:
-        res_ = p.map(_cpu_worker, [(paths[k::procs] or paths, seconds, res, mixed) for k in range(procs)])
+    res_ = _pool_map(_cpu_worker, [(paths[k::procs] or paths, seconds, res, mixed) for k in range(procs)], procs)
     return sum(n for n, _ in res_) / max(dt for _, dt in res_)
 
 
@@ -154,6 +200,32 @@ def host_cores() -> int:
         return len(os.sched_getaffinity(0))
     except AttributeError:
         return os.cpu_count() or 1
+
+
+def cpu_share() -> tuple[int, str]:
+    """CPUs this process may use, and where that number comes from: the cgroup CPU quota (v2
+    cpu.max, v1 cfs_quota_us), else the thread share the box declares (OMP_NUM_THREADS: a GPU box
+    exports its per-GPU CPU share there, while nproc shows the whole machine), else nproc."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max" and int(per) > 0:
+            return max(1, int(q) // int(per)), "cgroup v2 cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0 and per > 0:
+            return max(1, q // per), "cgroup v1 cfs quota"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        return min(int(omp), host_cores()), "OMP_NUM_THREADS (the box's declared CPU share)"
+    return host_cores(), "nproc (sched_getaffinity)"
 
 
 # ---------------------------------------------------------------- multi-rank launcher
@@ -282,7 +354,7 @@ def main():
 
     from sds_amd.distributed import compute_index_slice, max_over_ranks
 
-    workers = max(1, min(BOX_CPU_SHARE, host_cores()) // max(1, world))
+    workers = max(1, cpu_share()[0] // max(1, world))
     pool = make_pool(args.pool, workers, _make_mixed_image if mixed else _make_pool_image)
 
     # this rank's slice of the R*N-row index: row i holds pool image i % POOL.  The slice is laid
@@ -486,7 +558,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not stub:
-        procs = min(BOX_CPU_SHARE, host_cores())
+        procs, procs_src = cpu_share()
         folder = tempfile.mkdtemp(prefix="sdsj_cpu_")
         try:
             paths = []
@@ -508,8 +580,8 @@ def main():
         cpu = {"value": round(vp, 1), "unit": "images/s", "cores": procs, "kind": "reference",
                "sample": f"PIL {__import__('PIL').__version__}/libjpeg-turbo pipeline (functional.py:94-110 op order: "
                          f"file read, open+convert RGB, {what}, {procs} processes x {args.cpu_seconds:.0f} s "
-                         f"(single process: {v1:.1f} images/s; {procs} = this box's CPU share, "
-                         f"{host_cores()} visible)",
+                         f"(single process: {v1:.1f} images/s; {procs} processes from {procs_src}, "
+                         f"{host_cores()} CPUs visible)",
                "single_core_value": round(v1, 1), "host": platform.processor() or platform.machine()}
 
     if rank == 0:
@@ -537,6 +609,8 @@ def main():
             "per_rank_images_per_s": [round(B * args.steps / t, 1) for t in per_rank],
             "process_group": {"backend": args.backend if world > 1 else None, "world_size": world_seen,
                               "gpus_visible": ndev if not stub else 0},
+            # bound: of the schema's roofs (HBM, MFMA) the path can only be priced against HBM -- it issues
+            # no MFMA; `limiter` says from the counters which roof (HBM bytes or VALU issue) it is nearest
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": (traffic or {}).get("bytes_per_launch"),
@@ -545,8 +619,7 @@ def main():
                          "algorithmic_bytes_per_image": round(alg_bytes_per_img, 1),
                          "launch_ms": round(launch_ms, 4), "images_per_launch": B, "lanes": 1,
                          "timing": "HIP events on the launch stream, single-lane pass after the timed region",
-                         "limiter": "not HBM: integer VALU issue and dependent-latency of the serial Huffman decode "
-                                    "and fixed-point resample (DESIGN.md §4)",
+                         "limiter": measured_limiter(dom, B, launch_ms, traffic),
                          "pipeline_achieved": round(value / world * alg_bytes_per_img / 1e9, 2)},
             "stage_ms_per_step_single_lane": {k: round(v / args.roofline_steps, 4) for k, v in stages.items()},
             "pixel_check": pixel_check,

@@ -14,9 +14,11 @@ on the training process's GPU:
 
 torch's default collate leaves ``bytes`` fields as a list, so ``batch[image_field]`` arrives as the
 B encoded images.  Values equal the per-sample pipeline's (presets.py:716-744) stacked the way
-default_collate stacks them.  A sample the reference would have failed on (its OSError makes
-``_iter_chunks_`` skip the sample, dataset.py:366-371) is dropped from every field of the batch
-(``on_error="drop"``), or raises (``"raise"``).
+default_collate stacks them.  Samples the JPEG kernels do not decode (other formats, CMYK / arithmetic
+/ 12-bit JPEG, streams reported damaged) rerun on PIL on the host (functional.py:94-100) and are
+resized on the GPU into their row of the batch.  A sample the reference would have failed on (PIL's
+OSError makes ``_iter_chunks_`` skip it, dataset.py:366-371) is dropped from every field of the batch
+(``on_error="drop"``), or its exception is raised (``"raise"``).
 """
 from __future__ import annotations
 
@@ -24,9 +26,10 @@ from typing import Any, Optional, Sequence
 
 import torch
 
+from . import _lib
 from . import functional as F
 from .engine import ImageDecodeError, UnsupportedImageError, get_engine, raise_for_status
-from .presets import LoadFromDiskTransform, SampleTransform
+from .presets import LoadFromDiskTransform, SampleTransform, _frames_to_device, pil_decode
 
 
 def create_deferred_image_pipeline(image_field: str) -> Sequence[SampleTransform]:
@@ -93,14 +96,31 @@ class GpuDecodeBatch:
         n = len(encoded)
         flip = [bool(torch.rand(1) < self.hflip_prob) for _ in range(n)] if self.hflip_prob > 0.0 else None
         kw = self.resize_kwargs
-        images, status = get_engine(self.device).decode_resize(
-            encoded, self.resolution, crop_before_resize=kw.get("crop_before_resize", True),
-            filter=F.filter_name(kw.get("interpolation_mode", "bilinear")), normalize=self.normalize, flip=flip)
-        keep = [i for i in range(n) if int(status[i]) == 0]
+        eng = get_engine(self.device)
+        opts = dict(crop_before_resize=kw.get("crop_before_resize", True),
+                    filter=F.filter_name(kw.get("interpolation_mode", "bilinear")), normalize=self.normalize)
+        images, status = eng.decode_resize(encoded, self.resolution, flip=flip, **opts)
+        errors: dict[int, BaseException] = {}
+        for i in range(n):
+            st = int(status[i])
+            if st in (_lib.UNSUPPORTED, _lib.CORRUPT):  # rerun on the reference's PIL decode
+                try:
+                    pil = pil_decode(encoded[i])
+                except Exception as e:  # noqa: BLE001 -- what PIL raises is what the reference raises
+                    errors[i] = e
+                    continue
+                frames = _frames_to_device([pil], images.device)
+                img, fst = eng.resize_frames(frames, self.resolution, flip=None if flip is None else [flip[i]], **opts)
+                raise_for_status(int(fst[0].item()), i)
+                images[i].copy_(img[0])
+                eng.note_fallback()
+                status[i] = _lib.OK
+            elif st != _lib.OK:
+                errors[i] = ImageDecodeError(st, i)
+        keep = [i for i in range(n) if i not in errors]
         if len(keep) < n:
             if self.on_error == "raise":
-                bad = next(i for i in range(n) if int(status[i]) != 0)
-                raise_for_status(int(status[bad]), bad)
+                raise errors[min(errors)]
             batch = {k: _select(v, keep, n) for k, v in batch.items()}
             images = images[torch.as_tensor(keep, dtype=torch.long, device=images.device)]
         if self.as_video:

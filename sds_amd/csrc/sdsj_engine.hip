@@ -217,7 +217,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   mark(6);
   if (!(e->skip >> 6 & 1)) SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(7);
-  if (!(e->skip >> 7 & 1)) SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
+  SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, ln.routes, cap, s, rm));
   mark(8);
   SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s, rm));
   mark(9);

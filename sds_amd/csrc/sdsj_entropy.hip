@@ -32,6 +32,7 @@
 #include <type_traits>
 
 #include "sdsj_common.h"
+#include "sdsj_idct.h"
 #include "sdsj_kernels.h"
 
 namespace sdsj {
@@ -65,6 +66,7 @@ struct EntTables {
   int32_t nslots;
   uint32_t pk_dc[2], pk_ac[2], pk_c;  // per MCU block: DC slot, AC slot (4 bits each), component (2)
   uint32_t pad[4];
+  uint16_t qtT[kMaxComp][64];  // each component's quantisation table, column-major (the write pass's IDCT)
 };
 static_assert(sizeof(EntTables) % 16 == 0, "EntTables is copied in 16-byte units");
 
@@ -114,7 +116,15 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restric
     T.pk_c = pc;
     T.pad[0] = T.pad[1] = T.pad[2] = T.pad[3] = 0;
   }
-  for (int i = t; i < 80; i += kEntThreads) T.nat[i] = (uint8_t)natural_order(i);
+  // the write pass assembles blocks column-major: natural_order transposed (row r, column c -> c * 8 + r)
+  for (int i = t; i < 80; i += kEntThreads) {
+    const int nz = natural_order(i);
+    T.nat[i] = (uint8_t)(((nz & 7) << 3) | (nz >> 3));
+  }
+  for (int i = t; i < kMaxComp * 64; i += kEntThreads) {
+    const int c = i >> 6, k = i & 63;
+    T.qtT[c][((k & 7) << 3) | (k >> 3)] = c < d->ncomp ? tb->qt[d->comp[c].tq][k] : (uint16_t)0;
+  }
   __syncthreads();
   const int ns = T.nslots;
   const int lb = (ns << 11) <= kLutEntries ? 11 : 10;  // the variant that will decode this image
@@ -930,32 +940,28 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
 // ------------------------------------------------------------------------------------------
 // k_entwrite
 // ------------------------------------------------------------------------------------------
-#ifndef SDSJ_COEF_SC1
-#define SDSJ_COEF_SC1 0
-#endif
-// A 16-byte coefficient store.  SDSJ_COEF_SC1: `sc1`, which drops the line from the XCD's L2 once
-// written (MI355X_MICROARCH.md: plain / nt stores keep it), so the coefficient stream does not
-// evict the bit readers' lines (k_idct reads the coefficients long after, from beyond L2 anyway).
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void store_coef16(void* p, uint4 v) {
-#if SDSJ_COEF_SC1
-  const u32x4_t x = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
-#else
-  *reinterpret_cast<uint4*>(p) = v;
-#endif
-}
+// The write pass inverse-transforms every block it completes (dequantisation + jpeg_idct_islow,
+// sdsj_idct.h) and stores its 64 samples into the block-linear plane: the coefficients never leave
+// LDS.  A lane assembles its current block in its staging area in COLUMN-major order (the transposed
+// natural order in T.nat), so column r of a block is one 16-byte LDS read.  Completed blocks join a
+// per-wave pending list; whenever it holds more than kQCap blocks, the wave transforms 8 of them at
+// once (8 lanes per block, idct_batch), and the rest wait in the wave's queue slots (copied out of
+// their owners' staging areas, which must be free for the owners' next blocks).
+constexpr int kWaves = kEntThreads / 64;
+constexpr int kQCap = 7;  // queued blocks per wave (< 8: a step's leftovers move in one 64-lane copy)
+
 template <class TT>
 struct LdsWriteT {
   unsigned long long t0, it;
   TT T;
   alignas(16) int16_t stage[(kEntThreads + 1) * kStageStride];  // + one shared sink block
-  uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
+  alignas(16) int16_t qdat[kWaves][kQCap][kStageStride];        // queued blocks (column-major)
+  alignas(16) uint16_t qt[kMaxComp][64];                         // quantisation tables, column-major
+  int32_t qmeta[kWaves][kQCap];                                  // their decode-order block indices
+  uint32_t flist[kWaves][64];  // this step's completed blocks: (lane << 24) | block index (total_blocks < 2^24)
+  BlkGeo X;
   int32_t bad;
   unsigned long long sym;
-#ifdef SDSJ_EXP_LDSPAD
-  uint8_t pad_exp[SDSJ_EXP_LDSPAD];  // (occupancy experiment)
-#endif
 };
 
 // The compact two-level tables from the image's LB = 11 tables (HBM).  The staging area serves as
@@ -1013,6 +1019,69 @@ __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tm
   return ns;
 }
 
+// Inverse transform of the pending entries [pos, pos + nb) (nb <= 8) of wave wv: its queue slots
+// [0, qn), then this step's flist (blocks still in their owners' staging areas).  8 lanes per block:
+// lane r reads column r (16 bytes), dequantises it and runs pass 1; the columns are transposed through
+// the block's own 128 bytes in two halves (rows 0-3, then 4-7); lane r runs pass 2 on row r and
+// stores its 8 samples, so a block leaves as one contiguous 64-byte run.  A staging area is left
+// zeroed for its owner's next block.  Lanes beyond nb work on the sink block and store nothing.
+template <class LW>
+__device__ __forceinline__ void idct_batch(LW& L, int wv, int lane, int qn, int pos, int nb, uint8_t* planes) {
+  const int gi = lane >> 3, r = lane & 7, e = pos + gi;
+  const bool valid = gi < nb;
+  int16_t* src = L.stage + kEntThreads * kStageStride;  // sink
+  int g = 0;
+  bool staged = false;
+  if (valid) {
+    if (e < qn) {
+      src = L.qdat[wv][e];
+      g = L.qmeta[wv][e];
+    } else {
+      const uint32_t f = L.flist[wv][e - qn];
+      src = L.stage + (wv * 64 + (int)(f >> 24)) * kStageStride;
+      g = (int)(f & 0xFFFFFFu);
+      staged = true;
+    }
+  }
+  const uint4 col = *reinterpret_cast<const uint4*>(src + r * 8);
+  int c = 0, off = 0;
+  const bool keep = valid && blk_locate(L.X, g, c, off);
+  const uint4 q = *reinterpret_cast<const uint4*>(&L.qt[c][r * 8]);
+  // DEQUANTIZE: coefficient (int16) x quantisation value (uint16)
+  int x[8];
+  {
+    const uint32_t cw[4] = {col.x, col.y, col.z, col.w}, qw[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      x[2 * k] = (int)(int16_t)(cw[k] & 0xFFFFu) * (int)(qw[k] & 0xFFFFu);
+      x[2 * k + 1] = (int)(int16_t)(cw[k] >> 16) * (int)(qw[k] >> 16);
+    }
+  }
+  int w[8];
+  islow_pass1(x, w);
+  // transpose: column r's outputs w[k] -> W[row k][column r], rows 0-3 then 4-7 in the block's 128 B
+  int* W = reinterpret_cast<int*>(src);
+  int row[8];
+  asm volatile("" ::: "memory");  // (the column reads above come first in the wave's LDS order)
+#pragma unroll
+  for (int k = 0; k < 4; k++) W[k * 8 + r] = w[k];
+  if (r < 4) {
+    const int4 a = reinterpret_cast<const int4*>(W)[r * 2], b = reinterpret_cast<const int4*>(W)[r * 2 + 1];
+    row[0] = a.x, row[1] = a.y, row[2] = a.z, row[3] = a.w, row[4] = b.x, row[5] = b.y, row[6] = b.z, row[7] = b.w;
+  }
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int k = 4; k < 8; k++) W[(k - 4) * 8 + r] = w[k];
+  if (r >= 4) {
+    const int4 a = reinterpret_cast<const int4*>(W)[(r - 4) * 2], b = reinterpret_cast<const int4*>(W)[(r - 4) * 2 + 1];
+    row[0] = a.x, row[1] = a.y, row[2] = a.z, row[3] = a.w, row[4] = b.x, row[5] = b.y, row[6] = b.z, row[7] = b.w;
+  }
+  asm volatile("" ::: "memory");
+  const uint2 px = islow_pass2(row);
+  if (keep) *reinterpret_cast<uint2*>(planes + off + r * 8) = px;
+  if (staged) *reinterpret_cast<uint4*>(src + r * 8) = make_uint4(0, 0, 0, 0);
+}
+
 template <int LB>
 __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                                uint8_t* __restrict__ scratch) {
@@ -1028,12 +1097,16 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   {
     uint4* z4 = reinterpret_cast<uint4*>(L.stage);
     for (int i = t; i < (kEntThreads + 1) * kStageStride * 2 / 16; i += kEntThreads) z4[i] = make_uint4(0, 0, 0, 0);
+    const uint4* gq = reinterpret_cast<const uint4*>(tables[img].qtT);
+    uint4* lq = reinterpret_cast<uint4*>(L.qt);
+    for (int i = t; i < (int)(sizeof(L.qt) / 16); i += kEntThreads) lq[i] = gq[i];
   }
   if (t == 0) {
     L.bad = 0;
     L.sym = 0;
     L.it = 0;
     if (kStats) L.t0 = __builtin_amdgcn_s_memtime();
+    blkgeo_init(d, L.X);
   }
   __syncthreads();
   const TT& T = L.T;
@@ -1041,11 +1114,12 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
   const SubState* sub = reinterpret_cast<const SubState*>(scratch + d->off_sub);
-  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
+  uint8_t* planes = scratch + d->off_planes;
   const int nsub = d->nsub;
   const int blocks_per_seg = d->restart_interval ? d->restart_interval * K.bpm : (int)d->total_blocks;
   const int my_base = t * kStageStride, sink_base = kEntThreads * kStageStride;
   int bad = 0;
+  int qn = 0;  // blocks in this wave's queue (wave-uniform)
   unsigned long long nsym = 0, witers = 0;
 
   const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
@@ -1087,7 +1161,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     while (__builtin_amdgcn_ballot_w64(run)) {
       if (run) bits_fill(b);
       for (;;) {
-#pragma unroll
+#pragma unroll 1
        for (int u = 0; u < kWriteGroup; u++) {
         if (kStats) witers++;
         bool ready = false;
@@ -1098,7 +1172,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
           if (kStats) nsym++;
           bad |= sb;
-          // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
+          // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r] (transposed)
           pc += isdc ? val : 0;
           const int wpos = T.nat[z + r];  // (natural_order[0] = 0 for the DC symbol)
           L.stage[((writing & (isdc | (s != 0))) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
@@ -1120,27 +1194,36 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           const bool more_mid = (b.pos < end_bit) | (z != 0);
           run = (g < gend) & (last_of_seg ? more_last : more_mid);
         }
-        // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
+        // the blocks completed in this step join the wave's pending list (queue, then flist); every
+        // full batch of 8 is transformed, the rest (< 8 in all) wait in the queue
         const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
         if (m) {
           const int cnt = __popcll(m);
           if (ready) {
             const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            L.flist[wv][idx] = ((uint32_t)t << 24) | gdone;
+            L.flist[wv][idx] = ((uint32_t)lane << 24) | gdone;
           }
           // (a wave's LDS accesses execute in issue order: the reads below see these writes, and the
           // owner's next stage writes land after the clears -- no waits beyond the data dependences)
           __builtin_amdgcn_wave_barrier();
-          for (int b0 = 0; b0 < cnt; b0 += 8) {
-            const int bi = b0 + (lane >> 3);
-            if (bi < cnt) {
-              const uint32_t f = L.flist[wv][bi];
-              uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
-              const uint4 v = *sp;
-              store_coef16(reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64) + (lane & 7), v);
-              *sp = make_uint4(0, 0, 0, 0);
-            }
+          const int total = qn + cnt;
+          int pos = 0;
+          while (total - pos > kQCap) {
+            const int nb = total - pos < 8 ? total - pos : 8;
+            idct_batch(L, wv, lane, qn, pos, nb, planes);
+            pos += nb;
           }
+          // leftovers -> queue slots (from slot 0 once a batch consumed the queue)
+          const int k0 = pos > 0 ? pos - qn : 0, dst0 = pos > 0 ? 0 : qn, nleft = cnt - k0;
+          const int gi = lane >> 3;
+          if (gi < nleft) {
+            const uint32_t f = L.flist[wv][k0 + gi];
+            uint4* sp = reinterpret_cast<uint4*>(L.stage + (wv * 64 + (int)(f >> 24)) * kStageStride) + (lane & 7);
+            reinterpret_cast<uint4*>(L.qdat[wv][dst0 + gi])[lane & 7] = *sp;
+            if ((lane & 7) == 0) L.qmeta[wv][dst0 + gi] = (int32_t)(f & 0xFFFFFFu);
+            *sp = make_uint4(0, 0, 0, 0);
+          }
+          qn = total - pos;
           __builtin_amdgcn_wave_barrier();
         }
        }
@@ -1150,10 +1233,11 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       }
     }
     if (active && last_of_seg) {
-      if (g < gend) sv.vend[s_int] = g;                     // the rest of the interval stays zero
+      if (g < gend) sv.vend[s_int] = g;                     // the rest of the interval stays zero (k_cutfill)
       if (b.pos > lim) sv.flag[s_int] |= kSegIns;          // ran out of data (JWRN_HIT_MARKER)
     }
   }
+  if (qn > 0) idct_batch(L, wv, lane, qn, 0, qn, planes);  // the wave's queued blocks
   if (bad) atomicOr(&L.bad, 1);  // bad Huffman codes: libjpeg warns and decodes symbol 0 (statistics only)
   if (kStats) {
     atomicAdd(&L.sym, nsym);
@@ -1164,6 +1248,51 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     d->sym_write = (int64_t)L.sym;
     d->it_write = (int64_t)L.it;
     d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - L.t0);
+  }
+}
+
+// k_cutfill: the blocks libjpeg leaves with zero coefficients -- samples of 128 after the IDCT --
+// when a restart interval runs out of data (jdhuff.c insufficient_data): from vend[k] to the end of
+// interval k, and all of an empty interval entered out of data.  The write pass stops decoding there;
+// this writes those blocks (the ones the crop reads) after it.  One wave per image, nothing to do for
+// an intact stream.
+__global__ void __launch_bounds__(64) k_cutfill(int n, const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.x, lane = threadIdx.x;
+  if (img >= n) return;
+  const ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || d->progressive || d->geo == kGeoZeros) return;
+  __shared__ BlkGeo X;
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+  const int nseg = d->nseg, total = (int)d->total_blocks;
+  const int bps = d->restart_interval ? d->restart_interval * d->bpm : total;
+  uint8_t* planes = scratch + d->off_planes;
+  bool geo = false;
+  for (int k0 = 0; k0 < nseg; k0 += 64) {
+    const int k = k0 + lane;
+    int z0 = 0, z1 = 0;
+    if (k < nseg) {
+      const int s0 = k * bps;
+      z1 = s0 + bps < total ? s0 + bps : total;
+      const bool whole = k > 0 && (sv.flag[k] & kSegEmpty) && (sv.flag[k - 1] & kSegIns);
+      z0 = whole ? s0 : (sv.vend[k] > s0 ? sv.vend[k] : s0);
+    }
+    uint64_t m = __builtin_amdgcn_ballot_w64(z1 > z0);
+    if (!m) continue;
+    if (!geo) {
+      if (lane == 0) blkgeo_init(d, X);
+      __syncthreads();
+      geo = true;
+    }
+    while (m) {
+      const int q = __builtin_ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int a = __shfl(z0, q), e = __shfl(z1, q);
+      for (int gb = a + (lane >> 2); gb < e; gb += 16) {  // 4 lanes per block, 16 bytes each
+        int c, off;
+        if (blk_locate(X, gb, c, off))
+          reinterpret_cast<uint4*>(planes + off)[lane & 3] = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+      }
+    }
   }
 }
 
@@ -1281,6 +1410,8 @@ hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scr
                        scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
     hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  if (route_on(rm, kRtEnt11) || route_on(rm, kRtEnt11M) || route_on(rm, kRtEnt10))
+    hipLaunchKernelGGL(k_cutfill, dim3(n), dim3(64), 0, s, n, descs, scratch);
   return hipGetLastError();
 }
 

@@ -30,11 +30,10 @@ class ImageDecodeError(OSError):
 
 
 class UnsupportedImageError(ImageDecodeError):
-    """A valid image the MI355X path does not decode: a format other than JPEG (PNG, WebP, GIF, ... --
-    everything else in sds/structs.py:42 IMAGE_EXT), or an arithmetic-coded / 12-bit / lossless /
-    CMYK JPEG.  This is a documented divergence from functional.py:94-100 (PIL decodes them): the
-    sample raises this OSError, so sds's skip handler drops it (dataset.py:366-371), and the engine's
-    ``unsupported`` counter records it."""
+    """A valid image the MI355X JPEG kernels do not decode: a format other than JPEG (PNG, WebP, GIF,
+    ... -- everything else in sds/structs.py:42 IMAGE_EXT), or an arithmetic-coded / 12-bit / lossless
+    / CMYK JPEG (status UNSUPPORTED).  The transforms (presets.py, batched.py) rerun such samples on
+    PIL (functional.py:94-100) instead of raising; the raw engine API reports the status."""
 
 
 def raise_for_status(status: int, index: int = 0) -> None:
@@ -72,6 +71,7 @@ class JpegEngine:
         self._h = h
         self._pid = os.getpid()
         self._inflight: dict[int, tuple[torch.Tensor, int]] = {}
+        self._fallback = 0  # samples the transforms decoded with PIL on the host (counters()["fallback"])
 
     # -- lifetime --------------------------------------------------------------------------
     def close(self) -> None:
@@ -299,7 +299,16 @@ class JpegEngine:
         buf = (ctypes.c_uint64 * _lib.NUM_COUNTERS)()
         self._check(self.lib.sdsj_engine_counters(self._h, buf, _lib.NUM_COUNTERS, int(bool(reset))),
                     "sdsj_engine_counters")
-        return {self.lib.sdsj_counter_name(k).decode(): int(buf[k]) for k in range(_lib.NUM_COUNTERS)}
+        out = {self.lib.sdsj_counter_name(k).decode(): int(buf[k]) for k in range(_lib.NUM_COUNTERS)}
+        out["fallback"] = self._fallback
+        if reset:
+            self._fallback = 0
+        return out
+
+    def note_fallback(self, n: int = 1) -> None:
+        """Counts samples decoded by PIL on the host and resized by this engine (the transforms' rerun of
+        UNSUPPORTED / CORRUPT samples)."""
+        self._fallback += int(n)
 
     def set_lanes(self, lanes: int) -> None:
         """Kernel lanes per batch (1..4; see include/sdsj.h)."""

@@ -8,9 +8,15 @@ leaves a device tensor in ``sample[output_field]``.
 
 Transforms are plain picklable classes (presets.py:1-5): the native engine is created lazily in
 the process that first calls them (a DataLoader worker after fork), never pickled.
+
+Samples the MI355X JPEG path does not decode (other IMAGE_EXT formats, sds/structs.py:42; arithmetic /
+12-bit / lossless / CMYK JPEG; streams it reports damaged) rerun on the reference's own PIL decode on the
+host and are then cropped / resized on the GPU; PIL's exceptions propagate unchanged,
+so sds's skip / retry handling (dataset.py:212-226, :366-371) sees what the reference raises.
 """
 from __future__ import annotations
 
+import io
 import logging
 import os
 from typing import Any, Callable, Optional, Sequence
@@ -18,25 +24,47 @@ from typing import Any, Callable, Optional, Sequence
 import numpy as np
 import torch
 
+from . import _lib
 from . import functional as F
-from .engine import UnsupportedImageError, get_engine, raise_for_status
+from .engine import ImageDecodeError, get_engine, raise_for_status
 
 log = logging.getLogger("sds_amd")
-_unsupported_seen = {"pid": None, "n": 0}
+_fallback_seen = {"pid": None, "n": 0}
 
 
-def _note_unsupported(data: bytes, field: str) -> str:
-    """Logs (first time per process, then every 1,000th) a sample this path does not decode; returns
-    the format name for the error message (the drop is a documented divergence: DESIGN.md §7)."""
-    fmt = F.sniff_format(data)
-    if _unsupported_seen["pid"] != os.getpid():
-        _unsupported_seen.update(pid=os.getpid(), n=0)
-    _unsupported_seen["n"] += 1
-    n = _unsupported_seen["n"]
+def _note_fallback(data: bytes, field: str) -> None:
+    """Logs (first time per process, then every 1,000th) a sample decoded on the host."""
+    if _fallback_seen["pid"] != os.getpid():
+        _fallback_seen.update(pid=os.getpid(), n=0)
+    _fallback_seen["n"] += 1
+    n = _fallback_seen["n"]
     if n == 1 or n % 1000 == 0:
-        log.warning("sds_amd: field %r holds a %s image, which the MI355X path does not decode (sample skipped as "
-                    "by sds's transform-error handler; %d such samples in this process so far)", field, fmt, n)
-    return fmt
+        log.info("sds_amd: field %r holds a %s image, decoded by PIL on the host and resized on the GPU "
+                 "(%d such samples in this process so far)", field, F.sniff_format(data), n)
+
+
+def pil_decode(data: bytes):
+    """functional.py:94-100 load_image_from_bytes: ``Image.open(...).convert('RGB')`` -- the reference's
+    own decode, run on the host for the samples the MI355X JPEG path does not decode (other formats,
+    arithmetic / 12-bit / lossless / CMYK JPEG, streams it reports damaged).  Raises what PIL raises."""
+    from PIL import Image
+    return Image.open(io.BytesIO(data)).convert("RGB")
+
+
+class _RngSnapshot:
+    """The global RNG states a transform may draw from (np for random_resize, torch for the hflip
+    coin), so that a sample whose GPU decode must be redone on the host draws in the reference's order:
+    the reference draws only after its decode succeeded (functional.py:69-74, README.md:99-108)."""
+
+    def __init__(self, np_rng: bool, torch_rng: bool):
+        self.np_state = np.random.get_state() if np_rng else None
+        self.torch_state = torch.get_rng_state() if torch_rng else None
+
+    def restore(self) -> None:
+        if self.np_state is not None:
+            np.random.set_state(self.np_state)
+        if self.torch_state is not None:
+            torch.set_rng_state(self.torch_state)
 
 
 def _engine_in_worker(device):
@@ -165,29 +193,58 @@ class GpuDecodeResizeImageTransform(BaseTransform):
             raise TypeError(f"Field '{self.input_field}' must hold encoded image bytes, got {type(data)}")
         data = bytes(data)
         kw = self.resize_kwargs
-        resolution = self.resolution
-        if kw.get("allow_vertical") or kw.get("random_resize") is not None:
-            w, h = F.image_size(data)
-            resolution = F.target_resolution(w, h, self.resolution, kw.get("allow_vertical", False),
-                                             kw.get("random_resize"))
-        flip = None
-        if self.hflip_prob > 0.0:
-            flip = [bool(torch.rand(1) < self.hflip_prob)]
         eng = _engine_in_worker(self.device)
+        need_size = bool(kw.get("allow_vertical")) or kw.get("random_resize") is not None
+        resolution = self.resolution
+        if need_size:
+            st, info = _lib.probe(data)
+            if st != _lib.OK or info.width <= 0 or info.height <= 0:  # not a JPEG this path decodes
+                img = self._host(eng, data)
+                sample[self.output_field] = img.permute(2, 0, 1)
+                return sample
+            resolution = F.target_resolution(int(info.width), int(info.height), self.resolution,
+                                             kw.get("allow_vertical", False), kw.get("random_resize"))
+        rng = _RngSnapshot(kw.get("random_resize") is not None, self.hflip_prob > 0.0)
+        flip = [bool(torch.rand(1) < self.hflip_prob)] if self.hflip_prob > 0.0 else None
         out, status = eng.decode_resize([data], resolution, crop_before_resize=kw.get("crop_before_resize", True),
                                         filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),
                                         normalize=self.normalize, flip=flip, layout="hwc")
-        try:
-            raise_for_status(int(status[0]))
-        except UnsupportedImageError as e:
-            fmt = _note_unsupported(data, self.input_field)
-            raise UnsupportedImageError(e.status, 0, f"field {self.input_field!r}: {fmt} input is not decoded by the "
-                                                     f"MI355X JPEG path (documented divergence, DESIGN.md §7)") from None
-        img = out[0]
+        st = int(status[0])
+        if st == _lib.OK:
+            img = out[0]
+        elif st in (_lib.UNSUPPORTED, _lib.CORRUPT):
+            # the sample reruns on the reference's own PIL decode (bit-exact by
+            # definition); PIL raises for what it cannot decode, as functional.py:100 would
+            rng.restore()
+            img = self._host(eng, data)
+        else:
+            raise_for_status(st)
         if self.output_device is not None and self.output_device != img.device:
             img = img.to(self.output_device)
         sample[self.output_field] = img.permute(2, 0, 1)  # [3, h, w] view of HWC storage
         return sample
+
+    def _host(self, eng, data: bytes) -> torch.Tensor:
+        """PIL decode on the host (functional.py:94-100), then the same crop / resize / flip / layout /
+        normalise on the GPU through the frame path (pinned bit-exact to PIL.Image.resize); returns the
+        [h, w, 3] HWC tensor.  The RNG draws follow the decode, as in the reference."""
+        kw = self.resize_kwargs
+        pil = pil_decode(data)
+        w, h = pil.size
+        resolution = F.target_resolution(w, h, self.resolution, kw.get("allow_vertical", False),
+                                         kw.get("random_resize"))
+        flip = [bool(torch.rand(1) < self.hflip_prob)] if self.hflip_prob > 0.0 else None
+        frames = _frames_to_device([pil], torch.device("cuda", eng.device))
+        out, status = eng.resize_frames(frames, resolution, crop_before_resize=kw.get("crop_before_resize", True),
+                                        filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),
+                                        normalize=self.normalize, flip=flip, layout="hwc")
+        raise_for_status(int(status[0].item()))
+        eng.note_fallback()
+        _note_fallback(data, self.input_field)
+        img = out[0]
+        if self.output_device is not None and self.output_device != img.device:
+            img = img.to(self.output_device)
+        return img
 
 
 def _frames_to_device(frames, device) -> torch.Tensor:

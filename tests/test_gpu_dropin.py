@@ -105,29 +105,66 @@ def test_output_device_cpu_returns_the_reference_type():
     assert G.sha(s["image"].contiguous().numpy()) == meta["images"][0]["u8_256_sha256"]
 
 
-def test_png_sample_is_counted_and_reported_not_silently_dropped(caplog):
-    """A PNG in the image field (sds/structs.py:42 IMAGE_EXT lists it): the MI355X path does not decode it.
-    The transform raises UnsupportedImageError (an OSError, so sds skips the sample as it skips any
-    transform error, dataset.py:366-371), logs it, and the engine counts it."""
-    import io
+def _g6():
+    meta = G.load_json("g6_fallback.json")
+    z = np.load(os.path.join(G.GOLDEN, "g6_fallback.npz"))
+    return meta, z
 
-    from PIL import Image
 
-    from sds_amd.engine import UnsupportedImageError, get_engine
+def test_fallback_samples_match_reference_g6():
+    """SURVEY.md §8(b) UNSUPPORTED / CORRUPT contract: PNG (RGB, RGBA, L, P), WebP, GIF, BMP, TIFF, a
+    CMYK JPEG and a JPEG without EOI (which the GPU parser reports truncated, and Pillow decodes) rerun on
+    PIL on the host and are resized on the GPU: equal to the reference pipeline's outputs (G6, made by
+    tests/golden/make_fallback.py from the reference itself) in every variant (two resolutions,
+    normalize, crop_before_resize=False); samples the reference fails on raise its OSError."""
+    from sds_amd.engine import get_engine
     from sds_amd.presets import create_standard_image_pipeline
-    buf = io.BytesIO()
-    Image.fromarray(np.zeros((20, 30, 3), np.uint8)).save(buf, format="PNG")
-    p = _write(tempfile.mkdtemp(), "0.png", buf.getvalue())
+    meta, z = _g6()
     eng = get_engine("cuda")
     before = eng.counters()
-    with caplog.at_level("WARNING", logger="sds_amd"):
-        with pytest.raises(UnsupportedImageError, match="PNG"):
-            _run(create_standard_image_pipeline("png", (64, 64), device="cuda"), {"png": p})
+    tmp = tempfile.mkdtemp()
+    n_ok = 0
+    for case in meta["cases"]:
+        data = z[f"{case['name']}__bytes"].tobytes()
+        p = _write(tmp, case["name"], data)
+        for vname, res, kw in meta["variants"]:
+            ref = case["variants"][vname]
+            ts = create_standard_image_pipeline("img", tuple(res), device="cuda", **kw)
+            if not ref["ok"]:
+                with pytest.raises(OSError):
+                    _run(ts, {"img": p})
+                continue
+            img = _run(ts, {"img": p})["image"]
+            assert img.device.type == "cuda" and list(img.shape) == ref["shape"], (case["name"], vname)
+            assert str(img.dtype).replace("torch.", "") == ref["dtype"]
+            h, w = ref["shape"][1:]
+            assert img.stride() == (1, w * 3, 3)  # HWC storage viewed as CHW, as the reference's tensor
+            got = img.cpu().contiguous().numpy()
+            if f"{case['name']}__{vname}" in z.files:
+                np.testing.assert_array_equal(got, z[f"{case['name']}__{vname}"], err_msg=f"{case['name']} {vname}")
+            assert G.sha(got) == ref["sha256"], (case["name"], vname)
+            n_ok += 1
     after = eng.counters()
-    assert after["unsupported"] == before["unsupported"] + 1
-    assert after["images"] == before["images"] + 1
-    assert after["bytes_in"] == before["bytes_in"] + len(buf.getvalue())
-    assert any("PNG" in r.getMessage() for r in caplog.records)
+    assert n_ok >= 40
+    assert after["fallback"] - before["fallback"] == n_ok
+
+
+def test_fallback_in_gpu_decode_batch():
+    """f1 (sds_amd.batched.GpuDecodeBatch): a collated batch mixing JPEGs with G6 samples -- the fallback
+    rows equal the reference's images, the sample the reference fails on is dropped from every field."""
+    from sds_amd.batched import GpuDecodeBatch
+    meta, z = _g6()
+    _, jpgs = G.g2_jpegs()
+    names = ["png_rgb_64x48", "png_truncated", "jpeg_cmyk_48x32", "webp_64x48", "jpeg_no_eoi_64x48"]
+    enc = [jpgs[0]] + [z[f"{n}__bytes"].tobytes() for n in names] + [jpgs[1]]
+    batch = {"img": enc, "index": torch.arange(len(enc))}
+    out = GpuDecodeBatch("img", (32, 32), device="cuda")(batch)
+    assert out["index"].tolist() == [0, 1, 3, 4, 5, 6]
+    imgs = out["image"].cpu().numpy()
+    for row, n in zip(imgs[1:5], [names[0], names[2], names[3], names[4]]):
+        np.testing.assert_array_equal(row, z[f"{n}__r32"], err_msg=n)
+    with pytest.raises(OSError):
+        GpuDecodeBatch("img", (32, 32), device="cuda", on_error="raise")({"img": enc})
 
 
 def _case(name):

@@ -143,3 +143,38 @@ def test_oracle_progressive_damaged_status_matches_pil():
                 except O.OracleError:
                     oracle_ok = False
                 assert pil_ok == oracle_ok, (seed, kind)
+
+
+def test_oracle_frame_resize_matches_g6_fallback_goldens():
+    """G6 (tests/golden/make_fallback.py, made by the reference pipeline itself): for the samples the
+    GPU JPEG kernels hand to PIL (PNG / WebP / GIF / BMP / TIFF / CMYK JPEG / JPEG without EOI), PIL's
+    decode followed by the oracle's crop (functional.py:118-147) + resize (Pillow Resample.c) -- the
+    checker of the GPU frame path that resizes them -- equals the reference's uint8 outputs."""
+    import io
+    import os
+
+    from PIL import Image
+    meta = G.load_json("g6_fallback.json")
+    z = np.load(os.path.join(G.GOLDEN, "g6_fallback.npz"))
+    checked = 0
+    for case in meta["cases"]:
+        data = z[f"{case['name']}__bytes"].tobytes()
+        for vname, res, kw in meta["variants"]:
+            key = f"{case['name']}__{vname}"
+            if not case["variants"][vname]["ok"]:
+                with pytest.raises(OSError):
+                    Image.open(io.BytesIO(data)).convert("RGB")
+                continue
+            if key not in z.files:  # (float outputs are pinned by digest on the GPU side)
+                continue
+            rgb = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
+            h, w = rgb.shape[:2]
+            out_h, out_w = res
+            if (w, h) != (out_w, out_h):
+                if kw.get("resize_kwargs", {}).get("crop_before_resize", True):
+                    x0, y0, x1, y1 = O.crop_box(w, h, out_h, out_w)
+                    rgb = rgb[y0:y1, x0:x1]
+                rgb = O.resize(rgb, out_h, out_w)
+            np.testing.assert_array_equal(rgb.transpose(2, 0, 1), z[key], err_msg=key)
+            checked += 1
+    assert checked >= 30
