@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SDSJ_ABI_VERSION 1
+#define SDSJ_ABI_VERSION 2 /* 2: blob_bytes on the device entry point */
 
 /* status codes (per call and per sample) */
 #define SDSJ_OK 0
@@ -109,12 +109,14 @@ int sdsj_decode_resize_batch(sdsj_engine* eng, int n, const uint8_t* const* jpg,
                              const sdsj_op* op, const uint8_t* flip, void* out, int32_t* status,
                              void* hip_stream);
 
-/* Same with inputs already in DEVICE memory: sample i is d_blob[d_offsets[i] .. + d_lengths[i]).
- * d_flip (n bytes) may be NULL; d_status is a device array of n ints.  Fully asynchronous on
- * `hip_stream` (no host synchronisation, capturable into a hipGraph for a fixed n). */
-int sdsj_decode_resize_batch_device(sdsj_engine* eng, int n, const uint8_t* d_blob, const int64_t* d_offsets,
-                                    const int32_t* d_lengths, const sdsj_op* op, const uint8_t* d_flip,
-                                    void* d_out, int32_t* d_status, void* hip_stream);
+/* Same with inputs already in DEVICE memory: sample i is d_blob[d_offsets[i] .. + d_lengths[i]) of the
+ * blob_bytes-byte buffer d_blob; a sample whose range is negative or leaves the buffer reports
+ * SDSJ_EINVAL (checked on the device before anything reads it).  d_flip (n bytes) may be NULL;
+ * d_status is a device array of n ints.  Fully asynchronous on `hip_stream` (no host
+ * synchronisation, capturable into a hipGraph for a fixed n). */
+int sdsj_decode_resize_batch_device(sdsj_engine* eng, int n, const uint8_t* d_blob, size_t blob_bytes,
+                                    const int64_t* d_offsets, const int32_t* d_lengths, const sdsj_op* op,
+                                    const uint8_t* d_flip, void* d_out, int32_t* d_status, void* hip_stream);
 
 /* Asynchronous host path with double-buffered pinned staging (downloader /
  * host cache -> pinned staging -> H2D -> decode, overlapped; config 5).  Up to SDSJ_SLOTS batches are

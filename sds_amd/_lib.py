@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # SDSJ_LIBRARY: an alternative in-tree build (kernel experiments under tools/); default = the product
 LIB_PATH = os.environ.get("SDSJ_LIBRARY") or os.path.join(_HERE, "lib", "libsdsj.so")
 
-SDSJ_ABI_VERSION = 1
+SDSJ_ABI_VERSION = 2
 OK, EINVAL, UNSUPPORTED, CORRUPT, ENOMEM, EHIP, ECAPACITY = 0, -1, -2, -3, -4, -5, -6
 STATUS_NAMES = {OK: "OK", EINVAL: "EINVAL", UNSUPPORTED: "UNSUPPORTED", CORRUPT: "CORRUPT", ENOMEM: "ENOMEM",
                 EHIP: "EHIP", ECAPACITY: "ECAPACITY"}
@@ -87,7 +87,7 @@ def load() -> ctypes.CDLL:
         lib.sdsj_decode_resize_batch.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                                  ctypes.POINTER(sz), ctypes.POINTER(SdsjOp), vp, vp,
                                                  ctypes.POINTER(i32), vp]
-        lib.sdsj_decode_resize_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, ctypes.POINTER(SdsjOp), vp, vp,
+        lib.sdsj_decode_resize_batch_device.argtypes = [vp, ctypes.c_int, vp, sz, vp, vp, ctypes.POINTER(SdsjOp), vp, vp,
                                                         vp, vp]
         lib.sdsj_resize_frames_device.argtypes = [vp, ctypes.c_int, vp, i32, i32, i64, ctypes.POINTER(SdsjOp), vp, vp,
                                                   vp, vp]

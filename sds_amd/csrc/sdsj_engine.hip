@@ -40,7 +40,6 @@ struct sdsj_engine {
   int64_t capacity = 0;
   bool grow = true;
   int warm_bits = -1;  // entropy warm-up override (SDSJ_WARM_BITS, experiments); < 0 = plan default
-  int skip = 0;        // SDSJ_SKIP_STAGES (timing experiments only: bit k skips mark-k's stage; outputs invalid)
   uint8_t* scratch = nullptr;
   ImgDesc* descs = nullptr;
   ImgTables* tables = nullptr;
@@ -59,7 +58,6 @@ struct sdsj_engine {
   int32_t* h_froutes = nullptr;
   float* d_lut = nullptr;
   unsigned long long* d_counters = nullptr;  // SDSJ_CTR_* (k_finish)
-  int64_t host_ctr_adj[SDSJ_NUM_COUNTERS] = {};  // host-side corrections (unreadable files)
   // host-bytes path
   uint8_t* h_stage = nullptr;
   size_t h_stage_cap = 0;
@@ -183,7 +181,7 @@ struct Lane {
 
 // Runs the kernel sequence for one lane (n <= max_batch images) of device-resident inputs.
 // after_spec (optional) is recorded once the lane's speculative entropy pass is queued.
-int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const int64_t* d_offsets,
+int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, int64_t blob_bytes, const int64_t* d_offsets,
              const int32_t* d_lengths, const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status,
              hipStream_t s, hipEvent_t after_spec, uint64_t rm) {
   std::vector<hipEvent_t>* evs = nullptr;
@@ -200,7 +198,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
     if (after_spec && (e->lane_mid == k || (e->lane_mid < 0 && k == kMarkAfterSpec))) (void)hipEventRecord(after_spec, s);
   };
   mark(0);
-  SDSJ_HIP(e, launch_parse(n, d_blob, d_offsets, d_lengths, op, e->warm_bits, ln.descs, ln.tables, s));
+  SDSJ_HIP(e, launch_parse(n, d_blob, blob_bytes, d_offsets, d_lengths, op, e->warm_bits, ln.descs, ln.tables, s));
   mark(1);
   const int cap = e->max_batch;
   SDSJ_HIP(e, launch_plan(n, ln.descs, e->capacity, ln.base, ln.total, ln.routes, cap, s));
@@ -211,11 +209,11 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   // (after mark 3: the next lane may start while this lane's progressive images decode)
   SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s, rm));
   mark(4);
-  if (!(e->skip >> 4 & 1)) SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(5);
-  if (!(e->skip >> 5 & 1)) SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(6);
-  if (!(e->skip >> 6 & 1)) SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(7);
   SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, ln.routes, cap, s, rm));
   mark(8);
@@ -227,8 +225,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
   mark(11);
   SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s, rm));
   mark(12);
-  if (!(e->skip >> 12 & 1))
-    SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s, rm));
+  SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s, rm));
   SDSJ_HIP(e, launch_finish(n, ln.descs, op, d_out, d_status, e->d_lut, d_lengths, e->d_counters, s));
   mark(13);
   return SDSJ_OK;
@@ -244,13 +241,14 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, const
 constexpr int kLaneMin = 128;
 
 // rm: the routes the chunk's images may take (host planning), or kAllRoutes
-int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_offsets, const int32_t* d_lengths,
+int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, int64_t blob_bytes, const int64_t* d_offsets, const int32_t* d_lengths,
               const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status, hipStream_t s,
               uint64_t rm = kAllRoutes) {
   int nl = std::min(std::max(e->lanes, 1), kMaxLanes);
   while (nl > 1 && n < nl * kLaneMin) nl--;
   const Lane first{e->descs, e->tables, e->d_etab, e->d_routes, e->d_total, nullptr};
-  if (nl == 1) return run_lane(e, first, n, d_blob, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr, rm);
+  if (nl == 1)
+    return run_lane(e, first, n, d_blob, blob_bytes, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr, rm);
   for (int k = 0; k + 1 < nl; k++)
     if (!e->aux[k]) {
       SDSJ_HIP(e, hipStreamCreateWithFlags(&e->aux[k], hipStreamNonBlocking));
@@ -268,7 +266,7 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_off
                                   k == 1 ? e->d_total : e->d_totals_x + (k - 2)};
     hipStream_t ls = k == 0 ? s : e->aux[k - 1];
     if (k > 0) SDSJ_HIP(e, hipStreamWaitEvent(ls, e->ev_mid[k - 1], 0));
-    int st = run_lane(e, ln, i1 - i0, d_blob, d_offsets + i0, d_lengths + i0, op, d_flip ? d_flip + i0 : nullptr,
+    int st = run_lane(e, ln, i1 - i0, d_blob, blob_bytes, d_offsets + i0, d_lengths + i0, op, d_flip ? d_flip + i0 : nullptr,
                       static_cast<uint8_t*>(d_out) + i0 * ob, d_status + i0, ls,
                       k + 1 < nl ? e->ev_mid[k] : nullptr, rm);
     if (st != SDSJ_OK) return st;
@@ -403,7 +401,7 @@ int slot_launch(sdsj_engine* e, Slot& sl, int n, size_t bytes, const sdsj_op& op
   SDSJ_HIP(e, hipMemcpyAsync(sl.d_flip, sl.h_flip, n, hipMemcpyHostToDevice, cs));
   SDSJ_HIP(e, hipEventRecord(sl.ev_h2d, cs));
   SDSJ_HIP(e, hipStreamWaitEvent(s, sl.ev_h2d, 0));
-  const int rc = run_chunk(e, n, sl.d_blob, sl.d_offsets, sl.d_lengths, op, sl.d_flip, out, sl.d_status, s, rmask.load());
+  const int rc = run_chunk(e, n, sl.d_blob, (int64_t)bytes, sl.d_offsets, sl.d_lengths, op, sl.d_flip, out, sl.d_status, s, rmask.load());
   if (rc != SDSJ_OK) return rc;
   SDSJ_HIP(e, hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
   SDSJ_HIP(e, hipEventRecord(sl.ev_done, s));
@@ -501,7 +499,7 @@ int sdsj_submit_files(sdsj_engine* e, int slot, int n, const char* const* paths,
   parallel_for(n, [&](int i0, int i1) {
     for (int i = i0; i < i1; i++) {
       const bool ok = sizes[i] >= 0 && read_file(paths[i], sl.h_stage + sl.h_offsets[i], sizes[i]);
-      sl.h_lengths[i] = ok ? (int32_t)sizes[i] : 0;
+      sl.h_lengths[i] = ok ? (int32_t)sizes[i] : -1;  // (k_finish reports a negative length as EINVAL, counted "other")
       sl.h_pre[i] = ok ? SDSJ_OK : SDSJ_EINVAL;
     }
   });
@@ -520,13 +518,8 @@ int sdsj_wait_batch(sdsj_engine* e, int slot, int32_t* status) {
   Slot& sl = e->slots[slot];
   SDSJ_HIP(e, hipEventSynchronize(sl.ev_done));
   sl.pending = false;
-  for (int i = 0; i < sl.n; i++) {
-    if (status) status[i] = sl.h_pre[i] != SDSJ_OK ? sl.h_pre[i] : sl.h_status[i];
-    if (sl.h_pre[i] != SDSJ_OK) {  // the device decoded an empty sample (CORRUPT): count it as unreadable
-      e->host_ctr_adj[SDSJ_CTR_CORRUPT]--;
-      e->host_ctr_adj[SDSJ_CTR_OTHER]++;
-    }
-  }
+  if (status)  // (an unreadable file went to the device with length -1: k_finish reports it EINVAL)
+    for (int i = 0; i < sl.n; i++) status[i] = sl.h_pre[i] != SDSJ_OK ? sl.h_pre[i] : sl.h_status[i];
   return SDSJ_OK;
 }
 
@@ -575,7 +568,6 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   if (!e) return SDSJ_ENOMEM;
   e->device = hip_device;
   if (const char* w = getenv("SDSJ_WARM_BITS")) e->warm_bits = atoi(w);
-  if (const char* w = getenv("SDSJ_SKIP_STAGES")) e->skip = atoi(w);
   if (cfg && cfg->max_batch > 0) e->max_batch = cfg->max_batch;
   DeviceGuard g(hip_device);
   int st = SDSJ_OK;
@@ -657,9 +649,9 @@ int sdsj_engine_destroy(sdsj_engine* e) {
   return SDSJ_OK;
 }
 
-int sdsj_decode_resize_batch_device(sdsj_engine* e, int n, const uint8_t* d_blob, const int64_t* d_offsets,
-                                    const int32_t* d_lengths, const sdsj_op* op, const uint8_t* d_flip, void* d_out,
-                                    int32_t* d_status, void* hip_stream) {
+int sdsj_decode_resize_batch_device(sdsj_engine* e, int n, const uint8_t* d_blob, size_t blob_bytes,
+                                    const int64_t* d_offsets, const int32_t* d_lengths, const sdsj_op* op,
+                                    const uint8_t* d_flip, void* d_out, int32_t* d_status, void* hip_stream) {
   if (!e) return SDSJ_EINVAL;
   if (n < 0 || (n > 0 && (!d_blob || !d_offsets || !d_lengths || !d_out || !d_status)) || !valid_op(op))
     return fail(e, SDSJ_EINVAL, "invalid argument");
@@ -673,7 +665,7 @@ int sdsj_decode_resize_batch_device(sdsj_engine* e, int n, const uint8_t* d_blob
   const int64_t ob = out_bytes_per_image(*op);
   for (int c0 = 0; c0 < n; c0 += e->max_batch) {
     int m = std::min(e->max_batch, n - c0);
-    int st = run_chunk(e, m, d_blob, d_offsets + c0, d_lengths + c0, *op, d_flip ? d_flip + c0 : nullptr,
+    int st = run_chunk(e, m, d_blob, (int64_t)blob_bytes, d_offsets + c0, d_lengths + c0, *op, d_flip ? d_flip + c0 : nullptr,
                        reinterpret_cast<uint8_t*>(d_out) + c0 * ob, d_status + c0, s);
     if (st != SDSJ_OK) return st;
   }
@@ -737,7 +729,7 @@ int sdsj_decode_resize_batch(sdsj_engine* e, int n, const uint8_t* const* jpg, c
     SDSJ_HIP(e, hipMemcpyAsync(e->d_offsets, e->h_offsets, sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
     SDSJ_HIP(e, hipMemcpyAsync(e->d_lengths, e->h_lengths, sizeof(int32_t) * m, hipMemcpyHostToDevice, s));
     SDSJ_HIP(e, hipMemcpyAsync(e->d_flip, e->h_flip, m, hipMemcpyHostToDevice, s));
-    rc = run_chunk(e, m, e->d_blob, e->d_offsets, e->d_lengths, *op, e->d_flip,
+    rc = run_chunk(e, m, e->d_blob, off, e->d_offsets, e->d_lengths, *op, e->d_flip,
                    reinterpret_cast<uint8_t*>(out) + c0 * ob, e->d_status, s, rm);
     if (rc != SDSJ_OK) return rc;
     SDSJ_HIP(e, hipMemcpyAsync(e->h_status, e->d_status, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s));
@@ -857,10 +849,9 @@ int sdsj_engine_counters(sdsj_engine* e, uint64_t* out, int cap, int reset) {
   unsigned long long h[SDSJ_NUM_COUNTERS];
   SDSJ_HIP(e, hipDeviceSynchronize());
   SDSJ_HIP(e, hipMemcpy(h, e->d_counters, sizeof(h), hipMemcpyDeviceToHost));
-  for (int k = 0; k < cap && k < SDSJ_NUM_COUNTERS; k++) out[k] = (uint64_t)((int64_t)h[k] + e->host_ctr_adj[k]);
+  for (int k = 0; k < cap && k < SDSJ_NUM_COUNTERS; k++) out[k] = (uint64_t)h[k];
   if (reset) {
     SDSJ_HIP(e, hipMemset(e->d_counters, 0, sizeof(h)));
-    for (auto& a : e->host_ctr_adj) a = 0;
   }
   return SDSJ_OK;
 }

@@ -322,16 +322,6 @@ __device__ __forceinline__ bool bits_can(const BitsQ<Q>& b) { return b.nb > 32 |
 
 template <int Q>
 __device__ __forceinline__ void bits_pull(BitsQ<Q>& b) {
-#ifdef SDSJ_PULL_BRANCH
-  if (b.nb <= 32) {
-    b.buf |= (uint64_t)b.q[0] << (32 - b.nb);
-    b.nb += 32;
-#pragma unroll
-    for (int k = 0; k + 1 < Q; k++) b.q[k] = b.q[k + 1];
-    b.nq--;
-    b.wi++;
-  }
-#else
   // branch-free: a divergent branch here made the compiler copy the whole queue around it on every
   // symbol (phi copies on both paths); selects shift it in place
   const bool need = b.nb <= 32;
@@ -341,7 +331,6 @@ __device__ __forceinline__ void bits_pull(BitsQ<Q>& b) {
   for (int k = 0; k + 1 < Q; k++) b.q[k] = need ? b.q[k + 1] : b.q[k];
   b.nq -= need ? 1 : 0;
   b.wi += need ? 1u : 0u;
-#endif
 }
 
 // MCU position -> table slots and component, from packed per-image registers.
@@ -434,13 +423,9 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   int l = e & 15;
   s = (e >> 4) & 15;
   r = (e >> 8) & 15;
-#ifdef SDSJ_EXP_NOLONG
-  if (l == 0) { l = 16; s = 0; r = 0; }  // (timing experiment: wrong output)
-#else
   // (two-level tables: a prefix without a second level -- more long prefixes than kW2Cap / 4 -- may
   // hold 10- and 11-bit codes too, so their search starts past the first level's width)
   if (l == 0) long_code<TT::kTwoLevel ? kW1 : LB>(T, slot, isdc, hi, l, s, r, bad);
-#endif
   // HUFF_EXTEND without branches: x < 2^(s-1) -> x - (2^s - 1); s = 0 -> 0
   const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - s) & 31);
   const uint32_t half = (1u << s) >> 1;
@@ -1306,15 +1291,19 @@ __device__ __forceinline__ void ent_phase(int img, int grp, ImgDesc* descs, cons
 // The entropy kernels take images from a route list.  MODE 0: one workgroup per list entry (grid =
 // batch size, surplus workgroups exit at once) -- the main route (LB = 11, one group per image).
 // MODE 1: a small grid strides over the list and runs each image's groups in turn (LB = 10).  MODE 3:
-// one workgroup per (image, group) task of the LB = 11 images with ent_groups > 1 (grid = batch x
-// kMaxEntGroups, surplus workgroups exit at once).  The sync pass is per image (MODE 0 for them too).
+// (image, group) tasks of the LB = 11 images with ent_groups > 1, a grid of at most kTaskGrid
+// workgroups striding over them.  The sync pass is per image (MODE 0 for them too).
 template <int LB, int PHASE, int RT, int MODE, int NTS = kSyncThreads>
 __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables, uint8_t* scratch, int32_t* routes,
                                          int cap) {
-  if (MODE == 3) {  // one workgroup per (image, group) task (k_plan's group_tasks list)
-    if ((int)blockIdx.x >= routes[kRtEnt11G]) return;
-    const int task = group_tasks(routes, cap)[blockIdx.x];
-    ent_phase<LB, PHASE, NTS>(task >> kGroupShift, task & ((1 << kGroupShift) - 1), descs, tables, scratch);
+  if (MODE == 3) {  // (image, group) tasks (k_plan's group_tasks list); a capped grid strides over them
+    const int nt = routes[kRtEnt11G];
+    const int32_t* tasks = group_tasks(routes, cap);
+    for (int k = blockIdx.x; k < nt; k += gridDim.x) {
+      const int task = tasks[k];
+      ent_phase<LB, PHASE, NTS>(task >> kGroupShift, task & ((1 << kGroupShift) - 1), descs, tables, scratch);
+      __syncthreads();  // LDS reuse by the next task
+    }
     return;
   }
   const int cnt = routes[RT];
@@ -1364,6 +1353,9 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ 
 
 size_t enttab_bytes() { return sizeof(EntTables); }
 
+constexpr int kTaskGrid = 4096;  // MODE 3 grid cap (>= the workgroups the chip holds at once)
+static int task_grid(int n) { return n * kMaxEntGroups < kTaskGrid ? n * kMaxEntGroups : kTaskGrid; }
+
 hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
                           int cap, hipStream_t s, uint64_t rm) {
   const int g = n;  // one workgroup per image on the main route
@@ -1374,7 +1366,7 @@ hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* e
   if (route_on(rm, kRtEnt11))
     hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt11M))
-    hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3>), dim3(g * kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables,
+    hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3>), dim3(task_grid(n)), dim3(kEntThreads), 0, s, descs, tables,
                        scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
     hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
@@ -1406,7 +1398,7 @@ hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scr
   if (route_on(rm, kRtEnt11))
     hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt11M))
-    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(g * kMaxEntGroups), dim3(kEntThreads), 0, s, descs, tables,
+    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(task_grid(n)), dim3(kEntThreads), 0, s, descs, tables,
                        scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
     hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);

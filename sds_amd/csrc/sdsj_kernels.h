@@ -10,7 +10,9 @@ namespace sdsj {
 // device-resident path passes kAllRoutes (its route lists exist only on the device).
 constexpr uint64_t kAllRoutes = ~0ull;
 SDSJ_HD inline bool route_on(uint64_t rm, int r) { return (rm >> r) & 1ull; }
-hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, const int32_t* lengths, const sdsj_op& op,
+// blob_bytes: the blob's size -- a sample whose [offset, offset + length) leaves it is reported EINVAL
+hipError_t launch_parse(int n, const uint8_t* blob, int64_t blob_bytes, const int64_t* offsets, const int32_t* lengths,
+                        const sdsj_op& op,
                         int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s);
 // base: scratch bytes a previous lane of the batch already took (device), or null
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* base, int64_t* total, int32_t* routes,
@@ -51,7 +53,8 @@ hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, in
                               const uint8_t* flip, void* out, const int32_t* routes, int cap, const float* lut,
                               hipStream_t s, uint64_t rm = kAllRoutes);
 // lengths: the samples' encoded sizes (null: raw frames); counters: SDSJ_CTR_* accumulators (or null)
-hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
+// (a negative length: the sample is reported as EINVAL -- an unreadable file of the host path)
+hipError_t launch_finish(int n, ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
                          const int32_t* lengths, unsigned long long* counters, hipStream_t s);
 // host-side planning (same code as k_parse): returns the scratch bytes image `jpg` needs, or < 0
 // *routes (optional): the routes the image takes (bits as in route masks; all of them when the host

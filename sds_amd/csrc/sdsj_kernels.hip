@@ -218,12 +218,20 @@ struct DevSink {
   __device__ void dqt(uint16_t* qt, int pq, int64_t src) const { add(pq ? 2 : 1, qt, src, 64); }
 };
 
-__global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
-                                              const int32_t* __restrict__ lengths, sdsj_op op, int warm_bits,
-                                              ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables) {
+__global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__ blob, int64_t blob_bytes,
+                                              const int64_t* __restrict__ offsets, const int32_t* __restrict__ lengths,
+                                              sdsj_op op, int warm_bits, ImgDesc* __restrict__ descs,
+                                              ImgTables* __restrict__ tables) {
   const int img = blockIdx.x;
   if (img >= n) return;
   const int lane = threadIdx.x;
+  {  // the sample's range must lie inside the blob (nothing below reads outside it); otherwise EINVAL
+    const int64_t o = offsets[img], l = lengths[img];
+    if (o < 0 || l < 0 || o > blob_bytes || l > blob_bytes - o) {
+      if (lane == 0) descs[img].status = SDSJ_EINVAL;
+      return;
+    }
+  }
   __shared__ alignas(16) uint8_t hdr[kHdrStage];
   __shared__ ImgDesc sd;
   __shared__ ImgTables st;
@@ -387,27 +395,21 @@ __global__ void __launch_bounds__(kPlanThreads) k_plan_apply(int n, ImgDesc* __r
   if (rr >= 0) routes[kRouteSlots + rr * cap + gbase[rr] + ir] = i;
 }
 
-// k_finish: publishes every sample's status and writes the zeros of failed samples and of empty
-// crops (presets.py:160-162 normalise maps them to -1.0 through the LUT, as zeros would).  Also
-// accumulates the engine's per-process counters (SDSJ_CTR_*): one thread per sample, a few 64-bit
-// atomics per sample (lengths == null: the frames path).
+// k_finish: publishes every sample's status and accumulates the engine's per-process counters
+// (SDSJ_CTR_*): one thread per sample, counters summed in LDS, one 64-bit atomic per counter and
+// workgroup (lengths == null: the frames path).  k_zerofill then writes the zeros of failed samples and empty crops
+// (presets.py:160-162 normalise maps them to -1.0 through the LUT, as zeros would).
 __global__ void __launch_bounds__(256) k_finish(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
-                                                void* __restrict__ out, int32_t* __restrict__ status,
-                                                const float* __restrict__ lut, const int32_t* __restrict__ lengths,
+                                                int32_t* __restrict__ status, const int32_t* __restrict__ lengths,
                                                 unsigned long long* __restrict__ counters) {
-  // one thread per image for its status and counters (summed in LDS, one atomic per counter and
-  // workgroup); the workgroup then zero-fills its failed / empty-crop images together
   __shared__ unsigned long long acc[SDSJ_NUM_COUNTERS];
-  __shared__ int zlist[256];
-  __shared__ int nz;
   const int t = threadIdx.x, img = blockIdx.x * 256 + t;
   if (t < SDSJ_NUM_COUNTERS) acc[t] = 0;
-  if (t == 0) nz = 0;
   __syncthreads();
-  const int64_t plane = (int64_t)op.out_h * op.out_w, total = plane * 3;
+  const int64_t total = (int64_t)op.out_h * op.out_w * 3;
   if (img < n) {
     const ImgDesc* d = &descs[img];
-    const int st = d->status;
+    const int st = d->status;  // (k_parse: EINVAL for a sample outside the blob / a negative length)
     status[img] = st;
     if (counters) {
       const int k = st == SDSJ_OK ? SDSJ_CTR_OK
@@ -416,23 +418,35 @@ __global__ void __launch_bounds__(256) k_finish(int n, const ImgDesc* __restrict
                     : st == SDSJ_ECAPACITY ? SDSJ_CTR_CAPACITY : SDSJ_CTR_OTHER;
       atomicAdd(&acc[lengths ? SDSJ_CTR_IMAGES : SDSJ_CTR_FRAMES], 1ull);
       atomicAdd(&acc[k], 1ull);
-      if (lengths) atomicAdd(&acc[SDSJ_CTR_BYTES_IN], (unsigned long long)(uint32_t)lengths[img]);
+      if (lengths && lengths[img] > 0) atomicAdd(&acc[SDSJ_CTR_BYTES_IN], (unsigned long long)lengths[img]);
       atomicAdd(&acc[SDSJ_CTR_BYTES_OUT], (unsigned long long)(total * (op.out_dtype == SDSJ_DTYPE_F32 ? 4 : 1)));
       if (lengths && st == SDSJ_OK && d->progressive) atomicAdd(&acc[SDSJ_CTR_PROGRESSIVE], 1ull);
     }
-    if (!(st == SDSJ_OK && d->geo != kGeoZeros)) zlist[atomicAdd(&nz, 1)] = img;
   }
   __syncthreads();
   if (counters && t < SDSJ_NUM_COUNTERS && acc[t]) atomicAdd(&counters[t], acc[t]);
-  for (int q = 0; q < nz; q++) {
-    const int64_t zi = zlist[q];
+}
+
+// k_zerofill: zeros of failed samples and empty crops.  Work items = (image, chunk of 1/kZeroChunks of
+// its output); a capped grid strides over them, each workgroup checking its item's status, so a batch
+// of many failures is filled by the whole grid and a batch of none costs one status read per item.
+constexpr int kZeroChunks = 16;
+constexpr int kZeroGrid = 2048;
+__global__ void __launch_bounds__(256) k_zerofill(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+                                                  void* __restrict__ out, const float* __restrict__ lut) {
+  const int64_t total = (int64_t)op.out_h * op.out_w * 3, per = (total + kZeroChunks - 1) / kZeroChunks;
+  for (int w = blockIdx.x; w < n * kZeroChunks; w += gridDim.x) {
+    const int img = w / kZeroChunks, ch = w % kZeroChunks;
+    const ImgDesc* d = &descs[img];
+    if (d->status == SDSJ_OK && d->geo != kGeoZeros) continue;
+    const int64_t e0 = ch * per, e1 = e0 + per < total ? e0 + per : total;
     if (op.out_dtype == SDSJ_DTYPE_F32) {
-      float* o = reinterpret_cast<float*>(out) + zi * total;
+      float* o = reinterpret_cast<float*>(out) + (int64_t)img * total;
       const float z = lut[0];
-      for (int64_t i = t; i < total; i += blockDim.x) o[i] = z;
+      for (int64_t i = e0 + threadIdx.x; i < e1; i += blockDim.x) o[i] = z;
     } else {
-      uint8_t* o = reinterpret_cast<uint8_t*>(out) + zi * total;
-      for (int64_t i = t; i < total; i += blockDim.x) o[i] = 0;
+      uint8_t* o = reinterpret_cast<uint8_t*>(out) + (int64_t)img * total;
+      for (int64_t i = e0 + threadIdx.x; i < e1; i += blockDim.x) o[i] = 0;
     }
   }
 }
@@ -777,35 +791,16 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_us_serial(const uint8_t* __
     int nsplit = 0, end_code = -1;
     UsRaw raw;
     if (ntiles > 0) us_load(e, L, t * kUsBytes, raw);
-#ifdef SDSJ_US_PROF
-    int64_t ph[4] = {0, 0, 0, 0};
-#endif
     for (int j = 0; j < ntiles; j++) {
-#ifdef SDSJ_US_PROF
-      const int64_t c0 = clock64();
-#endif
       const int64_t my0 = (int64_t)j * kUsTile + t * kUsBytes;
       UsClass c;
       us_classify(e, L, my0, raw, c);
       if (j + 1 < ntiles) us_load(e, L, my0 + kUsTile, raw);  // the next tile's loads fly meanwhile
-#ifdef SDSJ_US_PROF
-      const int64_t c1 = clock64();
-#endif
       const int my_end = us_my_end(c, t);
       const int tile_end = us_tile_end(my_end, t, wmin);
       const bool ends = tile_end != kUsNone;
       if (ends && my_end == tile_end) s_code = us_end_code(c, t, tile_end);
-#ifdef SDSJ_US_PROF
-      const int64_t c2 = clock64();
-#endif
       const int tot = us_place(c, my0, t, tile_end, obase, nsplit, ends || j == ntiles - 1, out, sv, buf, wsum);
-#ifdef SDSJ_US_PROF
-      const int64_t c3 = clock64();
-      ph[0] += c1 - c0;
-      ph[1] += c2 - c1;
-      ph[2] += c3 - c2;
-      ph[3] += 1;
-#endif
       obase += tot & 0xFFFF;
       nsplit += tot >> 16;
       if (ends) {
@@ -815,10 +810,6 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_us_serial(const uint8_t* __
       }
     }
     us_finish(d, sv, t, obase, nsplit, end_code, end_raw, out);
-#ifdef SDSJ_US_PROF
-    if (t == 0)
-      for (int k = 0; k < 4; k++) d->t_rs[k] = ph[k];
-#endif
   }
 }
 
@@ -1449,9 +1440,10 @@ __global__ void __launch_bounds__(256) k_vpass(int n, const ImgDesc* __restrict_
 // ------------------------------------------------------------------------------------------
 // Host-side launchers (called by the engine; all asynchronous on `stream`).
 // ------------------------------------------------------------------------------------------
-hipError_t launch_parse(int n, const uint8_t* blob, const int64_t* offsets, const int32_t* lengths, const sdsj_op& op,
-                        int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s) {
-  hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, offsets, lengths, op, warm_bits, descs, tables);
+hipError_t launch_parse(int n, const uint8_t* blob, int64_t blob_bytes, const int64_t* offsets, const int32_t* lengths,
+                        const sdsj_op& op, int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s) {
+  hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, blob_bytes, offsets, lengths, op, warm_bits, descs,
+                     tables);
   return hipGetLastError();
 }
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* base, int64_t* total, int32_t* routes,
@@ -1475,10 +1467,12 @@ hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, Im
   }
   return hipGetLastError();
 }
-hipError_t launch_finish(int n, const ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
+hipError_t launch_finish(int n, ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,
                          const int32_t* lengths, unsigned long long* counters, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_finish, dim3((n + 255) / 256), dim3(256), 0, s, n, descs, op, out, status, lut, lengths, counters);
+  hipLaunchKernelGGL(k_finish, dim3((n + 255) / 256), dim3(256), 0, s, n, descs, op, status, lengths, counters);
+  const int zg = n * kZeroChunks < kZeroGrid ? n * kZeroChunks : kZeroGrid;
+  hipLaunchKernelGGL(k_zerofill, dim3(zg), dim3(256), 0, s, n, descs, op, out, lut);
   return hipGetLastError();
 }
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,

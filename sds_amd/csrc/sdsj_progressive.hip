@@ -539,7 +539,6 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
     } else {
       nmcu = mcux * d->mcuy;
     }
-    const unsigned long long t_scan0 = __builtin_amdgcn_s_memtime();
     PBits b;
     b.d = raw;
     b.n = n;
@@ -611,14 +610,6 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
             pblock(b, L, L.qdsl[q], 4, q, coef + g * 64, ss, se, ah, al, &L.ldc[q], &eobrun);
           }
       }
-    }
-    {  // diagnostics: s_memtime ticks per scan kind (DC first / AC first / DC refine / AC refine)
-      const long long dt = (long long)(__builtin_amdgcn_s_memtime() - t_scan0);
-      const int kind = (ss ? 1 : 0) + (ah ? 2 : 0);
-      if (kind == 0) d->t_spec += dt;
-      else if (kind == 1) d->t_sync += dt;
-      else if (kind == 2) d->t_scan += dt;
-      else d->t_write += dt;
     }
     if (b.eof) return SDSJ_CORRUPT;  // the input ended inside the scan (Pillow: truncated)
     if (!b.hit_marker && pnext_marker(b) < 0) return SDSJ_CORRUPT;

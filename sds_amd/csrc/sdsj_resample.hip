@@ -25,12 +25,6 @@
 
 namespace sdsj {
 
-#ifndef SDSJ_RS_TIMING
-#define SDSJ_RS_TIMING 0  // 1: accumulate per-phase s_memtime ticks into ImgDesc::t_rs (experiments)
-#endif
-#ifndef SDSJ_RS_PHASES
-#define SDSJ_RS_PHASES 15  // experiment mask (tools/rs_phases.sh): 1 stage, 2 convert, 4 H, 8 V
-#endif
 
 constexpr int kRsThreads = 256;
 constexpr int kStepRows = 4;                 // source rows per step (fewer when the staging pool is short)
@@ -242,14 +236,6 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
   const int ox = A.fl ? A.ow - 1 - xx : xx;
   int nb = A.oy0;  // next output row to finish
 
-  uint64_t tk[4] = {0, 0, 0, 0}, tm = SDSJ_RS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
-  auto mark = [&](int k) {
-    if (SDSJ_RS_TIMING) {
-      const uint64_t now = __builtin_amdgcn_s_memtime();
-      tk[k] += now - tm;
-      tm = now;
-    }
-  };
   for (int ra = r_lo; ra < r_hi; ra += rs) {
     const int rb = ra + rs < r_hi ? ra + rs : r_hi;  // crop rows [ra, rb) this step
     const int ya = A.cy0 + ra, yb = A.cy0 + rb;     // image rows
@@ -271,7 +257,7 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
           for (int h = 0; h < nch; h++, chunk++) {
             if ((chunk & 3) != wv) continue;
             const int k = h * 64 + lane;
-            if ((SDSJ_RS_PHASES & 1) && k < nd[c])
+            if (k < nd[c])
               __builtin_amdgcn_global_load_lds(  // (block-linear plane: per-lane source address, bl_off)
                   (const __attribute__((address_space(1))) void*)(g + bl_off_clamped(cd.bw, jal[c] + 4 * k, i)),
                   (__attribute__((address_space(3))) void*)(L.st + o + (i - ilo[c]) * nd[c] + h * 64), 4, 0, 0);
@@ -281,13 +267,10 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
       }
     }
     __syncthreads();  // DMA landed (vmcnt(0)); previous step's H reads of rgb are done
-    mark(0);
     // B. upsample + colour convert
-    if (SDSJ_RS_PHASES & 2)
-      for (int q = 0; q < rb - ra; q++) convert_row(L, A, q, ya + q, ax0, ax1, soff, ilo, nd, jal);
+    for (int q = 0; q < rb - ra; q++) convert_row(L, A, q, ya + q, ax0, ax1, soff, ilo, nd, jal);
     __syncthreads();
-    mark(1);
-    if (active && (SDSJ_RS_PHASES & 4)) {
+    if (active) {
 #pragma unroll
       for (int q = 0; q < kStepRows; q++) {
         if (q >= rb - ra) break;
@@ -315,7 +298,7 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
         // V. output rows whose window [vmin, vmin + vcnt) ends at row r (ring_rows >= ksv keeps
         // the whole window; own column only, so no barrier)
         for (;;) {
-          if (!(SDSJ_RS_PHASES & 8) || nb >= A.oy1) break;
+          if (nb >= A.oy1) break;
           const int vmin = __builtin_amdgcn_readfirstlane(L.vb[nb - A.oy0][0]);
           const int vcnt = __builtin_amdgcn_readfirstlane(L.vb[nb - A.oy0][1]);
           if (vmin + vcnt > r + 1) break;
@@ -333,10 +316,7 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
         }
       }
     }
-    mark(2);
   }
-  if (SDSJ_RS_TIMING && (t & 63) == 0)
-    for (int k = 0; k < 3; k++) atomicAdd((unsigned long long*)&A.dmut->t_rs[k], (unsigned long long)tk[k]);
 }
 
 // One image's share (output rows of strip blockIdx.y, column tiles from blockIdx.z) of the generic

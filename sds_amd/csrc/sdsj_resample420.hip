@@ -21,12 +21,6 @@
 #include "sdsj_kernels.h"
 #include "sdsj_pixel.h"
 
-#ifndef SDSJ_RS_TIMING
-#define SDSJ_RS_TIMING 0
-#endif
-#ifndef SDSJ_RS_EXP
-#define SDSJ_RS_EXP 0  // experiments (tools/rs_timing.py): 1 = no output stores, 2 = no vertical gather
-#endif
 
 #ifndef SDSJ_VUNROLL
 #define SDSJ_VUNROLL 1  // (0: the vertical taps as a runtime loop, for A/B runs)
@@ -180,14 +174,6 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
     const int ox = fl ? ow - 1 - xx : xx;
     int nb = oy0;
 
-    uint64_t tk[4] = {0, 0, 0, 0}, tm = SDSJ_RS_TIMING ? __builtin_amdgcn_s_memtime() : 0;
-    auto mark = [&](int k) {
-      if (SDSJ_RS_TIMING) {
-        const uint64_t now = __builtin_amdgcn_s_memtime();
-        tk[k] += now - tm;
-        tm = now;
-      }
-    };
     // Plane rows of a step (4 source rows): luma rows ya..; chroma rows ilo..ilo + nrc - 1 -- for
     // 4:2:0 the rows the h2v2 fancy upsampling reads (row i = y >> 1 and its neighbour f = i -/+ 1
     // for even/odd y, clamped: at most 4 per plane), otherwise the luma rows' own.
@@ -297,7 +283,6 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
       const bool more = ra + kFRows < r_hi;
       const Step nxt = more ? plan_step(ra + kFRows) : cur;
       if (more) issue(nxt);
-      mark(0);
       if (LAY != kRsGray) {
         // B. fancy upsampling + ycc->rgb on 8 pixels per item
         for (int it = t; it < nr * ng; it += kFThreads) {
@@ -395,7 +380,6 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
         }
         __syncthreads();
       }
-      mark(1);
       if (active) {
 #pragma unroll
         for (int q = 0; q < kFRows; q++) {
@@ -412,7 +396,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
             ring[(r & rmask) * rstride] = pack3(s0, s1, s2);
           }
           // V. output rows whose window ends at row r
-          while (!(SDSJ_RS_EXP & 2) && nb < oy1) {
+          while (nb < oy1) {
             const int vmin = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][0]);
             const int vcnt = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][1]);
             if (vmin + vcnt > r + 1) break;
@@ -429,10 +413,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
                 for (int k = 0; k < vcnt; k++) v0 += tap((int32_t)ring[((vmin + k) & rmask) * rstride], wk[k]);
               }
               const int c = rs_clip8(v0);
-              if (SDSJ_RS_EXP & 1)
-                asm volatile("" ::"v"(c));
-              else
-                put3(out, om, lut, (int64_t)nb * ow + ox, c, c, c);
+              put3(out, om, lut, (int64_t)nb * ow + ox, c, c, c);
             } else {
               int32_t v0 = 1 << 21, v1 = 1 << 21, v2 = 1 << 21;
               auto vtap = [&](int k) {
@@ -448,10 +429,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
               } else {
                 for (int k = 0; k < vcnt; k++) vtap(k);
               }
-              if (SDSJ_RS_EXP & 1)
-                asm volatile("" ::"v"(v0), "v"(v1), "v"(v2));
-              else
-                put3(out, om, lut, (int64_t)nb * ow + ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
+              put3(out, om, lut, (int64_t)nb * ow + ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
             }
             nb++;
           }
@@ -463,11 +441,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
         cur = nxt;
       }
       __syncthreads();  // next step's rows staged; this step's H reads are done
-      mark(2);
     }
-    if (SDSJ_RS_TIMING && lane == 0)
-      for (int k = 0; k < 3; k++)
-        atomicAdd((unsigned long long*)&const_cast<ImgDesc*>(d)->t_rs[k], (unsigned long long)tk[k]);
     __syncthreads();  // LDS reuse by the next tile
   }
 }

@@ -251,7 +251,7 @@ class JpegEngine:
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream(self.device).cuda_stream
             rc = self.lib.sdsj_decode_resize_batch_device(
-                self._h, n, ctypes.c_void_p(blob.data_ptr()), ctypes.c_void_p(offsets.data_ptr()),
+                self._h, n, ctypes.c_void_p(blob.data_ptr()), blob.numel(), ctypes.c_void_p(offsets.data_ptr()),
                 ctypes.c_void_p(lengths.data_ptr()), ctypes.byref(op),
                 ctypes.c_void_p(flip.data_ptr()) if flip is not None else None, ctypes.c_void_p(out.data_ptr()),
                 ctypes.c_void_p(status.data_ptr()), ctypes.c_void_p(stream))

@@ -306,3 +306,27 @@ def test_progressive_dri_between_scans_vs_oracle(engine):
         assert int(st[k]) == ost, f"case {k}: gpu {int(st[k])} vs oracle {ost}"
         if ost == O.OK:
             np.testing.assert_array_equal(got[k].cpu().numpy(), ref, err_msg=f"case {k}")
+
+
+@pytest.mark.gpu
+def test_device_entry_rejects_ranges_outside_the_blob():
+    """ABI v2: sdsj_decode_resize_batch_device takes the blob's size; a sample whose [offset, offset +
+    length) is negative or leaves the blob reports SDSJ_EINVAL (checked on the device before any read),
+    and the valid samples of the same batch decode normally."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sds_amd import _lib
+    from sds_amd.engine import JpegEngine
+    _, jpgs = G.g2_jpegs()
+    j = jpgs[0]
+    blob = torch.from_numpy(np.frombuffer(j + bytes(64), np.uint8).copy()).cuda()
+    n = blob.numel()
+    offs = torch.tensor([0, n - 10, -16, 0, 32], dtype=torch.int64).cuda()
+    lens = torch.tensor([len(j), 100, len(j), -1, n], dtype=torch.int32).cuda()
+    eng = JpegEngine("cuda:0", max_batch=16)
+    eng.reserve(JpegEngine.scratch_need([j], (64, 64)) * 2 + (16 << 20))
+    out, st = eng.decode_resize_device(blob, offs, lens, (64, 64))
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [_lib.OK, _lib.EINVAL, _lib.EINVAL, _lib.EINVAL, _lib.EINVAL]
+    np.testing.assert_array_equal(out[0].cpu().numpy(), O.pipeline(j, (64, 64)))
+    assert int(out[1:].abs().sum()) == 0  # failed samples are zero-filled
