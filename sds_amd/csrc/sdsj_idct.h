@@ -26,13 +26,19 @@ namespace sdsj {
 #define SDSJ_FIX_2_562915447 20995
 #define SDSJ_FIX_3_072711026 25172
 
+// Multiply for the ISLOW butterflies: F24 = 24-bit signed operands (v_mul_i32_i24, full rate),
+// exact -- the same low 32 bits as the 32-bit multiply -- whenever both operands lie in (-2^23, 2^23).
+template <bool F24>
+__device__ __forceinline__ int imul(int a, int b) { return F24 ? __mul24(a, b) : a * b; }
+
 // One 1-D ISLOW butterfly (even/odd parts, jidctint.c); inputs x0..x7, outputs scaled sums
-// before the final DESCALE: o[0..7].
+// before the final DESCALE: o[0..7].  Every multiplicand is a sum of at most 4 inputs.
+template <bool F24 = false>
 __device__ __forceinline__ void islow_1d(int x0, int x1, int x2, int x3, int x4, int x5, int x6, int x7, int o[8]) {
   int z2 = x2, z3 = x6;
-  int z1 = (z2 + z3) * SDSJ_FIX_0_541196100;
-  int t2 = z1 + z3 * (-SDSJ_FIX_1_847759065);
-  int t3 = z1 + z2 * SDSJ_FIX_0_765366865;
+  int z1 = imul<F24>(z2 + z3, SDSJ_FIX_0_541196100);
+  int t2 = z1 + imul<F24>(z3, -SDSJ_FIX_1_847759065);
+  int t3 = z1 + imul<F24>(z2, SDSJ_FIX_0_765366865);
   int t0 = (x0 + x4) * (1 << 13);
   int t1 = (x0 - x4) * (1 << 13);
   int t10 = t0 + t3, t13 = t0 - t3, t11 = t1 + t2, t12 = t1 - t2;
@@ -44,15 +50,15 @@ __device__ __forceinline__ void islow_1d(int x0, int x1, int x2, int x3, int x4,
   z2 = t1 + t2;
   z3 = t0 + t2;
   int z4 = t1 + t3;
-  int z5 = (z3 + z4) * SDSJ_FIX_1_175875602;
-  t0 *= SDSJ_FIX_0_298631336;
-  t1 *= SDSJ_FIX_2_053119869;
-  t2 *= SDSJ_FIX_3_072711026;
-  t3 *= SDSJ_FIX_1_501321110;
-  z1 *= -SDSJ_FIX_0_899976223;
-  z2 *= -SDSJ_FIX_2_562915447;
-  z3 *= -SDSJ_FIX_1_961570560;
-  z4 *= -SDSJ_FIX_0_390180644;
+  int z5 = imul<F24>(z3 + z4, SDSJ_FIX_1_175875602);
+  t0 = imul<F24>(t0, SDSJ_FIX_0_298631336);
+  t1 = imul<F24>(t1, SDSJ_FIX_2_053119869);
+  t2 = imul<F24>(t2, SDSJ_FIX_3_072711026);
+  t3 = imul<F24>(t3, SDSJ_FIX_1_501321110);
+  z1 = imul<F24>(z1, -SDSJ_FIX_0_899976223);
+  z2 = imul<F24>(z2, -SDSJ_FIX_2_562915447);
+  z3 = imul<F24>(z3, -SDSJ_FIX_1_961570560);
+  z4 = imul<F24>(z4, -SDSJ_FIX_0_390180644);
   z3 += z5;
   z4 += z5;
   t0 += z1 + z3;
@@ -78,18 +84,23 @@ __device__ __forceinline__ uint32_t range_limit(int x) {
 
 // Pass 1 on one column: dequantised coefficients of rows 0..7 -> workspace column, DESCALE(,
 // CONST_BITS - PASS1_BITS).  (jidctint.c's all-AC-zero shortcut gives the same values.)
+// F24 is exact when every dequantised coefficient of the block lies in (-2^12, 2^12): pass-1
+// multiplicands then stay below 2^14, sums before the DESCALE below 2^30, so pass-2 inputs below 2^19
+// and their multiplicands below 2^21 (real 8-bit images stay near 2^11: kF24Bound).
+template <bool F24 = false>
 __device__ __forceinline__ void islow_pass1(const int x[8], int w[8]) {
   int o[8];
-  islow_1d(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], o);
+  islow_1d<F24>(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], o);
 #pragma unroll
   for (int k = 0; k < 8; k++) w[k] = (o[k] + (1 << 10)) >> 11;
 }
 
 // Pass 2 on one workspace row -> 8 samples, little-endian in two dwords (DESCALE(, CONST_BITS +
 // PASS1_BITS + 3), range limit).
+template <bool F24 = false>
 __device__ __forceinline__ uint2 islow_pass2(const int w[8]) {
   int o[8];
-  islow_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
+  islow_1d<F24>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
   uint32_t lo = 0, hi = 0;
 #pragma unroll
   for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
@@ -97,6 +108,8 @@ __device__ __forceinline__ uint2 islow_pass2(const int w[8]) {
   for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
   return make_uint2(lo, hi);
 }
+
+constexpr int kF24Bound = 1 << 12;
 
 // a / b for 0 <= a < 2^24, 1 <= b < 2^16: float estimate, then one correction each way (exact)
 __device__ __forceinline__ int qdiv(int a, int b, float rb) {
