@@ -89,7 +89,7 @@ struct CompDesc {
   int32_t rh, rv;     // upsampling ratio hmax/h, vmax/v (1 or 2)
   int32_t dw, dh;     // downsampled width / height (jdinput.c)
   int32_t bw, bh;     // coded blocks per row / column (MCU padded when interleaved)
-  int32_t pitch;      // samples per plane row (bw * 8); planes are block-linear (bl_off)
+  int32_t pitch;      // plane row pitch in bytes (bw * 8)
   int64_t plane_off;  // byte offset of this plane inside the image's plane area
 };
 
@@ -278,19 +278,6 @@ SDSJ_HD inline int gen_route(int kt) {
 
 SDSJ_HD inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 SDSJ_HD inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
-
-// Sample planes are block-linear: a component's 8x8 blocks, 64 bytes each (8 rows of 8 samples), in
-// raster order of blocks (bw per block row).  The entropy write pass stores each inverse-transformed
-// block as one contiguous 64-byte run; readers address sample (x, y) -- or the dword at a 4-aligned x
-// -- through bl_off.  (Plane bytes < 2^30: total_blocks < 2^24, setup_geometry.)
-SDSJ_HD inline int32_t bl_off(int bw, int x, int y) { return (((y >> 3) * bw + (x >> 3)) << 6) | ((y & 7) << 3) | (x & 7); }
-// ... with the block column clamped to [0, bw): reads a few samples past a row end (or before its start)
-// see the edge block instead of leaving the plane (those samples only feed pixels outside the tile)
-SDSJ_HD inline int32_t bl_off_clamped(int bw, int x, int y) {
-  int bx = x >> 3;
-  bx = bx < 0 ? 0 : (bx >= bw ? bw - 1 : bx);
-  return (((y >> 3) * bw + bx) << 6) | ((y & 7) << 3) | (x & 7);
-}
 
 // jutils.c jpeg_natural_order (+16 guard entries)
 #if defined(__HIPCC__)
@@ -524,7 +511,7 @@ SDSJ_HD inline int setup_geometry(ImgDesc* d, const ImgTables* t) {
     CompDesc& cp = d->comp[c];
     cp.pitch = cp.bw * 8;
     cp.plane_off = plane;
-    plane += align_up((int64_t)cp.bw * cp.bh * 64, 256);
+    plane += align_up((int64_t)cp.pitch * cp.bh * 8, 256);
   }
   d->total_blocks = (int64_t)d->mcux * d->mcuy * d->bpm;
   if (d->total_blocks >= (int64_t)1 << 24) return SDSJ_UNSUPPORTED;  // > ~700 MP (block indices are 24-bit)

@@ -215,7 +215,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, int64
   mark(6);
   SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(7);
-  SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
   mark(8);
   SDSJ_HIP(e, launch_color(n, ln.descs, e->scratch, ln.routes, cap, s, rm));
   mark(9);

@@ -32,7 +32,6 @@
 #include <type_traits>
 
 #include "sdsj_common.h"
-#include "sdsj_idct.h"
 #include "sdsj_kernels.h"
 
 namespace sdsj {
@@ -66,7 +65,6 @@ struct EntTables {
   int32_t nslots;
   uint32_t pk_dc[2], pk_ac[2], pk_c;  // per MCU block: DC slot, AC slot (4 bits each), component (2)
   uint32_t pad[4];
-  uint16_t qtT[kMaxComp][64];  // each component's quantisation table, column-major (the write pass's IDCT)
 };
 static_assert(sizeof(EntTables) % 16 == 0, "EntTables is copied in 16-byte units");
 
@@ -116,15 +114,7 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restric
     T.pk_c = pc;
     T.pad[0] = T.pad[1] = T.pad[2] = T.pad[3] = 0;
   }
-  // the write pass assembles blocks column-major: natural_order transposed (row r, column c -> c * 8 + r)
-  for (int i = t; i < 80; i += kEntThreads) {
-    const int nz = natural_order(i);
-    T.nat[i] = (uint8_t)(((nz & 7) << 3) | (nz >> 3));
-  }
-  for (int i = t; i < kMaxComp * 64; i += kEntThreads) {
-    const int c = i >> 6, k = i & 63;
-    T.qtT[c][((k & 7) << 3) | (k >> 3)] = c < d->ncomp ? tb->qt[d->comp[c].tq][k] : (uint16_t)0;
-  }
+  for (int i = t; i < 80; i += kEntThreads) T.nat[i] = (uint8_t)natural_order(i);
   __syncthreads();
   const int ns = T.nslots;
   const int lb = (ns << 11) <= kLutEntries ? 11 : 10;  // the variant that will decode this image
@@ -928,71 +918,22 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
 // ------------------------------------------------------------------------------------------
 // k_entwrite
 // ------------------------------------------------------------------------------------------
-// The write pass inverse-transforms every block it completes (dequantisation + jpeg_idct_islow,
-// sdsj_idct.h) and stores its 64 samples into the block-linear plane: the coefficients never leave
-// LDS.  The workgroup has two kinds of waves:
-//   * kEntThreads decode lanes (4 waves), one subsequence each.  A lane assembles its current block in
-//     its staging area in COLUMN-major order (the transposed natural order in T.nat).  At every step
-//     the blocks that just completed are copied (8 lanes x 16 B per block) into a ring of kRing LDS
-//     slots under consecutive tickets, and the staging areas are cleared for their owners' next
-//     blocks;
-//   * kXfWaves transform waves.  Transform wave w takes tickets [kXfBatch b, kXfBatch (b + 1)) for b = w,
-//     w + kXfWaves, ...: it waits until those blocks are published, transforms them (8 lanes per block,
-//     kXfJ blocks per lane group) and frees their slots.
-// So the transform's arithmetic and its LDS round trips run beside the decode waves' dependent
-// chains instead of inside them.  Ticket T lives in slot T % kRing; a decode lane waits (rarely) until
-// the slot's previous ticket T - kRing is transformed.  That ticket belongs to batch b - kXfWaves, the
-// same transform wave's previous batch, so the waits cannot form a cycle (kRing = kXfBatch kXfWaves).
-#ifndef SDSJ_IDCT24
-#define SDSJ_IDCT24 1  // 24-bit IDCT multiplies behind a per-batch range check (0: 32-bit)
-#endif
-#ifndef SDSJ_XF_WAVES
-#define SDSJ_XF_WAVES 4
-#endif
-constexpr int kWaves = kEntThreads / 64;
-#ifndef SDSJ_XF_J
-#define SDSJ_XF_J 2
-#endif
-#ifndef SDSJ_XF_DIAG
-#define SDSJ_XF_DIAG 0  // 1: per-image ring statistics into the ImgDesc diagnostics fields (tools/xf_diag.py)
-#endif
-constexpr int kXfWaves = SDSJ_XF_WAVES;                     // transform waves per workgroup
-constexpr int kXfJ = SDSJ_XF_J;                             // blocks per lane group of a transform wave
-constexpr int kXfBatch = 8 * kXfJ;                          // tickets per transform batch
-constexpr int kRing = kXfBatch * kXfWaves;                   // ring slots (blocks)
-constexpr int kWriteThreads = kEntThreads + 64 * kXfWaves;   // the write pass's workgroup
-// (a step's tickets are published 8 at a time, after ALL of those 8 slots are free: a slot's previous
-// ticket must lie in an earlier batch than any ticket of the same 8 -- two or more transform waves)
-static_assert(kRing >= kXfBatch + 8, "ring too small: a step's publish group could wait on its own batch");
-
+// A 16-byte coefficient store (plain: the coefficient stream is read back by k_idct long after).
+__device__ __forceinline__ void store_coef16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 template <class TT>
 struct LdsWriteT {
   unsigned long long t0, it;
   TT T;
   alignas(16) int16_t stage[(kEntThreads + 1) * kStageStride];  // + one shared sink block
-  alignas(16) int16_t ring[kRing][kStageStride];                 // completed blocks, column-major
-  alignas(16) uint16_t qt[kMaxComp][64];                         // quantisation tables, column-major
-  int32_t rmeta[kRing];      // decode-order block index of the slot's block
-  uint32_t rready[kRing];    // ticket + 1 once the slot's block is copied in
-  uint32_t rdone[kRing];     // ticket + 1 once it is transformed (the slot is free for ticket + kRing)
-  uint32_t flist[kWaves][64];  // this step's completed blocks: (lane << 24) | block index (total_blocks < 2^24)
-  BlkGeo X;
-  uint32_t tail;  // tickets handed out
-  int32_t pdone;  // decode waves finished (every ticket published)
-  unsigned long long dg_busy, dg_wait, dg_spin, dg_batches;  // (SDSJ_XF_DIAG)
+  uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
   int32_t bad;
   unsigned long long sym;
 };
 
-__device__ __forceinline__ uint32_t lds_vload(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
-__device__ __forceinline__ int32_t lds_vload(const int32_t* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
-__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 // The compact two-level tables from the image's LB = 11 tables (HBM).  The staging area serves as
-// the scan's scratch before it is cleared.  (Threads beyond kEntThreads join the barriers only.)
+// the scan's scratch before it is cleared.
 __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tmp) {
   const int t = threadIdx.x;
-  const bool dec = t < kEntThreads;
   const int ns = g->nslots;
   if (!variant_owns<11>(ns)) return ns;
   // which 9-bit prefixes lead to longer codes: 8 consecutive prefixes per thread, one block scan
@@ -1002,39 +943,37 @@ __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tm
 #pragma unroll
   for (int j = 0; j < kPer; j++) {
     const int i = t * kPer + j, q = i >> kW1, k = i & ((1 << kW1) - 1);
-    const uint32_t e = dec && q < ns ? g->lut[(q << 11) + (k << 2)] : 0u;
+    const uint32_t e = q < ns ? g->lut[(q << 11) + (k << 2)] : 0u;
     const int l = e & 15;
-    const bool lng = dec && q < ns && (l == 0 || l > kW1);
+    const bool lng = q < ns && (l == 0 || l > kW1);
     longmask |= lng ? 1u << j : 0u;
     cnt += lng ? 1 : 0;
   }
   int total;
   int base = block_excl_scan<kEntThreads>(cnt, tmp, &total);
-  if (dec) {
 #pragma unroll
-    for (int j = 0; j < kPer; j++) {
-      const int i = t * kPer + j, q = i >> kW1, k = i & ((1 << kW1) - 1);
-      uint32_t e = q < ns ? g->lut[(q << 11) + (k << 2)] : 0u;
-      if ((longmask >> j) & 1) {
-        const int sub = base++;
-        if (sub < kW2Cap / 4) {
-          for (int m = 0; m < 4; m++) W.l2[sub * 4 + m] = g->lut[(q << 11) + (k << 2) + m];
-          e = (uint32_t)(sub + 1) << 4;
-        } else {
-          e = 0;  // no second level left: the canonical search
-        }
+  for (int j = 0; j < kPer; j++) {
+    const int i = t * kPer + j, q = i >> kW1, k = i & ((1 << kW1) - 1);
+    uint32_t e = q < ns ? g->lut[(q << 11) + (k << 2)] : 0u;
+    if ((longmask >> j) & 1) {
+      const int sub = base++;
+      if (sub < kW2Cap / 4) {
+        for (int m = 0; m < 4; m++) W.l2[sub * 4 + m] = g->lut[(q << 11) + (k << 2) + m];
+        e = (uint32_t)(sub + 1) << 4;
+      } else {
+        e = 0;  // no second level left: the canonical search
       }
-      W.lut[i] = (uint16_t)e;
     }
+    W.lut[i] = (uint16_t)e;
   }
-  for (int i = t; i < 4 * 18; i += blockDim.x) {
+  for (int i = t; i < 4 * 18; i += kEntThreads) {
     W.maxcode[i / 18][i % 18] = g->maxcode[i / 18][i % 18];
     W.valoff[i / 18][i % 18] = g->valoff[i / 18][i % 18];
   }
   const uint32_t* gv = reinterpret_cast<const uint32_t*>(g->vals);
   uint32_t* wvls = reinterpret_cast<uint32_t*>(W.vals);
-  for (int i = t; i < 4 * 64; i += blockDim.x) wvls[i] = gv[i];
-  for (int i = t; i < 80; i += blockDim.x) W.nat[i] = g->nat[i];
+  for (int i = t; i < 4 * 64; i += kEntThreads) wvls[i] = gv[i];
+  for (int i = t; i < 80; i += kEntThreads) W.nat[i] = g->nat[i];
   if (t == 0) {
     W.pk_dc[0] = g->pk_dc[0];
     W.pk_dc[1] = g->pk_dc[1];
@@ -1044,125 +983,6 @@ __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tm
   }
   __syncthreads();
   return ns;
-}
-
-// Transform of the ring's tickets [t0, t0 + nb) (nb <= kXfBatch) by one transform wave.  8 lanes per
-// block, each lane group taking kXfJ blocks (tickets t0 + gi + 8 j) whose chains interleave: lane r reads
-// column r (16 bytes), dequantises it and runs pass 1; the columns are transposed through the slot's
-// own 128 bytes in two halves (rows 0-3, then 4-7); lane r runs pass 2 on row r and stores its 8
-// samples, so a block leaves as one contiguous 64-byte run (only the blocks the crop reads).  Then
-// the slots are freed.
-template <class LW>
-__device__ __forceinline__ void xf_batch(LW& L, int lane, uint32_t t0, int nb, uint8_t* planes) {
-  const int gi = lane >> 3, r = lane & 7;
-  int16_t* src[kXfJ];
-  int off[kXfJ], x[kXfJ][8];
-  bool valid[kXfJ], keep[kXfJ];
-  int amax = 0;
-#pragma unroll
-  for (int j = 0; j < kXfJ; j++) {
-    const int e = gi + 8 * j;
-    valid[j] = e < nb;
-    const uint32_t slot = (t0 + (uint32_t)e) % kRing;
-    src[j] = valid[j] ? L.ring[slot] : L.stage + kEntThreads * kStageStride;  // (sink: scratch for idle lanes)
-    const int g = valid[j] ? L.rmeta[slot] : 0;
-    const uint4 col = *reinterpret_cast<const uint4*>(src[j] + r * 8);
-    int c = 0;
-    off[j] = 0;
-    keep[j] = valid[j] && blk_locate(L.X, g, c, off[j]);
-    const uint4 q = *reinterpret_cast<const uint4*>(&L.qt[c][r * 8]);
-    // DEQUANTIZE: coefficient (int16) x quantisation value (uint16) -- both below 2^23 in magnitude, so
-    // the 24-bit multiply is exact
-    const uint32_t cw[4] = {col.x, col.y, col.z, col.w}, qw[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      x[j][2 * k] = __mul24((int)(int16_t)(cw[k] & 0xFFFFu), (int)(qw[k] & 0xFFFFu));
-      x[j][2 * k + 1] = __mul24((int)(int16_t)(cw[k] >> 16), (int)(qw[k] >> 16));
-    }
-#pragma unroll
-    for (int k = 0; k < 8; k++) amax = valid[j] ? max(amax, abs(x[j][k])) : amax;
-  }
-  // 24-bit butterflies when every block of the batch is within kF24Bound (real images: always)
-  const bool f24 = SDSJ_IDCT24 && !__builtin_amdgcn_ballot_w64(amax >= kF24Bound);
-  int w[kXfJ][8];
-#pragma unroll
-  for (int j = 0; j < kXfJ; j++) {
-    if (f24) islow_pass1<true>(x[j], w[j]);
-    else islow_pass1<false>(x[j], w[j]);
-  }
-  // transpose: column r's outputs w[k] -> W[row k][column r], rows 0-3 then 4-7 in each slot's 128 B
-  int row[kXfJ][8];
-  asm volatile("" ::: "memory");  // (the column reads above come first in the wave's LDS order)
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-#pragma unroll
-    for (int j = 0; j < kXfJ; j++) {
-      int* W = reinterpret_cast<int*>(src[j]);
-#pragma unroll
-      for (int k = 0; k < 4; k++) W[k * 8 + r] = w[j][4 * h + k];
-    }
-#pragma unroll
-    for (int j = 0; j < kXfJ; j++) {
-      if ((r >> 2) == h) {
-        const int4* W4 = reinterpret_cast<const int4*>(src[j]) + (r - 4 * h) * 2;
-        const int4 a = W4[0], b = W4[1];
-        row[j][0] = a.x, row[j][1] = a.y, row[j][2] = a.z, row[j][3] = a.w;
-        row[j][4] = b.x, row[j][5] = b.y, row[j][6] = b.z, row[j][7] = b.w;
-      }
-    }
-    asm volatile("" ::: "memory");
-  }
-#pragma unroll
-  for (int j = 0; j < kXfJ; j++) {
-    const uint2 px = f24 ? islow_pass2<true>(row[j]) : islow_pass2<false>(row[j]);
-    if (keep[j]) *reinterpret_cast<uint2*>(planes + off[j] + r * 8) = px;
-  }
-  lds_wait();  // every read of the slots has returned before they are handed back
-  if (r == 0) {
-#pragma unroll
-    for (int j = 0; j < kXfJ; j++) {
-      const uint32_t tk = t0 + (uint32_t)(gi + 8 * j);
-      if (valid[j]) __atomic_store_n(&L.rdone[tk % kRing], tk + 1, __ATOMIC_RELAXED);
-    }
-  }
-}
-
-// Transform wave xw: batches b = xw, xw + kXfWaves, ... (kXfBatch tickets each) until the decode waves
-// are done and every ticket is transformed.
-template <class LW>
-__device__ void xf_loop(LW& L, int xw, int lane, uint8_t* planes) {
-  for (uint32_t b = (uint32_t)xw;; b += kXfWaves) {
-    const uint32_t t0 = kXfBatch * b;
-    int nb = 0;
-    const unsigned long long w0 = SDSJ_XF_DIAG ? __builtin_amdgcn_s_memtime() : 0;
-    for (;;) {
-      const uint32_t tk = t0 + (uint32_t)lane;
-      const bool pub = lane < kXfBatch && lds_vload(&L.rready[tk % kRing]) == tk + 1;
-      const uint64_t m = __builtin_amdgcn_ballot_w64(pub);
-      if (m == (kXfBatch == 64 ? ~0ull : ((1ull << kXfBatch) - 1))) {
-        nb = kXfBatch;
-        break;
-      }
-      if (lds_vload(&L.pdone) == kWaves) {  // every ticket is published: tail is final
-        const uint32_t tail = lds_vload(&L.tail);
-        nb = tail > t0 ? (int)(tail - t0 < (uint32_t)kXfBatch ? tail - t0 : (uint32_t)kXfBatch) : 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (SDSJ_XF_DIAG && lane == 0) atomicAdd(&L.dg_wait, __builtin_amdgcn_s_memtime() - w0);
-    if (nb == 0) return;
-    if (SDSJ_XF_DIAG) {
-      const unsigned long long a = __builtin_amdgcn_s_memtime();
-      xf_batch(L, lane, t0, nb, planes);
-      if (lane == 0) {
-        atomicAdd(&L.dg_busy, __builtin_amdgcn_s_memtime() - a);
-        atomicAdd(&L.dg_batches, 1ull);
-      }
-    } else {
-      xf_batch(L, lane, t0, nb, planes);
-    }
-  }
 }
 
 template <int LB>
@@ -1179,38 +999,21 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   if (!variant_owns<LB>(ns)) return;
   {
     uint4* z4 = reinterpret_cast<uint4*>(L.stage);
-    for (int i = t; i < (kEntThreads + 1) * kStageStride * 2 / 16; i += blockDim.x) z4[i] = make_uint4(0, 0, 0, 0);
-    const uint4* gq = reinterpret_cast<const uint4*>(tables[img].qtT);
-    uint4* lq = reinterpret_cast<uint4*>(L.qt);
-    for (int i = t; i < (int)(sizeof(L.qt) / 16); i += blockDim.x) lq[i] = gq[i];
-    for (int i = t; i < kRing; i += blockDim.x) {
-      L.rready[i] = 0;
-      L.rdone[i] = 0;
-    }
+    for (int i = t; i < (kEntThreads + 1) * kStageStride * 2 / 16; i += kEntThreads) z4[i] = make_uint4(0, 0, 0, 0);
   }
   if (t == 0) {
     L.bad = 0;
     L.sym = 0;
     L.it = 0;
-    L.tail = 0;
-    L.pdone = 0;
-    L.dg_busy = L.dg_wait = L.dg_spin = L.dg_batches = 0;
     if (kStats) L.t0 = __builtin_amdgcn_s_memtime();
-    blkgeo_init(d, L.X);
   }
   __syncthreads();
-  uint8_t* planes = scratch + d->off_planes;
-  const unsigned long long tstart = SDSJ_XF_DIAG ? __builtin_amdgcn_s_memtime() : 0;
-  if (t >= kEntThreads) {  // a transform wave
-    xf_loop(L, wv - kWaves, lane, planes);
-    __syncthreads();
-    return;
-  }
   const TT& T = L.T;
   const BlkCtx K = make_ctx(T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
   const SubState* sub = reinterpret_cast<const SubState*>(scratch + d->off_sub);
+  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
   const int nsub = d->nsub;
   const int blocks_per_seg = d->restart_interval ? d->restart_interval * K.bpm : (int)d->total_blocks;
   const int my_base = t * kStageStride, sink_base = kEntThreads * kStageStride;
@@ -1218,7 +1021,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   unsigned long long nsym = 0, witers = 0;
 
   const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
-  for (int jb = j0; jb < j1; jb += kEntThreads) {  // uniform trip count for the decode waves
+  for (int jb = j0; jb < j1; jb += kEntThreads) {  // uniform trip count for the whole workgroup
     const int j = jb + t;
     const bool active = j < j1;
     Bits b;
@@ -1267,7 +1070,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
           if (kStats) nsym++;
           bad |= sb;
-          // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r] (transposed)
+          // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
           pc += isdc ? val : 0;
           const int wpos = T.nat[z + r];  // (natural_order[0] = 0 for the DC symbol)
           L.stage[((writing & (isdc | (s != 0))) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
@@ -1289,38 +1092,26 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           const bool more_mid = (b.pos < end_bit) | (z != 0);
           run = (g < gend) & (last_of_seg ? more_last : more_mid);
         }
-        // the blocks completed in this step go to the ring under consecutive tickets: 8 lanes x 16 B
-        // per block, then their staging areas are cleared for the owners' next blocks
+        // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
         const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
         if (m) {
           const int cnt = __popcll(m);
           if (ready) {
             const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            L.flist[wv][idx] = ((uint32_t)lane << 24) | gdone;
+            L.flist[wv][idx] = ((uint32_t)t << 24) | gdone;
           }
-          uint32_t base = 0;
-          if (lane == 0) base = atomicAdd(&L.tail, (uint32_t)cnt);
-          base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-          // (a wave's LDS accesses execute in issue order: the reads below see the flist writes, and the
-          // owner's next stage writes land after the clears)
+          // (a wave's LDS accesses execute in issue order: the reads below see these writes, and the
+          // owner's next stage writes land after the clears -- no waits beyond the data dependences)
           __builtin_amdgcn_wave_barrier();
-          const int gi = lane >> 3, r8 = lane & 7;
           for (int b0 = 0; b0 < cnt; b0 += 8) {
-            const int k = b0 + gi;
-            const uint32_t tk = base + (uint32_t)k, slot = tk % kRing;
-            if (k < cnt) {
-              while (lds_vload(&L.rdone[slot]) + kRing <= tk) {  // slot still in use
-                if (SDSJ_XF_DIAG && r8 == 0) atomicAdd(&L.dg_spin, 1ull);
-                __builtin_amdgcn_s_sleep(1);
-              }
-              const uint32_t f = L.flist[wv][k];
-              uint4* sp = reinterpret_cast<uint4*>(L.stage + (wv * 64 + (int)(f >> 24)) * kStageStride) + r8;
-              reinterpret_cast<uint4*>(L.ring[slot])[r8] = *sp;
-              if (r8 == 0) L.rmeta[slot] = (int32_t)(f & 0xFFFFFFu);
+            const int bi = b0 + (lane >> 3);
+            if (bi < cnt) {
+              const uint32_t f = L.flist[wv][bi];
+              uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
+              const uint4 v = *sp;
+              store_coef16(reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64) + (lane & 7), v);
               *sp = make_uint4(0, 0, 0, 0);
             }
-            lds_wait();  // the block is in the ring before its ticket is published
-            if (k < cnt && r8 == 0) __atomic_store_n(&L.rready[slot], tk + 1, __ATOMIC_RELAXED);
           }
           __builtin_amdgcn_wave_barrier();
         }
@@ -1331,12 +1122,10 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       }
     }
     if (active && last_of_seg) {
-      if (g < gend) sv.vend[s_int] = g;                     // the rest of the interval stays zero (k_cutfill)
+      if (g < gend) sv.vend[s_int] = g;                     // the rest of the interval stays zero
       if (b.pos > lim) sv.flag[s_int] |= kSegIns;          // ran out of data (JWRN_HIT_MARKER)
     }
   }
-  lds_wait();
-  if (lane == 0) atomicAdd(&L.pdone, 1);  // every ticket of this wave is published
   if (bad) atomicOr(&L.bad, 1);  // bad Huffman codes: libjpeg warns and decodes symbol 0 (statistics only)
   if (kStats) {
     atomicAdd(&L.sym, nsym);
@@ -1347,58 +1136,6 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     d->sym_write = (int64_t)L.sym;
     d->it_write = (int64_t)L.it;
     d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - L.t0);
-  }
-  if (SDSJ_XF_DIAG && t == 0 && grp == 0) {  // ring statistics (the decode waves end at the barrier above)
-    d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - tstart);
-    d->t_sync = (int64_t)L.dg_busy;
-    d->t_scan = (int64_t)L.dg_wait;
-    d->it_sync = (int64_t)L.dg_spin;
-    d->it_spec = (int64_t)L.dg_batches;
-  }
-}
-
-// k_cutfill: the blocks libjpeg leaves with zero coefficients -- samples of 128 after the IDCT --
-// when a restart interval runs out of data (jdhuff.c insufficient_data): from vend[k] to the end of
-// interval k, and all of an empty interval entered out of data.  The write pass stops decoding there;
-// this writes those blocks (the ones the crop reads) after it.  One wave per image, nothing to do for
-// an intact stream.
-__global__ void __launch_bounds__(64) k_cutfill(int n, const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch) {
-  const int img = blockIdx.x, lane = threadIdx.x;
-  if (img >= n) return;
-  const ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK || d->progressive || d->geo == kGeoZeros) return;
-  __shared__ BlkGeo X;
-  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
-  const int nseg = d->nseg, total = (int)d->total_blocks;
-  const int bps = d->restart_interval ? d->restart_interval * d->bpm : total;
-  uint8_t* planes = scratch + d->off_planes;
-  bool geo = false;
-  for (int k0 = 0; k0 < nseg; k0 += 64) {
-    const int k = k0 + lane;
-    int z0 = 0, z1 = 0;
-    if (k < nseg) {
-      const int s0 = k * bps;
-      z1 = s0 + bps < total ? s0 + bps : total;
-      const bool whole = k > 0 && (sv.flag[k] & kSegEmpty) && (sv.flag[k - 1] & kSegIns);
-      z0 = whole ? s0 : (sv.vend[k] > s0 ? sv.vend[k] : s0);
-    }
-    uint64_t m = __builtin_amdgcn_ballot_w64(z1 > z0);
-    if (!m) continue;
-    if (!geo) {
-      if (lane == 0) blkgeo_init(d, X);
-      __syncthreads();
-      geo = true;
-    }
-    while (m) {
-      const int q = __builtin_ffsll((long long)m) - 1;
-      m &= m - 1;
-      const int a = __shfl(z0, q), e = __shfl(z1, q);
-      for (int gb = a + (lane >> 2); gb < e; gb += 16) {  // 4 lanes per block, 16 bytes each
-        int c, off;
-        if (blk_locate(X, gb, c, off))
-          reinterpret_cast<uint4*>(planes + off)[lane & 3] = make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
-      }
-    }
   }
 }
 
@@ -1466,7 +1203,7 @@ __global__ void __launch_bounds__(NTS) k_entsync(ImgDesc* __restrict__ descs, co
 }
 
 template <int LB, int RT, int MODE>
-__global__ void __launch_bounds__(kWriteThreads) k_entwrite(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
+__global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                                                           uint8_t* __restrict__ scratch, int32_t* __restrict__ routes,
                                                           int cap) {
   ent_feed<LB, 2, RT, MODE>(descs, tables, scratch, routes, cap);
@@ -1517,14 +1254,12 @@ hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scr
   const EntTables* tables = static_cast<const EntTables*>(etab);
   const int gs = g < 256 ? g : 256;
   if (route_on(rm, kRtEnt11))
-    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kWriteThreads), 0, s, descs, tables, scratch, routes, cap);
+    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt11M))
-    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(task_grid(n)), dim3(kWriteThreads), 0, s, descs, tables,
+    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(task_grid(n)), dim3(kEntThreads), 0, s, descs, tables,
                        scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
-    hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kWriteThreads), 0, s, descs, tables, scratch, routes, cap);
-  if (route_on(rm, kRtEnt11) || route_on(rm, kRtEnt11M) || route_on(rm, kRtEnt10))
-    hipLaunchKernelGGL(k_cutfill, dim3(n), dim3(64), 0, s, n, descs, scratch);
+    hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 

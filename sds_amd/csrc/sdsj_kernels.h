@@ -35,9 +35,7 @@ hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, i
                           uint64_t rm = kAllRoutes);
 hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
                            hipStream_t s, uint64_t rm = kAllRoutes);
-// progressive images only (route kRtProg): dequantisation + IDCT of the coefficients k_prog decoded
-hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, const int32_t* routes,
-                       int cap, hipStream_t s, uint64_t rm = kAllRoutes);
+hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
 hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,
                         uint64_t rm = kAllRoutes);
 hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s);

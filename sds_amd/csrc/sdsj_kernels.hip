@@ -175,9 +175,9 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
   d->off_sub = take((int64_t)d->nsub_cap * sizeof(SubState));
   d->off_rec = take((int64_t)d->nsub_cap * kRec * sizeof(SyncRec));
   d->off_ptab = take(prog ? (int64_t)sizeof(ProgTables) : 0);
-  d->off_coef = take(prog ? d->total_blocks * 128 : 0);  // (baseline blocks never leave the write pass as coefficients)
-  int64_t planes = 0;  // block-linear sample planes (bl_off): bw * bh blocks of 64 bytes each
-  for (int c = 0; c < d->ncomp; c++) planes += align_up((int64_t)d->comp[c].bw * d->comp[c].bh * 64, 256);
+  d->off_coef = take(d->total_blocks * 128);
+  int64_t planes = 0;
+  for (int c = 0; c < d->ncomp; c++) planes += align_up((int64_t)d->comp[c].pitch * d->comp[c].bh * 8, 256);
   d->off_planes = take(planes);
   d->off_rgb = take(d->fused || frames ? 0 : (int64_t)d->src_w * (d->src_y1 - d->src_y0) * 3);
   d->rgb_pitch = d->src_w;  // k_color packs the crop rows
@@ -983,9 +983,7 @@ __global__ void __launch_bounds__(64) k_scanmap(int n, const uint8_t* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// k_idct: dequantisation + jpeg_idct_islow of PROGRESSIVE images (k_prog leaves their coefficients
-// in scratch); a baseline image's blocks are inverse-transformed by the entropy write pass as they
-// complete (sdsj_entropy.hip).  8 threads per block, 32 blocks per iteration.
+// k_idct: dequantisation + jpeg_idct_islow; 8 threads per block, 32 blocks per iteration.
 // ------------------------------------------------------------------------------------------
 constexpr int kIdctThreads = 256;
 constexpr int kIdctBlocks = kIdctThreads / 8;
@@ -993,11 +991,10 @@ constexpr int kIdctBlocks = kIdctThreads / 8;
 #define SDSJ_IDCT_GRID 8
 #endif
 constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides over 8-block groups)
-constexpr int kIdctImages = 1024;          // workgroup rows striding over the progressive route list
 constexpr int kWsStride = 72;  // ints per block in LDS (conflict-free column reads per half-wave)
 
-// Work unit = one wave: 8 horizontally adjacent blocks of one component (a "group"), so the wave's
-// 8 row stores write 512 contiguous bytes of the block-linear plane.  8 threads per block
+// Work unit = one wave: 8 horizontally adjacent blocks of one component (a "group"), so each of
+// the 8 row stores of the wave writes 64 contiguous bytes of a plane row.  8 threads per block
 // (thread r: row r, then column r); the 8 threads of a block share a wave, so the LDS transposes
 // need only in-wave ordering, no workgroup barrier.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1005,10 +1002,13 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ void idct_image(int img, const ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
-                           uint8_t* __restrict__ scratch) {
+__global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __restrict__ descs,
+                                                       const ImgTables* __restrict__ tables,
+                                                       uint8_t* __restrict__ scratch) {
+  const int img = blockIdx.y;
+  if (img >= n) return;
   const ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK || d->geo == kGeoZeros || !d->progressive) return;
+  if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
   __shared__ alignas(16) int ws[kIdctBlocks * kWsStride];
   __shared__ alignas(16) int32_t qt[kMaxComp][64];
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
@@ -1056,6 +1056,19 @@ __device__ void idct_image(int img, const ImgDesc* __restrict__ descs, const Img
   const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
   uint8_t* planes = scratch + d->off_planes;
   const int ngroups = gstart[ncomp];
+  // blocks the entropy decoder left zero (jdhuff.c insufficient_data): from vend[k] to the end of
+  // restart interval k, and all of an empty interval entered out of data
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+  const int nseg = d->nseg;
+  const int bps = d->restart_interval ? d->restart_interval * bpm : (int)d->total_blocks;
+  const int vend0 = d->progressive ? 0 : sv.vend[0];
+  const bool prog = d->progressive != 0;  // (k_prog decodes every block; no cut intervals)
+  auto zero_block = [&](int g) {
+    if (prog) return false;
+    if (nseg == 1) return g >= vend0;
+    const int k = g / bps;
+    return g >= sv.vend[k] || (k > 0 && (sv.flag[k] & kSegEmpty) && (sv.flag[k - 1] & kSegIns));
+  };
   // block of this lane in group grp: component, block coordinates, decode-order index
   // a / b for 0 <= a < 2^22, 1 <= b: float estimate, then one correction each way (exact)
   auto qdiv = [](int a, int b, float rb) {
@@ -1083,7 +1096,7 @@ __device__ void idct_image(int img, const ImgDesc* __restrict__ descs, const Img
     const bool valid = g >= 0;
     if (valid) {
       // row r of the block, dequantised (DEQUANTIZE: coef * quantval), stored as two 16-byte writes
-      const uint4 v = raw;
+      const uint4 v = zero_block(g) ? make_uint4(0, 0, 0, 0) : raw;
       const int4 q0 = *reinterpret_cast<const int4*>(&qt[c][r * 8]), q1 = *reinterpret_cast<const int4*>(&qt[c][r * 8 + 4]);
       auto lo16 = [](uint32_t x) { return (int)(int16_t)(x & 0xFFFF); };
       auto hi16 = [](uint32_t x) { return (int)(int16_t)(x >> 16); };
@@ -1117,7 +1130,7 @@ __device__ void idct_image(int img, const ImgDesc* __restrict__ descs, const Img
       uint32_t lo = 0, hi = 0;
       for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
       for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
-      *reinterpret_cast<uint2*>(planes + cplane[c] + (((int64_t)by * cbw[c] + bx) << 6) + r * 8) = make_uint2(lo, hi);
+      *reinterpret_cast<uint2*>(planes + cplane[c] + (int64_t)(by * 8 + r) * cpitch[c] + bx * 8) = make_uint2(lo, hi);
     }
     wave_lds_sync();
   };
@@ -1138,53 +1151,43 @@ __device__ void idct_image(int img, const ImgDesc* __restrict__ descs, const Img
   }
 }
 
-__global__ void __launch_bounds__(kIdctThreads) k_idct(const ImgDesc* __restrict__ descs,
-                                                       const ImgTables* __restrict__ tables,
-                                                       uint8_t* __restrict__ scratch,
-                                                       const int32_t* __restrict__ routes, int cap) {
-  const int cnt = routes[kRtProg];
-  const int32_t* lst = route_list(routes, cap, kRtProg);
-  for (int e = blockIdx.y; e < cnt; e += gridDim.y) {
-    idct_image(lst[e], descs, tables, scratch);
-    __syncthreads();  // LDS reuse by the next image
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // k_color: fancy upsampling (jdsample.c, context rows per jdmainct.c) + ycc_rgb_convert.
 // One thread per RGB pixel of rows [src_y0, src_y1) x cols [src_x0, src_x0 + src_w).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ int up_sample(const uint8_t* P, const CompDesc& c, int x, int y) {
-  auto at = [&](int xx, int yy) { return (int)P[bl_off(c.bw, xx, yy)]; };  // block-linear plane
-  if (c.rh == 1 && c.rv == 1) return at(x, y);
+  if (c.rh == 1 && c.rv == 1) return P[(int64_t)y * c.pitch + x];
   const int dw = c.dw, dh = c.dh;
   if (c.rv == 2) {
     const int i = y >> 1;
     int f = (y & 1) ? i + 1 : i - 1;
     f = f < 0 ? 0 : (f > dh - 1 ? dh - 1 : f);
+    const uint8_t* r0 = P + (int64_t)i * c.pitch;
+    const uint8_t* r1 = P + (int64_t)f * c.pitch;
     if (c.rh == 2) {
       const int jx = x >> 1;
-      if (dw <= 2) return at(jx, i);  // h2v2_upsample (box)
-      const int cs = at(jx, i) * 3 + at(jx, f);
+      if (dw <= 2) return P[(int64_t)i * c.pitch + jx];  // h2v2_upsample (box)
+      const int cs = r0[jx] * 3 + r1[jx];
       if ((x & 1) == 0) {
         const int k = jx > 0 ? jx - 1 : 0;
-        const int cn = jx > 0 ? at(k, i) * 3 + at(k, f) : cs;
+        const int cn = jx > 0 ? r0[k] * 3 + r1[k] : cs;
         return (cs * 3 + cn + 8) >> 4;
       } else {
         const int k = jx < dw - 1 ? jx + 1 : dw - 1;
-        const int cn = jx < dw - 1 ? at(k, i) * 3 + at(k, f) : cs;
+        const int cn = jx < dw - 1 ? r0[k] * 3 + r1[k] : cs;
         return (cs * 3 + cn + 7) >> 4;
       }
     }
     // h1v2_fancy_upsample
-    return (at(x, i) * 3 + at(x, f) + ((y & 1) ? 2 : 1)) >> 2;
+    return (r0[x] * 3 + r1[x] + ((y & 1) ? 2 : 1)) >> 2;
   }
   // rh == 2, rv == 1: h2v1
+  const uint8_t* row = P + (int64_t)y * c.pitch;
   const int jx = x >> 1;
-  const int a = at(jx, y);
+  const int a = row[jx];
   if (dw <= 2) return a;
-  if ((x & 1) == 0) return jx == 0 ? a : (a * 3 + at(jx - 1, y) + 1) >> 2;
-  return jx == dw - 1 ? a : (a * 3 + at(jx + 1, y) + 2) >> 2;
+  if ((x & 1) == 0) return jx == 0 ? a : (a * 3 + row[jx - 1] + 1) >> 2;
+  return jx == dw - 1 ? a : (a * 3 + row[jx + 1] + 2) >> 2;
 }
 
 __device__ __forceinline__ uint32_t clamp255(int v) { return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
@@ -1480,11 +1483,8 @@ hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, Im
   hipLaunchKernelGGL(k_scanmap, dim3((n + 63) / 64), dim3(64), 0, s, n, blob, offsets, descs, scratch);
   return hipGetLastError();
 }
-hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, const int32_t* routes,
-                       int cap, hipStream_t s, uint64_t rm) {
-  if (!route_on(rm, kRtProg)) return hipSuccess;
-  hipLaunchKernelGGL(k_idct, dim3(kIdctGrid, n < kIdctImages ? n : kIdctImages), dim3(kIdctThreads), 0, s, descs, tables,
-                     scratch, routes, cap);
+hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
+  hipLaunchKernelGGL(k_idct, dim3(kIdctGrid, n), dim3(kIdctThreads), 0, s, n, descs, tables, scratch);
   return hipGetLastError();
 }
 hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,

@@ -253,13 +253,13 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
         comp_rows(cd, ya, yb, &ilo[c], &ihi);
         const int nch = (nd[c] + 63) >> 6;
         for (int i = ilo[c]; i <= ihi; i++) {
-          const uint8_t* g = A.planes + cd.plane_off;
+          const uint8_t* g = A.planes + cd.plane_off + (int64_t)i * cd.pitch + jal[c];
           for (int h = 0; h < nch; h++, chunk++) {
             if ((chunk & 3) != wv) continue;
             const int k = h * 64 + lane;
             if (k < nd[c])
-              __builtin_amdgcn_global_load_lds(  // (block-linear plane: per-lane source address, bl_off)
-                  (const __attribute__((address_space(1))) void*)(g + bl_off_clamped(cd.bw, jal[c] + 4 * k, i)),
+              __builtin_amdgcn_global_load_lds(
+                  (const __attribute__((address_space(1))) void*)(g + 4 * k),
                   (__attribute__((address_space(3))) void*)(L.st + o + (i - ilo[c]) * nd[c] + h * 64), 4, 0, 0);
           }
         }

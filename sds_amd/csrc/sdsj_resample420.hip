@@ -21,7 +21,6 @@
 #include "sdsj_kernels.h"
 #include "sdsj_pixel.h"
 
-
 #ifndef SDSJ_VUNROLL
 #define SDSJ_VUNROLL 1  // (0: the vertical taps as a runtime loop, for A/B runs)
 #endif
@@ -131,7 +130,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
   const uint8_t* pY = scratch + d->off_planes + d->comp[0].plane_off;
   const uint8_t* pCb = LAY == kRsGray ? pY : scratch + d->off_planes + d->comp[1].plane_off;
   const uint8_t* pCr = LAY == kRsGray ? pY : scratch + d->off_planes + d->comp[2].plane_off;
-  const int bwY = d->comp[0].bw, bwC = LAY == kRsGray ? 0 : d->comp[1].bw;  // blocks per plane row (bl_off)
+  const int pitchY = d->comp[0].pitch, pitchC = LAY == kRsGray ? 0 : d->comp[1].pitch;
   const int ntiles = (ow + tw - 1) / tw;
   const int r_lo = bv[2 * oy0], r_hi = bv[2 * (oy1 - 1)] + bv[2 * (oy1 - 1) + 1];
   // the strip's vertical windows and weights
@@ -151,7 +150,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
     // 8-pixel groups: luma columns [xb, xb + 8 ng) with xb 8-aligned (dword writes); half-width
     // chroma columns [jb - 4, jb + 4 ng + 4) (the fancy upsampling reads one neighbour each side),
     // full-width chroma (4:4:4) columns [xb, xb + 8 ng).  Bytes past a row end (or before the first
-    // one) come from the row's edge block (bl_off_clamped) and only feed pixels outside the tile.
+    // one) come from neighbouring scratch and only feed pixels outside the tile.
     const int jb = (ax0 >> 1) & ~3;
     const int xb = 2 * jb;
     const int ng = (ax1 - 1 - xb) / 8 + 1;
@@ -202,28 +201,17 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
     // Wave wv holds staged rows wv, wv + 4, wv + 8 (<= 12 rows), 64 dwords per load.
     constexpr int kPR = (G::kRows + 3) / 4, kPC = (kMaxSpan / 4 + 2 + 63) / 64;
     uint32_t pre[kPR][kPC];
-    // staged row `row` of a step: its plane, blocks per plane row, sample row, first column (4-aligned),
-    // dwords and LDS offset; each lane loads the dwords at jal + 4 (64 h + lane) through bl_off
-    auto row_src = [&](const Step& p, int row, const uint8_t*& g, int& bw, int& y, int& jal, int& nd, int& o) {
+    auto row_src = [&](const Step& p, int row, const uint8_t*& g, int& nd, int& o) {
       if (row < p.nr) {
-        g = pY;
-        bw = bwY;
-        y = p.ya + row;
-        jal = jalY;
+        g = pY + (int64_t)(p.ya + row) * pitchY + jalY;
         nd = ndY;
         o = row * kFYDW;
       } else if (row < p.nr + p.nrc) {
-        g = pCb;
-        bw = bwC;
-        y = p.ilo + row - p.nr;
-        jal = jalC;
+        g = pCb + (int64_t)(p.ilo + row - p.nr) * pitchC + jalC;
         nd = ndC;
         o = kFRows * kFYDW + (row - p.nr) * G::kCDW;
       } else {
-        g = pCr;
-        bw = bwC;
-        y = p.ilo + row - p.nr - p.nrc;
-        jal = jalC;
+        g = pCr + (int64_t)(p.ilo + row - p.nr - p.nrc) * pitchC + jalC;
         nd = ndC;
         o = kFRows * kFYDW + G::kCRows * G::kCDW + (row - p.nr - p.nrc) * G::kCDW;
       }
@@ -234,13 +222,12 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
         const int row = wv + 4 * i;
         if (row < p.nr + 2 * p.nrc) {
           const uint8_t* g;
-          int bw, y, jal, nd, o;
-          row_src(p, row, g, bw, y, jal, nd, o);
+          int nd, o;
+          row_src(p, row, g, nd, o);
+          const uint32_t* g4 = reinterpret_cast<const uint32_t*>(g);
 #pragma unroll
           for (int h = 0; h < kPC; h++)
-            if (64 * h + lane < nd)
-              pre[i][h] = __builtin_nontemporal_load(
-                  reinterpret_cast<const uint32_t*>(g + bl_off_clamped(bw, jal + 4 * (64 * h + lane), y)));
+            if (64 * h + lane < nd) pre[i][h] = __builtin_nontemporal_load(g4 + 64 * h + lane);
         }
       }
     };
@@ -250,8 +237,8 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
         const int row = wv + 4 * i;
         if (row < p.nr + 2 * p.nrc) {
           const uint8_t* g;
-          int bw, y, jal, nd, o;
-          row_src(p, row, g, bw, y, jal, nd, o);
+          int nd, o;
+          row_src(p, row, g, nd, o);
 #pragma unroll
           for (int h = 0; h < kPC; h++)
             if (64 * h + lane < nd) L.st[o + 64 * h + lane] = pre[i][h];

@@ -82,10 +82,9 @@ def stage_report(engine, jpg: bytes, resolution=(256, 256)) -> list[str]:
     lines.append(f"desc: {d.width}x{d.height} ncomp={d.ncomp} bpm={d.bpm} mcu={d.mcux}x{d.mcuy} nseg={d.nseg} "
                  f"ulen={d.ulen} nsub={d.nsub} sub_bits={d.sub_bits} geo={d.geo} crop=({d.cx0},{d.cy0},{d.cw},{d.ch}) "
                  f"need_h={d.need_h} need_v={d.need_v} yf={d.yf} yl={d.yl} status={d.status}")
-    # coefficients (progressive images only: a baseline image's blocks are inverse-transformed inside
-    # the entropy write pass and never stored): decode order [g][64] natural order
-    coef = fetch(d.off_coef, d.total_blocks * 128).view(np.int16).reshape(-1, 64) if d.progressive else None
-    for c in range(d.ncomp if d.progressive else 0):
+    # coefficients: device layout is decode order [g][64] natural order
+    coef = fetch(d.off_coef, d.total_blocks * 128).view(np.int16).reshape(-1, 64)
+    for c in range(d.ncomp):
         ref = O.coefficients(jpg, c)  # [bh][bw][64]
         cd = d.comp[c]
         got = np.zeros_like(ref)
