@@ -22,7 +22,12 @@ namespace sdsj {
 constexpr int kMaxComp = 3;
 constexpr int kMaxBlocksPerMcu = 10;  // D_MAX_BLOCKS_IN_MCU
 constexpr int kRec = 64;              // block-boundary records kept per subsequence by k_entsync
-constexpr int kDecodeThreads = 256;   // threads (subsequences) per image in the entropy kernel
+#ifndef SDSJ_DECODE_THREADS
+#define SDSJ_DECODE_THREADS 256
+#endif
+constexpr int kDecodeThreads = SDSJ_DECODE_THREADS;  // threads (subsequences) per image in the entropy kernels
+static_assert((kDecodeThreads & (kDecodeThreads - 1)) == 0 && kDecodeThreads >= 64 && kDecodeThreads <= 256,
+              "a power of two number of waves");
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
 constexpr int kWarmBits = 3000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
 constexpr int kWarmBitsSmall = 4000;  // ... for lanes of fewer than kWarmSmallLane images (the sync pass is
