@@ -33,6 +33,19 @@ constexpr int kWarmBits = 3000;       // speculative warm-up before each subsequ
 constexpr int kWarmBitsSmall = 4000;  // ... for lanes of fewer than kWarmSmallLane images (the sync pass is
 constexpr int kWarmSmallLane = 512;   //     hidden by less concurrent work there, so it pays to shorten it)
 constexpr int kWarmDiv = 3;           // ... or sub_bits / kWarmDiv when that is larger
+// Latency mode (host-path chunks of at most kSmallBatch images, e.g. the per-sample drop-in's single
+// image): the entropy work of an image spreads over up to kMaxEntGroups workgroups of short
+// subsequences (kLatSubBits) with a fixed warm-up (kLatWarm), and its unstuffing goes tile-parallel,
+// so one image's serial chains are short -- at the price of more warm-up work per image.
+constexpr int kSmallBatch = 32;
+#ifndef SDSJ_LAT_SUB
+#define SDSJ_LAT_SUB 1024
+#endif
+#ifndef SDSJ_LAT_WARM
+#define SDSJ_LAT_WARM 4000
+#endif
+constexpr int kLatSubBits = SDSJ_LAT_SUB;
+constexpr int kLatWarm = SDSJ_LAT_WARM;
 // large images: ent_groups = ceil(bits / (kDecodeThreads x kGroupBits)) workgroups (<= kMaxEntGroups)
 // share the subsequences, so one lane's serial decode stays near kGroupBits
 #ifndef SDSJ_GROUP_BITS
@@ -162,7 +175,7 @@ struct ImgDesc {
   // progressive JPEG (SOF2): every scan is decoded by k_prog from sos_pos (the first SOS segment's
   // length field) into the zeroed coefficient array; ProgTables at off_ptab hold its table state
   int32_t progressive;
-  int32_t pad3;
+  int32_t lat;  // latency-mode plan (kSmallBatch)
   int64_t sos_pos;
   int64_t off_ptab;
   // k_unstuff: per 8 KiB tile of the entropy-coded data, the counts its first pass found (UsTile)

@@ -181,7 +181,7 @@ struct Lane {
 
 // Runs the kernel sequence for one lane (n <= max_batch images) of device-resident inputs.
 // after_spec (optional) is recorded once the lane's speculative entropy pass is queued.
-int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, int64_t blob_bytes, const int64_t* d_offsets,
+int run_lane(sdsj_engine* e, const Lane& ln, int n, bool small, const uint8_t* d_blob, int64_t blob_bytes, const int64_t* d_offsets,
              const int32_t* d_lengths, const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status,
              hipStream_t s, hipEvent_t after_spec, uint64_t rm) {
   std::vector<hipEvent_t>* evs = nullptr;
@@ -198,7 +198,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, int64
     if (after_spec && (e->lane_mid == k || (e->lane_mid < 0 && k == kMarkAfterSpec))) (void)hipEventRecord(after_spec, s);
   };
   mark(0);
-  SDSJ_HIP(e, launch_parse(n, d_blob, blob_bytes, d_offsets, d_lengths, op, e->warm_bits, ln.descs, ln.tables, s));
+  SDSJ_HIP(e, launch_parse(n, d_blob, blob_bytes, d_offsets, d_lengths, op, e->warm_bits, small, ln.descs, ln.tables, s));
   mark(1);
   const int cap = e->max_batch;
   SDSJ_HIP(e, launch_plan(n, ln.descs, e->capacity, ln.base, ln.total, ln.routes, cap, s));
@@ -240,15 +240,17 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, const uint8_t* d_blob, int64
 // single lane.
 constexpr int kLaneMin = 128;
 
-// rm: the routes the chunk's images may take (host planning), or kAllRoutes
+// rm: the routes the chunk's images may take (host planning), or kAllRoutes; small: the chunk was
+// host-planned in latency mode (host paths, n <= kSmallBatch)
 int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, int64_t blob_bytes, const int64_t* d_offsets, const int32_t* d_lengths,
               const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status, hipStream_t s,
-              uint64_t rm = kAllRoutes) {
+              uint64_t rm = kAllRoutes, bool small = false) {
   int nl = std::min(std::max(e->lanes, 1), kMaxLanes);
   while (nl > 1 && n < nl * kLaneMin) nl--;
   const Lane first{e->descs, e->tables, e->d_etab, e->d_routes, e->d_total, nullptr};
   if (nl == 1)
-    return run_lane(e, first, n, d_blob, blob_bytes, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr, rm);
+    return run_lane(e, first, n, small, d_blob, blob_bytes, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr,
+                    rm);
   for (int k = 0; k + 1 < nl; k++)
     if (!e->aux[k]) {
       SDSJ_HIP(e, hipStreamCreateWithFlags(&e->aux[k], hipStreamNonBlocking));
@@ -266,7 +268,7 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, int64_t blob_bytes, 
                                   k == 1 ? e->d_total : e->d_totals_x + (k - 2)};
     hipStream_t ls = k == 0 ? s : e->aux[k - 1];
     if (k > 0) SDSJ_HIP(e, hipStreamWaitEvent(ls, e->ev_mid[k - 1], 0));
-    int st = run_lane(e, ln, i1 - i0, d_blob, blob_bytes, d_offsets + i0, d_lengths + i0, op, d_flip ? d_flip + i0 : nullptr,
+    int st = run_lane(e, ln, i1 - i0, small, d_blob, blob_bytes, d_offsets + i0, d_lengths + i0, op, d_flip ? d_flip + i0 : nullptr,
                       static_cast<uint8_t*>(d_out) + i0 * ob, d_status + i0, ls,
                       k + 1 < nl ? e->ev_mid[k] : nullptr, rm);
     if (st != SDSJ_OK) return st;
@@ -373,6 +375,7 @@ int slot_reserve(sdsj_engine* e, Slot& sl, int n, size_t bytes) {
 // behind that copy, status D2H into pinned memory, completion event.
 int slot_launch(sdsj_engine* e, Slot& sl, int n, size_t bytes, const sdsj_op& op, void* out, hipStream_t s) {
   std::vector<int64_t> needs(n, 0);
+  const bool small = n <= kSmallBatch;
   std::atomic<uint64_t> rmask{0};  // the routes the batch takes (launchers skip the others)
   parallel_for(n, [&](int i0, int i1) {
     uint64_t rm = 0;
@@ -380,7 +383,7 @@ int slot_launch(sdsj_engine* e, Slot& sl, int n, size_t bytes, const sdsj_op& op
       if (sl.h_pre[i] != SDSJ_OK) continue;
       int st = SDSJ_OK;
       uint64_t r = 0;
-      const int64_t ni = host_plan_need(sl.h_stage + sl.h_offsets[i], sl.h_lengths[i], op, &st, &r);
+      const int64_t ni = host_plan_need(sl.h_stage + sl.h_offsets[i], sl.h_lengths[i], op, &st, &r, small);
       if (st == SDSJ_OK) needs[i] = align_up(ni, 256);
       rm |= r;
     }
@@ -401,7 +404,8 @@ int slot_launch(sdsj_engine* e, Slot& sl, int n, size_t bytes, const sdsj_op& op
   SDSJ_HIP(e, hipMemcpyAsync(sl.d_flip, sl.h_flip, n, hipMemcpyHostToDevice, cs));
   SDSJ_HIP(e, hipEventRecord(sl.ev_h2d, cs));
   SDSJ_HIP(e, hipStreamWaitEvent(s, sl.ev_h2d, 0));
-  const int rc = run_chunk(e, n, sl.d_blob, (int64_t)bytes, sl.d_offsets, sl.d_lengths, op, sl.d_flip, out, sl.d_status, s, rmask.load());
+  const int rc = run_chunk(e, n, sl.d_blob, (int64_t)bytes, sl.d_offsets, sl.d_lengths, op, sl.d_flip, out, sl.d_status, s,
+                           rmask.load(), small);
   if (rc != SDSJ_OK) return rc;
   SDSJ_HIP(e, hipMemcpyAsync(sl.h_status, sl.d_status, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s));
   SDSJ_HIP(e, hipEventRecord(sl.ev_done, s));
@@ -685,6 +689,7 @@ int sdsj_decode_resize_batch(sdsj_engine* e, int n, const uint8_t* const* jpg, c
   if (rc != SDSJ_OK) return rc;
   for (int c0 = 0; c0 < n; c0 += e->max_batch) {
     int m = std::min(e->max_batch, n - c0);
+    const bool small = m <= kSmallBatch;
     // host planning: exact scratch need of this chunk (same code as k_parse / k_plan)
     int64_t need = 0, bytes = 0;
     uint64_t rm = 0;  // the routes the chunk takes (launchers skip the others)
@@ -692,7 +697,7 @@ int sdsj_decode_resize_batch(sdsj_engine* e, int n, const uint8_t* const* jpg, c
       int st = SDSJ_OK;
       if (len[c0 + i] > (size_t)INT32_MAX) return fail(e, SDSJ_EINVAL, "sample larger than 2 GiB");
       uint64_t r = 0;
-      int64_t ni = host_plan_need(jpg[c0 + i], (int64_t)len[c0 + i], *op, &st, &r);
+      int64_t ni = host_plan_need(jpg[c0 + i], (int64_t)len[c0 + i], *op, &st, &r, small);
       if (st == SDSJ_OK) need += align_up(ni, 256);
       rm |= r;
       bytes += align_up((int64_t)len[c0 + i], 16);
@@ -703,34 +708,39 @@ int sdsj_decode_resize_batch(sdsj_engine* e, int n, const uint8_t* const* jpg, c
       rc = ensure_scratch(e, need);
       if (rc != SDSJ_OK) return rc;
     }
-    if ((size_t)bytes > e->h_stage_cap) {
+    // one staging region, one H2D copy: the samples, then their offsets, lengths and flip flags
+    const int64_t meta = align_up(bytes, 16);
+    const int64_t staged = meta + align_up((int64_t)m * 8, 16) + align_up((int64_t)m * 4, 16) + align_up(m, 16);
+    if ((size_t)staged > e->h_stage_cap) {
       SDSJ_HIP(e, hipStreamSynchronize(s));
       (void)hipHostFree(e->h_stage);
       (void)hipFree(e->d_blob);
       e->h_stage = nullptr;
       e->d_blob = nullptr;
       e->h_stage_cap = e->d_blob_cap = 0;
-      size_t cap = std::max<size_t>((size_t)bytes * 3 / 2, 1 << 20);
+      size_t cap = std::max<size_t>((size_t)staged * 3 / 2, 1 << 20);
       SDSJ_HIP(e, hipHostMalloc(&e->h_stage, cap));
       SDSJ_HIP(e, hipMalloc(&e->d_blob, cap));
       e->h_stage_cap = e->d_blob_cap = cap;
     }
     // the staging buffers are reused: wait for the previous chunk's H2D to finish
     SDSJ_HIP(e, hipStreamSynchronize(s));
+    const int64_t o_off = meta, o_len = o_off + align_up((int64_t)m * 8, 16), o_flip = o_len + align_up((int64_t)m * 4, 16);
+    int64_t* h_off = reinterpret_cast<int64_t*>(e->h_stage + o_off);
+    int32_t* h_len = reinterpret_cast<int32_t*>(e->h_stage + o_len);
+    uint8_t* h_fl = e->h_stage + o_flip;
     int64_t off = 0;
     for (int i = 0; i < m; i++) {
       memcpy(e->h_stage + off, jpg[c0 + i], len[c0 + i]);
-      e->h_offsets[i] = off;
-      e->h_lengths[i] = (int32_t)len[c0 + i];
-      e->h_flip[i] = flip ? flip[c0 + i] : 0;
+      h_off[i] = off;
+      h_len[i] = (int32_t)len[c0 + i];
+      h_fl[i] = flip ? flip[c0 + i] : 0;
       off += align_up((int64_t)len[c0 + i], 16);
     }
-    SDSJ_HIP(e, hipMemcpyAsync(e->d_blob, e->h_stage, off, hipMemcpyHostToDevice, s));
-    SDSJ_HIP(e, hipMemcpyAsync(e->d_offsets, e->h_offsets, sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
-    SDSJ_HIP(e, hipMemcpyAsync(e->d_lengths, e->h_lengths, sizeof(int32_t) * m, hipMemcpyHostToDevice, s));
-    SDSJ_HIP(e, hipMemcpyAsync(e->d_flip, e->h_flip, m, hipMemcpyHostToDevice, s));
-    rc = run_chunk(e, m, e->d_blob, off, e->d_offsets, e->d_lengths, *op, e->d_flip,
-                   reinterpret_cast<uint8_t*>(out) + c0 * ob, e->d_status, s, rm);
+    SDSJ_HIP(e, hipMemcpyAsync(e->d_blob, e->h_stage, (size_t)staged, hipMemcpyHostToDevice, s));
+    rc = run_chunk(e, m, e->d_blob, off, reinterpret_cast<const int64_t*>(e->d_blob + o_off),
+                   reinterpret_cast<const int32_t*>(e->d_blob + o_len), *op, e->d_blob + o_flip,
+                   reinterpret_cast<uint8_t*>(out) + c0 * ob, e->d_status, s, rm, small);
     if (rc != SDSJ_OK) return rc;
     SDSJ_HIP(e, hipMemcpyAsync(e->h_status, e->d_status, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s));
     SDSJ_HIP(e, hipStreamSynchronize(s));

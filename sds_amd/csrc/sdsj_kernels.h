@@ -12,8 +12,7 @@ constexpr uint64_t kAllRoutes = ~0ull;
 SDSJ_HD inline bool route_on(uint64_t rm, int r) { return (rm >> r) & 1ull; }
 // blob_bytes: the blob's size -- a sample whose [offset, offset + length) leaves it is reported EINVAL
 hipError_t launch_parse(int n, const uint8_t* blob, int64_t blob_bytes, const int64_t* offsets, const int32_t* lengths,
-                        const sdsj_op& op,
-                        int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s);
+                        const sdsj_op& op, int warm_bits, bool small, ImgDesc* descs, ImgTables* tables, hipStream_t s);
 // base: scratch bytes a previous lane of the batch already took (device), or null
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* base, int64_t* total, int32_t* routes,
                        int cap, hipStream_t s);
@@ -57,7 +56,9 @@ hipError_t launch_finish(int n, ImgDesc* descs, const sdsj_op& op, void* out, in
 // host-side planning (same code as k_parse): returns the scratch bytes image `jpg` needs, or < 0
 // *routes (optional): the routes the image takes (bits as in route masks; all of them when the host
 // parse fails, so the device's own verdict is never starved of a kernel)
-int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status, uint64_t* routes = nullptr);
+// small: the latency-mode plan of a chunk of at most kSmallBatch images (k_parse's `small`)
+int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status, uint64_t* routes = nullptr,
+                       bool small = false);
 // host-side planning of one raw RGB frame (width x height) for the unfused passes; returns scratch bytes
 int64_t host_plan_frame(ImgDesc* d, int width, int height, const sdsj_op& op);
 }  // namespace sdsj

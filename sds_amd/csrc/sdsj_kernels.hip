@@ -60,7 +60,7 @@ __device__ __host__ inline int warm_for(int sub_bits, int floor_bits) {
   return sub_bits * 3 / 2 < w ? sub_bits * 3 / 2 : w;
 }
 
-__device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, bool frames = false) {
+__device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, bool frames = false, bool small = false) {
   // Geometry: functional.py:78-80 shortcut, :118-147 crop, Pillow ImagingResampleInner.
   const int W = d->width, H = d->height;
   if (W == op.out_w && H == op.out_h) {
@@ -141,19 +141,22 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
       d->rs_lay = lay;
     }
   }
+  d->lat = small && !frames;
   {
-    const int64_t bits = d->entropy_len * 8, per_group = (int64_t)kDecodeThreads * kGroupBits;
+    const int64_t bits = d->entropy_len * 8;
+    const int64_t per_group = (int64_t)kDecodeThreads * (d->lat ? kLatSubBits : kGroupBits);
     int64_t g = (bits + per_group - 1) / per_group;
     g = g < 1 ? 1 : (g > kMaxEntGroups ? kMaxEntGroups : g);
     d->ent_groups = frames ? 1 : (int32_t)g;
     const int64_t lanes = (int64_t)kDecodeThreads * d->ent_groups;
     d->sub_bits = (int32_t)align_up((bits + lanes - 1) / lanes, 32);
   }
-  if (d->sub_bits < kMinSubBits) d->sub_bits = kMinSubBits;
+  const int min_sub = d->lat ? kLatSubBits : kMinSubBits;
+  if (d->sub_bits < min_sub) d->sub_bits = min_sub;
   // warm-up: kWarmBits (k_parse may raise the floor for small lanes), or sub_bits / kWarmDiv for long
   // subsequences (large images: a few percent more speculative work removes nearly every sync task,
-  // each of which is a serial re-decode)
-  d->warm_bits = warm_for(d->sub_bits, kWarmBits);
+  // each of which is a serial re-decode); latency mode: kLatWarm
+  d->warm_bits = d->lat ? kLatWarm : warm_for(d->sub_bits, kWarmBits);
   d->nsub_cap = (int32_t)((d->entropy_len * 8 + d->sub_bits - 1) / d->sub_bits) + d->nseg + 1;
   const bool prog = d->progressive && !frames;  // k_prog decodes it: no unstuffed stream, no subsequences
   if (prog) {
@@ -220,7 +223,7 @@ struct DevSink {
 
 __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__ blob, int64_t blob_bytes,
                                               const int64_t* __restrict__ offsets, const int32_t* __restrict__ lengths,
-                                              sdsj_op op, int warm_bits, ImgDesc* __restrict__ descs,
+                                              sdsj_op op, int warm_bits, int small, ImgDesc* __restrict__ descs,
                                               ImgTables* __restrict__ tables) {
   const int img = blockIdx.x;
   if (img >= n) return;
@@ -249,9 +252,9 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
     DevSink sink{jobs, &njobs, rd};
     int status = parse_headers(rd, len, &sd, &st, sink);
     if (status == SDSJ_OK) status = setup_geometry(&sd, &st);
-    if (status == SDSJ_OK) plan_image(&sd, op);
-    if (warm_bits >= 0) sd.warm_bits = warm_bits;                                 // override (experiments)
-    else if (n < kWarmSmallLane) sd.warm_bits = warm_for(sd.sub_bits, kWarmBitsSmall);  // small lane
+    if (status == SDSJ_OK) plan_image(&sd, op, false, small != 0);
+    if (warm_bits >= 0) sd.warm_bits = warm_bits;  // override (experiments)
+    else if (n < kWarmSmallLane && !sd.lat) sd.warm_bits = warm_for(sd.sub_bits, kWarmBitsSmall);  // small lane
     sd.status = status;
     for (int k = 0; k < 4; k++) sd.t_rs[k] = 0;
     s_status = status;
@@ -305,7 +308,7 @@ SDSJ_HD inline void image_routes(const ImgDesc& d, int* ru, int* re, int* rr) {
       for (int q = 0; q < ns; q++) seen |= keys[q] == key;
       if (!seen) keys[ns++] = key;
     }
-  *ru = d.progressive ? -1 : (d.ntiles > kUsSerialTiles ? kRtUsBig : kRtUsSmall);
+  *ru = d.progressive ? -1 : (d.ntiles > kUsSerialTiles || d.lat ? kRtUsBig : kRtUsSmall);
   *re = d.progressive ? kRtProg : ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
   *rr = d.geo == kGeoZeros ? -1
         : !d.fused ? kRtUnfused
@@ -1444,9 +1447,9 @@ __global__ void __launch_bounds__(256) k_vpass(int n, const ImgDesc* __restrict_
 // Host-side launchers (called by the engine; all asynchronous on `stream`).
 // ------------------------------------------------------------------------------------------
 hipError_t launch_parse(int n, const uint8_t* blob, int64_t blob_bytes, const int64_t* offsets, const int32_t* lengths,
-                        const sdsj_op& op, int warm_bits, ImgDesc* descs, ImgTables* tables, hipStream_t s) {
-  hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, blob_bytes, offsets, lengths, op, warm_bits, descs,
-                     tables);
+                        const sdsj_op& op, int warm_bits, bool small, ImgDesc* descs, ImgTables* tables, hipStream_t s) {
+  hipLaunchKernelGGL(k_parse, dim3(n), dim3(64), 0, s, n, blob, blob_bytes, offsets, lengths, op, warm_bits, (int)small,
+                     descs, tables);
   return hipGetLastError();
 }
 hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* base, int64_t* total, int32_t* routes,
@@ -1484,7 +1487,9 @@ hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, Im
   return hipGetLastError();
 }
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
-  hipLaunchKernelGGL(k_idct, dim3(kIdctGrid, n), dim3(kIdctThreads), 0, s, n, descs, tables, scratch);
+  // (a few images: more workgroups per image, for latency)
+  hipLaunchKernelGGL(k_idct, dim3(n <= kSmallBatch ? 8 * kIdctGrid : kIdctGrid, n), dim3(kIdctThreads), 0, s, n, descs,
+                     tables, scratch);
   return hipGetLastError();
 }
 hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,
@@ -1528,14 +1533,14 @@ int64_t host_plan_frame(ImgDesc* d, int width, int height, const sdsj_op& op) {
   return plan_image(d, op, true);
 }
 
-int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status, uint64_t* routes) {
+int64_t host_plan_need(const uint8_t* jpg, int64_t n, const sdsj_op& op, int* status, uint64_t* routes, bool small) {
   ImgDesc d;
   static thread_local ImgTables t;
   HostReader rd{jpg};
   int st = parse_headers(rd, n, &d, &t, CopySink<HostReader>{rd});
   if (st == SDSJ_OK) st = setup_geometry(&d, &t);
   int64_t need = 0;
-  if (st == SDSJ_OK) need = plan_image(&d, op);
+  if (st == SDSJ_OK) need = plan_image(&d, op, false, small);
   *status = st;
   if (routes) {
     *routes = kAllRoutes;

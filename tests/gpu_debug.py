@@ -37,7 +37,7 @@ class ImgDescC(ctypes.Structure):
                 ("it_write", i64), ("fused", i32), ("tile_w", i32), ("ring_rows", i32), ("rs_fast", i32), ("t_rs", i64 * 4),
                 ("warm_bits", i32), ("scan_end_code", i32), ("scan_end_raw", i64),
                 ("rgb_pitch", i32), ("ent_groups", i32),
-                ("progressive", i32), ("pad3", i32), ("sos_pos", i64), ("off_ptab", i64),
+                ("progressive", i32), ("lat", i32), ("sos_pos", i64), ("off_ptab", i64),
                 ("off_tiles", i64), ("ntiles", i32), ("rs_lay", i32), ("plan_base", i64)]
 
 
