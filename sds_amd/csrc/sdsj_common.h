@@ -183,6 +183,14 @@ struct ImgDesc {
   int32_t ntiles;
   int32_t rs_lay;  // chroma layout of the specialised fused kernel (RsLay) when rs_fast > 0
   int64_t plan_base;  // k_plan_scan: the image's first scratch byte (the offsets above are relative until k_plan_apply)
+  // progressive block smoothing (jdcoefct.c smoothing_ok / decompress_smooth_data), set by k_prog at
+  // EOI and applied by k_idct: smooth != 0 when some coefficient 1..9 is still inexact; per component
+  // the scans' coef_bits for coefficients 0..9 after the last scan (sm_bits[0]) and before the
+  // component's last scan (sm_bits[1], -1 = never coded), the latter for iMCU rows past sm_good (the
+  // last scan ran out of data in row sm_good: jdcoefct.c last_good_iMCU_row)
+  int32_t smooth, sm_good;
+  int8_t sm_bits[2][kMaxComp][10];
+  int8_t sm_pad[4];
 };
 
 // One tile of k_unstuff's first pass: bytes it emits and split markers (RSTn, codes below SOF0) it

@@ -54,9 +54,8 @@ constexpr int kMaxSlots = 2 * kMaxComp;  // a DC and an AC table per component a
 // ------------------------------------------------------------------------------------------
 // Per-image decode tables in LDS.
 // ------------------------------------------------------------------------------------------
-struct EntTables {
-  static constexpr bool kTwoLevel = false;
-  uint16_t lut[kLutEntries];
+// Canonical bounds, symbols and the MCU context: shared by every table layout below.
+struct TabCommon {
   int32_t maxcode[kMaxSlots][18];
   int32_t valoff[kMaxSlots][18];
   uint8_t vals[kMaxSlots][256];
@@ -66,7 +65,37 @@ struct EntTables {
   uint32_t pk_dc[2], pk_ac[2], pk_c;  // per MCU block: DC slot, AC slot (4 bits each), component (2)
   uint32_t pad[4];
 };
+static_assert(sizeof(TabCommon) % 16 == 0, "tables are copied in 16-byte units");
+
+// Multi-symbol lookahead (the LB = 11 images' speculative pass): kMW bits per slot, 32-bit entries.
+//   bits 0-11  the single symbol whose code fits kMW bits: len | size << 4 | run << 8 (0: a longer code)
+//   bits 12-16 AC slots: the bits a group of >= 2 consecutive symbols consumes (codes and extra bits)
+//              when every code of the group lies in the window; 0: no group
+//   bits 17-23 the group's coefficient advance (sum of run + 1 over value symbols, 16 per ZRL), + 1
+//              when it ends with an EOB: the group applies at block position z iff z + this <= 64,
+//              so a block can only end at a group's last symbol
+//   bit  24    the group ends with an EOB
+// Groups skip the values, so only passes that need no AC values (warm-up, speculative) use them.
+constexpr int kMW = 10;
+constexpr int kMSlots = 4;  // LB = 11 images have at most 4 slots
+
+// LDS copy with the single-symbol LUT (LB = 10 images; a prefix of EntTables).
+struct LutTables : TabCommon {
+  static constexpr bool kTwoLevel = false;
+  uint16_t lut[kLutEntries];
+};
+
+// What k_enttab writes per image (HBM).
+struct EntTables : LutTables {
+  uint32_t mlut[kMSlots << kMW];
+};
 static_assert(sizeof(EntTables) % 16 == 0, "EntTables is copied in 16-byte units");
+
+// The speculative pass's LDS copy for LB = 11 images: the multi-symbol table instead of the LUT.
+struct SpecTables : TabCommon {
+  static constexpr bool kTwoLevel = false;
+  uint32_t mlut[kMSlots << kMW];
+};
 
 // Is this image decoded by the LB variant?  (LB = 11 when its tables fit 4 slots, else LB = 10.)
 template <int LB>
@@ -162,6 +191,38 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restric
     T.lut[i] = e;
   }
   __syncthreads();
+  if (lb == 11) {
+    // the multi-symbol table (kMW bits): the single entry of codes <= kMW bits, and for AC slots the
+    // group of symbols whose codes lie in the window, walked with the LUT above (each step reads
+    // the window's remaining bits, zero-padded, so a code of <= kMW - used bits is decided by real bits)
+    for (int i = t; i < (ns << kMW); i += kEntThreads) {
+      const int q = i >> kMW, k = i & ((1 << kMW) - 1);
+      const uint32_t e1 = T.lut[(q << 11) + (k << 1)];
+      uint32_t e = (e1 & 15) <= kMW ? e1 : 0u;
+      if (T.slot_src[q] & 4) {
+        int used = 0, dz = 0, n = 0, eob = 0;
+        while (used < kMW) {
+          const uint32_t f = T.lut[(q << 11) + (((k << used) & ((1 << kMW) - 1)) << 1)];
+          const int l = f & 15, s = (f >> 4) & 15, r = (f >> 8) & 15;
+          if (l == 0 || l > kMW - used) break;
+          if (s == 0 && r != 15) {  // EOB ends the group (and the block)
+            eob = 1;
+            used += l;
+            n++;
+            break;
+          }
+          const int step = s == 0 ? 16 : r + 1;
+          if (dz + step > 63) break;
+          used += l + s;
+          dz += step;
+          n++;
+        }
+        if (n >= 2) e |= ((uint32_t)used << 12) | ((uint32_t)(dz + eob) << 17) | ((uint32_t)eob << 24);
+      }
+      T.mlut[i] = e;
+    }
+    __syncthreads();
+  }
   const uint4* src = reinterpret_cast<const uint4*>(&T);
   uint4* dst = reinterpret_cast<uint4*>(&out[blockIdx.x]);
   for (int i = t; i < (int)(sizeof(EntTables) / 16); i += kEntThreads) dst[i] = src[i];
@@ -169,14 +230,30 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restric
 
 // The image's tables into LDS (the LUT part the variant uses, and everything after it).
 template <int LB>
-__device__ __forceinline__ int load_tables(EntTables& T, const EntTables* g) {
+__device__ __forceinline__ int load_tables(LutTables& T, const EntTables* g) {
   const uint4* src = reinterpret_cast<const uint4*>(g);
   uint4* dst = reinterpret_cast<uint4*>(&T);
-  constexpr int kLut16 = (int)(sizeof(T.lut) / 16), kAll16 = (int)(sizeof(EntTables) / 16);
+  constexpr int kCom16 = (int)(sizeof(TabCommon) / 16);
   const int ns = g->nslots;
-  const int used16 = variant_owns<LB>(ns) ? ((ns << LB) * 2 + 15) / 16 : 0;
-  for (int i = threadIdx.x; i < kAll16; i += blockDim.x)
-    if (i < used16 || i >= kLut16) dst[i] = src[i];
+  const int used16 = kCom16 + (variant_owns<LB>(ns) ? ((ns << LB) * 2 + 15) / 16 : 0);
+  for (int i = threadIdx.x; i < used16; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  return ns;
+}
+
+// The speculative pass's tables for LB = 11 images: the common part and the multi-symbol table.
+__device__ __forceinline__ int load_tables(SpecTables& T, const EntTables* g) {
+  const uint4* src = reinterpret_cast<const uint4*>(g);
+  const uint4* msrc = reinterpret_cast<const uint4*>(g->mlut);
+  uint4* dst = reinterpret_cast<uint4*>(&T);
+  uint4* mdst = reinterpret_cast<uint4*>(T.mlut);
+  constexpr int kCom16 = (int)(sizeof(TabCommon) / 16);
+  const int ns = g->nslots;
+  const int m16 = variant_owns<11>(ns) ? (ns << kMW) * 4 / 16 : 0;
+  for (int i = threadIdx.x; i < kCom16 + m16; i += blockDim.x) {
+    if (i < kCom16) dst[i] = src[i];
+    else mdst[i - kCom16] = msrc[i - kCom16];
+  }
   __syncthreads();
   return ns;
 }
@@ -427,6 +504,35 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   b.pos += tot;
 }
 
+// One step through the multi-symbol table (SpecTables::mlut): a group of AC symbols that ends inside
+// the block (z + advance <= 64) at once, else one symbol -- the DC symbol (with its value when kVal),
+// or an AC symbol near the block end.  Gives the (s, r) next_z takes for the step: a group of value /
+// ZRL symbols advances like one symbol of run dz - 1, a group ending in EOB like an EOB.  The group's
+// symbols are exactly the ones single decodes would give (k_enttab walks them with the same LUT).
+template <bool kVal, class TT, int Q>
+__device__ __forceinline__ void decode_step(const TT& T, BitsQ<Q>& b, int slot, bool isdc, int z, int& s, int& r,
+                                            int& val, int& bad) {
+  bits_pull(b);
+  const uint32_t hi = (uint32_t)(b.buf >> 32);
+  const uint32_t e = T.mlut[(slot << kMW) + (hi >> (32 - kMW))];
+  int l = e & 15, sz = (e >> 4) & 15, rr = (e >> 8) & 15;
+  const int mb = (e >> 12) & 31, mdz = (e >> 17) & 127, eob = (e >> 24) & 1;
+  const bool multi = (mb != 0) & (z + mdz <= 64);
+  if (!multi && l == 0) long_code<kMW>(T, slot, isdc, hi, l, sz, rr, bad);
+  if (kVal) {  // (only DC values are used: a group is never a DC step)
+    const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - sz) & 31);
+    const uint32_t half = (1u << sz) >> 1;
+    const int ext = x < half ? (int)x - (int)((1u << sz) - 1u) : (int)x;
+    val = sz != 0 ? ext : 0;
+  }
+  const int tot = multi ? mb : l + sz;
+  s = multi ? (eob ^ 1) : sz;
+  r = multi ? (eob ? 0 : mdz - 1) : rr;
+  b.buf <<= tot;
+  b.nb -= tot;
+  b.pos += tot;
+}
+
 // decode_mcu's k loop: DC -> k = 1; AC value -> k += r + 1; ZRL -> k += 16; EOB -> done.
 // Returns true when the block is complete (z wraps to 0).  Branch-free: the step is r + 1 for a DC
 // symbol (r = 0), an AC value or ZRL (r = 15), and 64 for EOB.
@@ -467,7 +573,7 @@ __device__ inline int block_excl_scan(int v, int* tmp, int* total) {
 // ------------------------------------------------------------------------------------------
 // k_entsync
 // ------------------------------------------------------------------------------------------
-template <int NT, class TT = EntTables>
+template <int NT, class TT = LutTables>
 struct LdsSyncT {
   TT T;
   int32_t tmp[NT];  // block_excl_scan scratch
@@ -492,9 +598,10 @@ using LdsSync = LdsSyncT<kEntThreads>;
 // Huffman self-synchronisation; the MCU phase takes ~1k bits to lock on).  Then decode to the first
 // block boundary at or after end_bit, recording every block boundary.  A segment's first
 // subsequence starts exactly at its (known) state.
-template <int LB>
-__device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
+template <int LB, class TT>
+__device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
                          uint32_t seg_start, uint32_t warm) {
+  constexpr bool kMulti = std::is_same_v<TT, SpecTables>;  // LB = 11: the multi-symbol table
   // (bits at or beyond S.lim_bit read as zeros)
   const uint32_t start = S.start_bit, end = S.end_bit;
   const uint32_t ws = S.first ? start : (start - seg_start > warm ? start - warm : seg_start);
@@ -513,17 +620,25 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
 #pragma unroll
       for (int u = 0; u < kSpecGroup; u++) {
         if (warmup) {
-          bits_pull(b);
           const bool isdc = z == 0;
           const int slot = isdc ? sdc : sac;
-          const uint32_t hi = (uint32_t)(b.buf >> 32);
-          const uint32_t e = T.lut[(slot << LB) + (hi >> (32 - LB))];
-          int l = e & 15, sz = (e >> 4) & 15, r = (e >> 8) & 15;
-          if (l == 0) long_code<LB>(T, slot, isdc, hi, l, sz, r, bad);
-          const int tot = l + sz;
-          b.buf <<= tot;
-          b.nb -= tot;
-          b.pos += tot;
+          int sz, r;
+          if constexpr (kMulti) {
+            int unused;
+            decode_step<false>(T, b, slot, isdc, z, sz, r, unused, bad);
+          } else {
+            bits_pull(b);
+            const uint32_t hi = (uint32_t)(b.buf >> 32);
+            const uint32_t e = T.lut[(slot << LB) + (hi >> (32 - LB))];
+            int l = e & 15;
+            sz = (e >> 4) & 15;
+            r = (e >> 8) & 15;
+            if (l == 0) long_code<LB>(T, slot, isdc, hi, l, sz, r, bad);
+            const int tot = l + sz;
+            b.buf <<= tot;
+            b.nb -= tot;
+            b.pos += tot;
+          }
           if (kStats) nsym++;
           if (next_z(z, sz, r)) {
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
@@ -553,7 +668,8 @@ __device__ int spec_pass(const EntTables& T, const BlkCtx& K, const uint32_t* sr
         if (run) {
           int s, r, val;
           const bool isdc = z == 0;
-          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+          if constexpr (kMulti) decode_step<true>(T, b, isdc ? sdc : sac, isdc, z, s, r, val, bad);
+          else decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           const bool done = next_z(z, s, r);
@@ -674,8 +790,9 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
 
 // The speculative pass's LDS: tables, the layout scan's scratch, statistics -- not the sync kernel's
 // task / scan arrays (5 KB that cost it two workgroups per CU)
+template <int LB>
 struct LdsSpec {
-  EntTables T;
+  std::conditional_t<LB == 11, SpecTables, LutTables> T;
   int32_t tmp[kEntThreads];
   int32_t nsub;
   unsigned long long sym[1], it[1], t0, t1;
@@ -687,9 +804,11 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
                               uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
-  __shared__ LdsSpec L;
+  __shared__ LdsSpec<LB> L;
   const int t = threadIdx.x;
-  const int ns = load_tables<LB>(L.T, &tables[img]);
+  int ns;
+  if constexpr (LB == 11) ns = load_tables(L.T, &tables[img]);
+  else ns = load_tables<LB>(L.T, &tables[img]);
   if (!variant_owns<LB>(ns)) return;
   if (t == 0) {
     L.sym[0] = 0;
@@ -990,7 +1109,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
                                uint8_t* __restrict__ scratch) {
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
-  using TT = std::conditional_t<LB == 11, WriteTables, EntTables>;
+  using TT = std::conditional_t<LB == 11, WriteTables, LutTables>;
   __shared__ LdsWriteT<TT> L;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   int ns;

@@ -127,6 +127,7 @@ struct PLds {
   alignas(16) int16_t blk[64];  // the block an AC refinement scan updates (read-modify-write in LDS)
   int32_t qh[4], qv[4], qbo[4], qdsl[4], ldc[4];  // interleaved DC scans: per scan position h, v, block
                                                   // offset in the MCU, DC table slot, DC predictor
+  int32_t ins_m;  // the MCU in which the scan ran out of data (-1: none); in LDS, off the MCU loop's registers
 };
 
 // jdhuff.c jpeg_huff_decode: codes of <= 9 bits come from the scan position's lookahead table in one
@@ -462,6 +463,11 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
   }
   for (int c = 0; c < kMaxComp; c++) P->latched[c] = 0;
   d->t_spec = d->t_sync = d->t_scan = d->t_write = 0;
+  // block smoothing state (jdphuff.c start_pass_phuff_decoder coef_bits / prev_coef_bits)
+  d->smooth = 0;
+  for (int c = 0; c < kMaxComp; c++)
+    for (int k = 0; k < 10; k++) d->sm_bits[0][c][k] = d->sm_bits[1][c][k] = -1;
+  int nscans = 0, good = 1 << 30;
   int restart_interval = d->restart_interval;
   // first block of components 1 and 2 within an MCU
   const int boff1 = d->ncomp > 1 ? d->comp[0].h * d->comp[0].v : 0;
@@ -509,7 +515,12 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
       } else if (ss != 0) {
         if (ta[q] > 3 || !pderive(P, L, 4 + ta[q], q)) return SDSJ_CORRUPT;
       }
+      // coef_bits of the band (the smoothing reads coefficients 0..9), the previous values kept
+      for (int k = ss < 1 ? ss : 1; k < 10; k++) d->sm_bits[1][c][k] = nscans > 0 ? d->sm_bits[0][c][k] : 0;
+      for (int k = ss; k <= se && k < 10; k++) d->sm_bits[0][c][k] = (int8_t)al;
     }
+    nscans++;
+    good = 1 << 30;
     // the scan's geometry in registers (descriptor reads would repeat for every block: the
     // coefficient stores may alias them as far as the compiler knows)
     int sh[4] = {1, 1, 1, 1}, sv[4] = {1, 1, 1, 1}, sbw[4] = {0, 0, 0, 0}, sbo[4] = {0, 0, 0, 0};
@@ -558,6 +569,7 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
     };
     const bool refine = ss != 0 && ah != 0;
     int64_t gn = ns == 1 ? gpos() : 0;
+    L.ins_m = -1;
     for (int m = 0; m < nmcu; m++) {
       const int64_t g1 = gn;
       if (ns == 1) {
@@ -578,6 +590,7 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
       }
       if (restart_interval) {
         if (restarts_left == 0) {
+          if (b.insufficient && L.ins_m < 0) L.ins_m = m - 1;
           if (pprocess_restart(b, &next_num)) return SDSJ_CORRUPT;
           ldc0 = L.ldc[0] = L.ldc[1] = L.ldc[2] = L.ldc[3] = 0;
           eobrun = 0;
@@ -585,11 +598,17 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
         }
         restarts_left--;
       }
+      // (L.ins_m: the MCU in which this scan ran out of data -- the one before the first MCU skipped
+      // or restarted with insufficient data)
       if (refine) {
         if (!b.insufficient) prefine(b, L, asl0, coef + g1 * 64, ss, se, al, &eobrun);
+        else if (L.ins_m < 0) L.ins_m = m - 1;
         continue;
       }
-      if (b.insufficient) continue;  // the MCU's coefficients stay as they are
+      if (b.insufficient) {  // the MCU's coefficients stay as they are
+        if (L.ins_m < 0) L.ins_m = m - 1;
+        continue;
+      }
       if (ns == 1) {
         pblock(b, L, dsl0, asl0, 0, coef + g1 * 64, ss, se, ah, al, &ldc0, &eobrun);
         continue;
@@ -611,6 +630,11 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
           }
       }
     }
+    if (b.insufficient && L.ins_m < 0) L.ins_m = nmcu - 1;
+    if (L.ins_m >= 0) {  // later iMCU rows keep the previous scan's smoothing parameters
+      const int r = ns == 1 ? L.ins_m / cwb : L.ins_m / mcux;
+      good = ns == 1 && ncomp > 1 ? r / cv0 : r;
+    }
     if (b.eof) return SDSJ_CORRUPT;  // the input ended inside the scan (Pillow: truncated)
     if (!b.hit_marker && pnext_marker(b) < 0) return SDSJ_CORRUPT;
     // jdmarker.c read_markers until the next SOS or EOI
@@ -621,6 +645,20 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
       if (m == 0xD9) {
         // k_idct reads each component's latched table from slot c
         for (int c = 0; c < d->ncomp; c++) d->comp[c].tq = c;
+        // jdcoefct.c smoothing_ok: every component's latched Q00..Q30 nonzero and its DC at least
+        // partly known; useful when a coefficient 1..9 of some component is not exact
+        bool ok = true, useful = false;
+        for (int c = 0; c < d->ncomp; c++) {
+          const uint16_t* qc = t->qt[c];
+          ok = ok && qc[0] && qc[1] && qc[8] && qc[16] && qc[9] && qc[2] && qc[3] && qc[10] && qc[17] && qc[24] &&
+               d->sm_bits[0][c][0] >= 0;
+          for (int k = 1; k < 10; k++) {
+            useful = useful || d->sm_bits[0][c][k] != 0;
+            if (nscans <= 1) d->sm_bits[1][c][k] = -1;
+          }
+        }
+        d->smooth = ok && useful;
+        d->sm_good = good;
         return SDSJ_OK;
       }
       if ((m >= 0xD0 && m <= 0xD7) || m == 0x01) {
@@ -668,13 +706,16 @@ __global__ void __launch_bounds__(256) k_prog_zero(const ImgDesc* __restrict__ d
 
 // Zigzag -> natural order for the blocks of the progressive images: one block per thread, its 128
 // bytes in registers, the permutation resolved at compile time (no LDS, so the launch stays cheap
-// for batches without progressive images).
+// for batches without progressive images).  Images to be smoothed also get their DC plane (int16 per
+// block, decode order) in the plane area, which k_idct writes only later.
 __global__ void __launch_bounds__(256) k_prog_unzig(const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
                                                     const int32_t* __restrict__ routes, int cap) {
   if ((int)blockIdx.x >= routes[kRtProg]) return;
   const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[blockIdx.x]];
   if (d->status != SDSJ_OK) return;
   int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
+  const bool smooth = d->smooth != 0;
+  int16_t* dcs = reinterpret_cast<int16_t*>(scratch + d->off_planes);
   const int64_t nb = d->total_blocks;
   for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < nb; i += (int64_t)gridDim.y * 256) {
     uint4* p = reinterpret_cast<uint4*>(coef + i * 64);
@@ -696,13 +737,134 @@ __global__ void __launch_bounds__(256) k_prog_unzig(const ImgDesc* __restrict__ 
     }
 #pragma unroll
     for (int q = 0; q < 8; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    if (smooth) dcs[i] = (int16_t)(o[0] & 0xFFFF);  // the DC plane k_prog_smooth reads
+  }
+}
+
+// pred = num / (Q << 8) rounded half away from zero, clamped below 2^Al when Al > 0
+// (jdcoefct.c decompress_smooth_data)
+__device__ __forceinline__ int smooth_pred(int64_t num, int64_t q, int al) {
+  int pred = (int)(((q << 7) + (num >= 0 ? num : -num)) / (q << 8));
+  if (al > 0 && pred >= (1 << al)) pred = (1 << al) - 1;
+  return num >= 0 ? pred : -pred;
+}
+
+// Block smoothing of the progressive images whose coefficients 1..9 are not all exact after the
+// last scan (ImgDesc::smooth, k_prog): jdcoefct.c decompress_smooth_data, one thread per block of the
+// image in decode order.  Zero coefficients AC01 AC10 AC20 AC11 AC02 (and AC03 AC12 AC21 AC30 and
+// the DC itself when the component has no AC data at all) get estimates from the DC values of the
+// block's 5x5 neighbourhood, read from the DC plane k_prog_unzig copied into the (not yet written)
+// plane area -- libjpeg likewise reads the neighbours unmodified while it smooths a copy of the block.
+// Rows: jdcoefct.c's per-iMCU-row choice (the last iMCU row's real rows only); columns clamped to the
+// component's width in blocks (tests/test_gpu_parity.py: bit-exact against the Pillow-pinned CPU restatement).
+__global__ void __launch_bounds__(256) k_prog_smooth(const ImgDesc* __restrict__ descs,
+                                                     const ImgTables* __restrict__ tables,
+                                                     uint8_t* __restrict__ scratch, const int32_t* __restrict__ routes,
+                                                     int cap) {
+  if ((int)blockIdx.x >= routes[kRtProg]) return;
+  const int img = route_list(routes, cap, kRtProg)[blockIdx.x];
+  const ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || !d->smooth) return;
+  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
+  const int16_t* dcs = reinterpret_cast<const int16_t*>(scratch + d->off_planes);
+  const int ncomp = d->ncomp, bpm = d->bpm, mcux = d->mcux;
+  const int64_t nb = d->total_blocks;
+  for (int64_t g = (int64_t)blockIdx.y * 256 + threadIdx.x; g < nb; g += (int64_t)gridDim.y * 256) {
+    // block g -> component, block row / column (jdcoefct.c MCU order: components in turn, h x v each)
+    int c = 0, by, bx;
+    if (ncomp == 1) {
+      by = (int)(g / mcux);
+      bx = (int)(g - (int64_t)by * mcux);
+    } else {
+      const int m = (int)(g / bpm), b = (int)(g - (int64_t)m * bpm);
+      c = d->blk_comp[b];
+      const int my = m / mcux, mx = m - my * mcux;
+      bx = mx * d->comp[c].h + d->blk_dx[b];
+      by = my * d->comp[c].v + d->blk_dy[b];
+    }
+    const CompDesc& cd = d->comp[c];
+    const int h = ncomp == 1 ? 1 : cd.h, v = ncomp == 1 ? 1 : cd.v;
+    const int wib = (cd.dw + 7) >> 3, hib = (cd.dh + 7) >> 3;
+    if (bx >= wib || by >= hib) continue;  // (padding blocks: never output)
+    const int total = ncomp == 1 ? hib : d->mcuy, imcu = by / v, brow = by - imcu * v;
+    int block_rows = v;
+    if (imcu == total - 1) {
+      block_rows = hib % v;
+      if (block_rows == 0) block_rows = v;
+    }
+    const int ibr = imcu * block_rows + brow, ibrs = block_rows * total;
+    int rows[5];
+    rows[2] = by;
+    rows[1] = ibr > 0 ? by - 1 : by;
+    rows[0] = ibr > 1 ? by - 2 : rows[1];
+    rows[3] = ibr < ibrs - 1 ? by + 1 : by;
+    rows[4] = ibr < ibrs - 2 ? by + 2 : rows[3];
+    int boff = 0;  // first MCU block of component c
+    for (int q = 0; q < c; q++) boff += d->comp[q].h * d->comp[q].v;
+    int DC[5][5];
+    for (int i = 0; i < 5; i++)
+      for (int jx = 0; jx < 5; jx++) {
+        int x = bx + jx - 2;
+        x = x < 0 ? 0 : (x > wib - 1 ? wib - 1 : x);
+        const int y = rows[i];
+        const int64_t gg = ncomp == 1 ? (int64_t)y * mcux + x
+                                      : ((int64_t)(y / v) * mcux + x / h) * bpm + boff + (y % v) * h + (x % h);
+        DC[i][jx] = dcs[gg];
+      }
+    const int8_t* cb = d->sm_bits[imcu > d->sm_good ? 1 : 0][c];
+    bool change_dc = true;
+    for (int k = 1; k < 10; k++) change_dc = change_dc && cb[k] == -1;
+    const uint16_t* qt = tables[img].qt[c];  // (k_prog: the component's latched table sits in slot c)
+    const int64_t Q00 = qt[0];
+    int16_t* blk = coef + g * 64;
+    // DCnn of jdcoefct.c: DC01 .. DC25 row by row (DC13 = this block)
+#define SD(n) DC[((n) - 1) / 5][((n) - 1) % 5]
+    auto est = [&](int nat, int zz, int64_t num) {
+      const int al = cb[zz];
+      if (al != 0 && blk[nat] == 0) blk[nat] = (int16_t)smooth_pred(Q00 * num, qt[nat], al);
+    };
+    est(1, 1,
+        change_dc ? (-SD(1) - SD(2) + SD(4) + SD(5) - 3 * SD(6) + 13 * SD(7) - 13 * SD(9) + 3 * SD(10) - 3 * SD(11) +
+                     38 * SD(12) - 38 * SD(14) + 3 * SD(15) - 3 * SD(16) + 13 * SD(17) - 13 * SD(19) + 3 * SD(20) -
+                     SD(21) - SD(22) + SD(24) + SD(25))
+                  : (-7 * SD(11) + 50 * SD(12) - 50 * SD(14) + 7 * SD(15)));
+    est(8, 2,
+        change_dc ? (-SD(1) - 3 * SD(2) - 3 * SD(3) - 3 * SD(4) - SD(5) - SD(6) + 13 * SD(7) + 38 * SD(8) +
+                     13 * SD(9) - SD(10) + SD(16) - 13 * SD(17) - 38 * SD(18) - 13 * SD(19) + SD(20) + SD(21) +
+                     3 * SD(22) + 3 * SD(23) + 3 * SD(24) + SD(25))
+                  : (-7 * SD(3) + 50 * SD(8) - 50 * SD(18) + 7 * SD(23)));
+    est(16, 3,
+        change_dc ? (SD(3) + 2 * SD(7) + 7 * SD(8) + 2 * SD(9) - 5 * SD(12) - 14 * SD(13) - 5 * SD(14) + 2 * SD(17) +
+                     7 * SD(18) + 2 * SD(19) + SD(23))
+                  : (-SD(3) + 13 * SD(8) - 24 * SD(13) + 13 * SD(18) - SD(23)));
+    est(9, 4,
+        change_dc ? (-SD(1) + SD(5) + 9 * SD(7) - 9 * SD(9) - 9 * SD(17) + 9 * SD(19) + SD(21) - SD(25))
+                  : (-SD(2) + SD(4) - SD(6) + 10 * SD(7) - 10 * SD(9) + SD(10) + SD(16) - 10 * SD(17) + 10 * SD(19) -
+                     SD(20) + SD(22) - SD(24)));
+    est(2, 5,
+        change_dc ? (2 * SD(7) - 5 * SD(8) + 2 * SD(9) + SD(11) + 7 * SD(12) - 14 * SD(13) + 7 * SD(14) + SD(15) +
+                     2 * SD(17) - 5 * SD(18) + 2 * SD(19))
+                  : (-SD(11) + 13 * SD(12) - 24 * SD(13) + 13 * SD(14) - SD(15)));
+    if (change_dc) {
+      est(3, 6, SD(7) - SD(9) + 2 * SD(12) - 2 * SD(14) + SD(17) - SD(19));
+      est(10, 7, SD(7) - 3 * SD(8) + SD(9) - SD(17) + 3 * SD(18) - SD(19));
+      est(17, 8, SD(7) - SD(9) - 3 * SD(12) + 3 * SD(14) + SD(17) - SD(19));
+      est(24, 9, SD(7) + 2 * SD(8) + SD(9) - SD(17) - 2 * SD(18) - SD(19));
+      const int64_t num =
+          Q00 * (-2 * SD(1) - 6 * SD(2) - 8 * SD(3) - 6 * SD(4) - 2 * SD(5) - 6 * SD(6) + 6 * SD(7) + 42 * SD(8) +
+                 6 * SD(9) - 6 * SD(10) - 8 * SD(11) + 42 * SD(12) + 152 * SD(13) + 42 * SD(14) - 8 * SD(15) -
+                 6 * SD(16) + 6 * SD(17) + 42 * SD(18) + 6 * SD(19) - 6 * SD(20) - 2 * SD(21) - 6 * SD(22) -
+                 8 * SD(23) - 6 * SD(24) - 2 * SD(25));
+      blk[0] = (int16_t)smooth_pred(num, Q00, 0);
+    }
+#undef SD
   }
 }
 
 // One wave per progressive image: its lane walks all the scans (see the header); kProgLanes images per workgroup,
 // each with its derived tables in LDS.
 constexpr int kProgLanes = 1;  // (lanes of one wave walking different images would diverge on every branch)
-__global__ void __launch_bounds__(kProgLanes) k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables,
+__global__ void __launch_bounds__(kProgLanes) __attribute__((amdgpu_waves_per_eu(5))) k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables,
                                              const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
                                              const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
                                              const int32_t* __restrict__ routes, int cap) {
@@ -726,6 +888,7 @@ hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* 
   hipLaunchKernelGGL(k_prog, dim3((n + kProgLanes - 1) / kProgLanes), dim3(kProgLanes), 0, s, descs, tables, blob,
                      offsets, lengths, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog_unzig, dim3(n, 8), dim3(256), 0, s, descs, scratch, routes, cap);
+  hipLaunchKernelGGL(k_prog_smooth, dim3(n, 8), dim3(256), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 

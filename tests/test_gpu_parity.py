@@ -283,13 +283,38 @@ def test_progressive_bench_sized_images_vs_oracle(engine):
             np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res), err_msg=f"image {k} at {res}")
 
 
+def test_progressive_incomplete_scans_smoothing_vs_oracle(engine):
+    """Progressive images that end (EOI) after each of their scans: k_prog records the coefficient bits
+    and k_prog_smooth applies libjpeg-turbo's block smoothing (jdcoefct.c decompress_smooth_data, 5x5
+    DC neighbourhood, DC interpolation) before k_idct -- bit-exact against the oracle, which is pinned
+    to PIL on the same construction (test_oracle_progressive_smoothing_matches_pil).  Full-resolution
+    HWC decodes and a crop + resize with flips, mixed in one batch with complete images."""
+    from tests.golden.synth import progressive_jpegs
+    cases = []
+    for seed, mw, mh in ((5, 400, 300), (7, 40, 40)):
+        for j in progressive_jpegs(seed, 10, mw, mh):
+            sos = [i for i in range(2, len(j) - 1) if j[i] == 0xFF and j[i + 1] == 0xDA][1:]
+            cases += [j[:c] + b"\xff\xd9" for c in sos] + [j]
+    for j in cases[::7]:  # full resolution (the same-size shortcut: no resample)
+        ref = O.decode(j)
+        got, st = engine.decode_resize([j], ref.shape[:2], layout="hwc")
+        assert st[0] == 0
+        np.testing.assert_array_equal(got[0].cpu().numpy(), ref)
+    res = (48, 40)
+    flips = [k % 3 == 0 for k in range(len(cases))]
+    got, st = engine.decode_resize(cases, res, flip=flips)
+    assert (st == 0).all(), st
+    for k, j in enumerate(cases):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res, flip=flips[k]), err_msg=f"case {k}")
+
+
 def test_progressive_dri_between_scans_vs_oracle(engine):
     """A DRI segment between the scans of a progressive image (restart intervals that change per
     scan, jdmarker.c get_dri), with non-zero and zero intervals, against the oracle: status, and
-    pixels where the oracle decodes.  (The scans after a non-zero DRI lack their RSTn markers,
-    so they are damaged streams: PIL also smooths such blocks (jdcoefct.c decompress_smooth_data,
-    not restated), and on 6 of these 24 images differs from the oracle on <= 0.3 % of the pixels --
-    parity unpinned against PIL there, as for the other damaged progressive streams)"""
+    pixels where the oracle decodes.  (The scans after a non-zero DRI lack their RSTn markers, so
+    they are damaged streams: on 6 of these 24 images PIL differs from the oracle in a few pixels
+    swapped between 0 and 255 -- garbage coefficients past 16 bits, which Pillow's SIMD IDCT wraps
+    and the C jpeg_idct_islow restated here does not: DESIGN.md §2, divergence 2.)"""
     from tests.golden.synth import progressive_jpegs
     cases = []
     for j in progressive_jpegs(11, 8):
