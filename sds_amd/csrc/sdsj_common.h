@@ -141,7 +141,7 @@ struct ImgDesc {
   int64_t off_seg;      // int32 [nseg + 2]: segment start bytes, then the stream length
   int64_t off_sub;      // SubState [nsub_cap]
   int64_t off_rec;      // SyncRec [nsub_cap][kRec]
-  int64_t off_coef;     // int16 [total_blocks * 64]
+  int64_t off_coef;     // int16 [total_blocks * 64], zigzag order within a block
   int64_t off_planes;
   int64_t off_rgb;      // uint8 RGB rows [src_y0, src_y1) x [src_x0, src_x0 + src_w)
   int64_t off_tmp;      // uint8 horizontal-pass output (yl - yf) x out_w x 3

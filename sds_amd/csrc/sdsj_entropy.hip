@@ -16,10 +16,11 @@
 //                  until every entry equals its predecessor's exit (Jacobi fixed point);
 //               3. segmented exclusive scan of (blocks completed, DC differences) -> every
 //                  subsequence's first block index and DC predictors (prediction resets at RSTn).
-//   k_entwrite  4. verified decode: each lane assembles its current 8x8 block in LDS (natural order,
-//                  jpeg_natural_order with its 16 guard entries); the wave flushes completed blocks
-//                  cooperatively as 128-byte stores.  A block belongs to the subsequence in which
-//                  its DC symbol starts (the owner decodes past its end to finish it).
+//   k_entwrite  4. verified decode: each lane assembles its current 8x8 block in LDS (zigzag order,
+//                  positions past 63 at 63 like jpeg_natural_order's guard entries: k_idct reads
+//                  zigzag blocks); the wave flushes completed blocks cooperatively as 128-byte stores.
+//                  A block belongs to the subsequence in which its DC symbol starts (the owner
+//                  decodes past its end to finish it).
 //
 // Symbol decoding: 2^LB-entry lookup of (code length, size, run) -- LB = 11 for images using at
 // most 4 Huffman tables, LB = 10 otherwise (two kernel variants, each skips the other's images)
@@ -59,7 +60,6 @@ struct TabCommon {
   int32_t maxcode[kMaxSlots][18];
   int32_t valoff[kMaxSlots][18];
   uint8_t vals[kMaxSlots][256];
-  uint8_t nat[80];
   int32_t slot_src[kMaxSlots];  // (kind << 2) | id of the table in each slot (kind 0 = DC, 1 = AC)
   int32_t nslots;
   uint32_t pk_dc[2], pk_ac[2], pk_c;  // per MCU block: DC slot, AC slot (4 bits each), component (2)
@@ -84,6 +84,8 @@ struct LutTables : TabCommon {
   static constexpr bool kTwoLevel = false;
   uint16_t lut[kLutEntries];
 };
+
+static_assert(sizeof(LutTables) % 16 == 0, "LutTables is copied in 16-byte units");
 
 // What k_enttab writes per image (HBM).
 struct EntTables : LutTables {
@@ -111,7 +113,7 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restric
   const ImgDesc* d = &descs[blockIdx.x];
   if (d->status != SDSJ_OK || d->progressive) return;
   const ImgTables* tb = &tables[blockIdx.x];
-  __shared__ EntTables T;
+  __shared__ LutTables T;  // (the multi-symbol table goes straight to HBM: nothing here reads it back)
   __shared__ int32_t lim[kMaxSlots][12];
   const int t = threadIdx.x;
   if (t == 0) {
@@ -143,7 +145,6 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restric
     T.pk_c = pc;
     T.pad[0] = T.pad[1] = T.pad[2] = T.pad[3] = 0;
   }
-  for (int i = t; i < 80; i += kEntThreads) T.nat[i] = (uint8_t)natural_order(i);
   __syncthreads();
   const int ns = T.nslots;
   const int lb = (ns << 11) <= kLutEntries ? 11 : 10;  // the variant that will decode this image
@@ -219,13 +220,12 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restric
         }
         if (n >= 2) e |= ((uint32_t)used << 12) | ((uint32_t)(dz + eob) << 17) | ((uint32_t)eob << 24);
       }
-      T.mlut[i] = e;
+      out[blockIdx.x].mlut[i] = e;
     }
-    __syncthreads();
   }
   const uint4* src = reinterpret_cast<const uint4*>(&T);
   uint4* dst = reinterpret_cast<uint4*>(&out[blockIdx.x]);
-  for (int i = t; i < (int)(sizeof(EntTables) / 16); i += kEntThreads) dst[i] = src[i];
+  for (int i = t; i < (int)(sizeof(LutTables) / 16); i += kEntThreads) dst[i] = src[i];
 }
 
 // The image's tables into LDS (the LUT part the variant uses, and everything after it).
@@ -460,7 +460,6 @@ struct WriteTables {
   int32_t maxcode[4][18];
   int32_t valoff[4][18];
   uint8_t vals[4][256];
-  uint8_t nat[80];
   uint32_t pk_dc[2], pk_ac[2], pk_c;
   uint32_t pad[3];
 };
@@ -1092,7 +1091,6 @@ __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tm
   const uint32_t* gv = reinterpret_cast<const uint32_t*>(g->vals);
   uint32_t* wvls = reinterpret_cast<uint32_t*>(W.vals);
   for (int i = t; i < 4 * 64; i += kEntThreads) wvls[i] = gv[i];
-  for (int i = t; i < 80; i += kEntThreads) W.nat[i] = g->nat[i];
   if (t == 0) {
     W.pk_dc[0] = g->pk_dc[0];
     W.pk_dc[1] = g->pk_dc[1];
@@ -1191,8 +1189,10 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           bad |= sb;
           // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
           pc += isdc ? val : 0;
-          const int wpos = T.nat[z + r];  // (natural_order[0] = 0 for the DC symbol)
-          L.stage[((writing & (isdc | (s != 0))) ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
+          // zigzag position k + r (jpeg_natural_order's guard entries send positions past 63 to 63)
+          const int zp = z + r, wpos = zp < 63 ? zp : 63;
+          const bool put = writing & (isdc | (s != 0));
+          L.stage[(put ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
           // block end by selects (no branches): the component's predictor back, the next block's out
           const bool done = next_z(z, s, r);
           ready = done & writing;

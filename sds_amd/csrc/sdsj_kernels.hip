@@ -986,25 +986,17 @@ __global__ void __launch_bounds__(64) k_scanmap(int n, const uint8_t* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// k_idct: dequantisation + jpeg_idct_islow; 8 threads per block, 32 blocks per iteration.
+// k_idct: dequantisation + jpeg_idct_islow; one block per thread, 256 blocks per iteration.
 // ------------------------------------------------------------------------------------------
 constexpr int kIdctThreads = 256;
-constexpr int kIdctBlocks = kIdctThreads / 8;
 #ifndef SDSJ_IDCT_GRID
 #define SDSJ_IDCT_GRID 8
 #endif
 constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides over 8-block groups)
-constexpr int kWsStride = 72;  // ints per block in LDS (conflict-free column reads per half-wave)
 
-// Work unit = one wave: 8 horizontally adjacent blocks of one component (a "group"), so each of
-// the 8 row stores of the wave writes 64 contiguous bytes of a plane row.  8 threads per block
-// (thread r: row r, then column r); the 8 threads of a block share a wave, so the LDS transposes
-// need only in-wave ordering, no workgroup barrier.
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
+// Work unit = a group: 8 horizontally adjacent blocks of one component, one per thread, so each of
+// a block's 8 row stores joins the group's other 7 in 64 contiguous bytes of a plane row.  The
+// block stays in registers through both passes (64 values), so there is no LDS transpose.
 __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __restrict__ descs,
                                                        const ImgTables* __restrict__ tables,
                                                        uint8_t* __restrict__ scratch) {
@@ -1012,7 +1004,6 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   if (img >= n) return;
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
-  __shared__ alignas(16) int ws[kIdctBlocks * kWsStride];
   __shared__ alignas(16) int32_t qt[kMaxComp][64];
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
   __shared__ int32_t gstart[kMaxComp + 1], ngx[kMaxComp], cbw[kMaxComp], ch_[kMaxComp], cv_[kMaxComp], cpitch[kMaxComp];
@@ -1021,7 +1012,8 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
   __shared__ int64_t cplane[kMaxComp];
   const int t = threadIdx.x;
   const int ncomp = d->ncomp, bpm = d->bpm, mcux = d->mcux;
-  for (int i = t; i < ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][i % 64];
+  // quantisation tables in zigzag order (the coefficient blocks' order)
+  for (int i = t; i < ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][natural_order(i % 64)];
   if (t < bpm) binv[d->blk_comp[t]][d->blk_dy[t] * 4 + d->blk_dx[t]] = t;
   if (t == 0) {
     // only the blocks whose pixels the colour/resample passes read: the source rectangle
@@ -1054,8 +1046,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
     gstart[ncomp] = acc;
   }
   __syncthreads();
-  const int lane = t & 63, wv = t >> 6, lb = lane >> 3, r = lane & 7;
-  int* W = ws + (wv * 8 + lb) * kWsStride;
+  const int lb = t & 7;  // this lane's block within its group
   const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
   uint8_t* planes = scratch + d->off_planes;
   const int ngroups = gstart[ncomp];
@@ -1072,7 +1063,6 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
     const int k = g / bps;
     return g >= sv.vend[k] || (k > 0 && (sv.flag[k] & kSegEmpty) && (sv.flag[k - 1] & kSegIns));
   };
-  // block of this lane in group grp: component, block coordinates, decode-order index
   // a / b for 0 <= a < 2^22, 1 <= b: float estimate, then one correction each way (exact)
   auto qdiv = [](int a, int b, float rb) {
     int q = (int)((float)a * rb);
@@ -1080,6 +1070,7 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
     q += (q + 1) * b <= a ? 1 : 0;
     return q;
   };
+  // block lb of group grp: component, block coordinates, decode-order index (g < 0: none)
   auto locate = [&](int grp, int& c, int& by, int& bx, int& g) {
     c = ncomp > 1 && grp >= gstart[1] ? (ncomp > 2 && grp >= gstart[2] ? 2 : 1) : 0;
     const int local = grp - gstart[c];
@@ -1093,64 +1084,53 @@ __global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __r
       g = (my * mcux + mx) * bpm + binv[c][(by - my * v) * 4 + (bx - mx * h)];
     }
   };
-  const int gstride = gridDim.x * 4;
-  // transform + store the block of this lane (g < 0: none) from its coefficient row `raw`
-  auto process = [&](const uint4& raw, int c, int by, int bx, int g) {
-    const bool valid = g >= 0;
-    if (valid) {
-      // row r of the block, dequantised (DEQUANTIZE: coef * quantval), stored as two 16-byte writes
-      const uint4 v = zero_block(g) ? make_uint4(0, 0, 0, 0) : raw;
-      const int4 q0 = *reinterpret_cast<const int4*>(&qt[c][r * 8]), q1 = *reinterpret_cast<const int4*>(&qt[c][r * 8 + 4]);
-      auto lo16 = [](uint32_t x) { return (int)(int16_t)(x & 0xFFFF); };
-      auto hi16 = [](uint32_t x) { return (int)(int16_t)(x >> 16); };
-      *reinterpret_cast<int4*>(W + r * 8) = make_int4(lo16(v.x) * q0.x, hi16(v.x) * q0.y, lo16(v.y) * q0.z, hi16(v.y) * q0.w);
-      *reinterpret_cast<int4*>(W + r * 8 + 4) =
-          make_int4(lo16(v.z) * q1.x, hi16(v.z) * q1.y, lo16(v.w) * q1.z, hi16(v.w) * q1.w);
+  // One block per lane, held in registers: dequantise, columns (pass 1), rows (pass 2), each row's 8
+  // bytes stored straight to the plane -- no LDS transposes.  The 8 lanes of a group write 64
+  // contiguous bytes of a plane row per store.
+  for (int grp = blockIdx.x * (kIdctThreads / 8) + (t >> 3); grp < ngroups; grp += gridDim.x * (kIdctThreads / 8)) {
+    int c, by, bx, g;
+    locate(grp, c, by, bx, g);
+    if (g < 0) continue;
+    // the block (zigzag order, k_entwrite / k_prog), or zeros where the entropy decoder left it zero
+    const uint4* src = reinterpret_cast<const uint4*>(coef + (int64_t)g * 64);
+    const bool zb = zero_block(g);
+    uint4 raw[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) raw[i] = zb ? make_uint4(0, 0, 0, 0) : src[i];
+    // DEQUANTIZE: coef * quantval, zigzag position k into row-major natural_order(k)
+    int x[64];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int4 q0 = *reinterpret_cast<const int4*>(&qt[c][i * 8]), q1 = *reinterpret_cast<const int4*>(&qt[c][i * 8 + 4]);
+      const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+      const int q[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        x[natural_order(i * 8 + k)] = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFF) * q[k];
     }
-    wave_lds_sync();
-    // pass 1: column r
-    int col[8];
-    if (valid) {
-      int x[8];
-      for (int k = 0; k < 8; k++) x[k] = W[k * 8 + r];
-      if ((x[1] | x[2] | x[3] | x[4] | x[5] | x[6] | x[7]) == 0) {
-        for (int k = 0; k < 8; k++) col[k] = x[0] * 4;  // << PASS1_BITS
-      } else {
-        int o[8];
-        islow_1d(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7], o);
-        for (int k = 0; k < 8; k++) col[k] = (o[k] + (1 << 10)) >> 11;  // DESCALE(, CONST_BITS-PASS1_BITS)
-      }
-    }
-    wave_lds_sync();
-    if (valid)
-      for (int k = 0; k < 8; k++) W[k * 8 + r] = col[k];
-    wave_lds_sync();
-    // pass 2: row r -> 8 bytes of plane row by * 8 + r
-    if (valid) {
-      const int4 w0 = *reinterpret_cast<const int4*>(W + r * 8), w1 = *reinterpret_cast<const int4*>(W + r * 8 + 4);
+    // pass 1: columns (a column without AC terms: DC << PASS1_BITS, jidctint.c's shortcut)
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
       int o[8];
-      islow_1d(w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, o);
-      uint32_t lo = 0, hi = 0;
-      for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
-      for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
-      *reinterpret_cast<uint2*>(planes + cplane[c] + (int64_t)(by * 8 + r) * cpitch[c] + bx * 8) = make_uint2(lo, hi);
+      islow_1d(x[k], x[8 + k], x[16 + k], x[24 + k], x[32 + k], x[40 + k], x[48 + k], x[56 + k], o);
+      const bool dc_only = (x[8 + k] | x[16 + k] | x[24 + k] | x[32 + k] | x[40 + k] | x[48 + k] | x[56 + k]) == 0;
+      const int dc4 = x[k] * 4;
+#pragma unroll
+      for (int j = 0; j < 8; j++) x[j * 8 + k] = dc_only ? dc4 : (o[j] + (1 << 10)) >> 11;  // DESCALE(, CONST_BITS-PASS1_BITS)
     }
-    wave_lds_sync();
-  };
-  // two groups in flight per wave (ping-pong registers: a loop-carried copy would force the wait)
-  int c0, by0, bx0, g0, c1, by1, bx1, g1;
-  int grp = blockIdx.x * 4 + wv;
-  locate(grp, c0, by0, bx0, g0);
-  uint4 rawA, rawB;
-  rawA = *reinterpret_cast<const uint4*>(coef + (int64_t)(g0 >= 0 ? g0 : 0) * 64 + r * 8);
-  for (; grp < ngroups; grp += 2 * gstride) {
-    locate(grp + gstride, c1, by1, bx1, g1);
-    rawB = *reinterpret_cast<const uint4*>(coef + (int64_t)(g1 >= 0 ? g1 : 0) * 64 + r * 8);  // unconditional: keeps vmcnt countable
-    process(rawA, c0, by0, bx0, g0);
-    if (grp + gstride >= ngroups) break;
-    locate(grp + 2 * gstride, c0, by0, bx0, g0);
-    rawA = *reinterpret_cast<const uint4*>(coef + (int64_t)(g0 >= 0 ? g0 : 0) * 64 + r * 8);
-    process(rawB, c1, by1, bx1, g1);
+    // pass 2: rows -> 8 bytes of plane row by * 8 + r
+    uint8_t* dst = planes + cplane[c] + (int64_t)(by * 8) * cpitch[c] + bx * 8;
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      int o[8];
+      islow_1d(x[r * 8], x[r * 8 + 1], x[r * 8 + 2], x[r * 8 + 3], x[r * 8 + 4], x[r * 8 + 5], x[r * 8 + 6], x[r * 8 + 7], o);
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
+#pragma unroll
+      for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
+      *reinterpret_cast<uint2*>(dst + (int64_t)r * cpitch[c]) = make_uint2(lo, hi);
+    }
   }
 }
 

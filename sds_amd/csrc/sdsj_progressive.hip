@@ -301,8 +301,8 @@ __device__ int pread_dqt(ProgTables* P, const uint8_t* s, int sl) {
   return SDSJ_OK;
 }
 
-// Blocks are kept in zigzag order while the scans run (k_prog_unzig puts them in natural order for
-// k_idct): zigzag index k is natural_order(k), and natural_order's guard entries past 63 are all 63.
+// Blocks are kept in zigzag order (the order k_idct reads): zigzag index k is natural_order(k), and
+// natural_order's guard entries past 63 are all 63.
 __device__ __forceinline__ int zig(int k) { return k < 63 ? k : 63; }
 
 // One block of a DC scan or an AC first scan (jdphuff.c decode_mcu_DC_first / _DC_refine / _AC_first).
@@ -704,41 +704,18 @@ __global__ void __launch_bounds__(256) k_prog_zero(const ImgDesc* __restrict__ d
     p[i] = make_uint4(0, 0, 0, 0);
 }
 
-// Zigzag -> natural order for the blocks of the progressive images: one block per thread, its 128
-// bytes in registers, the permutation resolved at compile time (no LDS, so the launch stays cheap
-// for batches without progressive images).  Images to be smoothed also get their DC plane (int16 per
-// block, decode order) in the plane area, which k_idct writes only later.
-__global__ void __launch_bounds__(256) k_prog_unzig(const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
-                                                    const int32_t* __restrict__ routes, int cap) {
+// The DC plane of the progressive images to be smoothed (int16 per block, decode order) in their
+// plane area, which k_idct writes only later: k_prog_smooth reads the neighbours' DC values from it
+// while it rewrites blocks in place.  (Blocks stay in zigzag order: k_idct reads that order.)
+__global__ void __launch_bounds__(256) k_prog_dcs(const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                                  const int32_t* __restrict__ routes, int cap) {
   if ((int)blockIdx.x >= routes[kRtProg]) return;
   const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[blockIdx.x]];
-  if (d->status != SDSJ_OK) return;
-  int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
-  const bool smooth = d->smooth != 0;
+  if (d->status != SDSJ_OK || !d->smooth) return;
+  const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
   int16_t* dcs = reinterpret_cast<int16_t*>(scratch + d->off_planes);
   const int64_t nb = d->total_blocks;
-  for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < nb; i += (int64_t)gridDim.y * 256) {
-    uint4* p = reinterpret_cast<uint4*>(coef + i * 64);
-    uint32_t z[32], o[32];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint4 v = p[q];
-      z[4 * q] = v.x;
-      z[4 * q + 1] = v.y;
-      z[4 * q + 2] = v.z;
-      z[4 * q + 3] = v.w;
-    }
-#pragma unroll
-    for (int q = 0; q < 32; q++) o[q] = 0;
-#pragma unroll
-    for (int k = 0; k < 64; k++) {
-      const int j = natural_order(k);
-      o[j >> 1] |= ((z[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu) << ((j & 1) * 16);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; q++) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-    if (smooth) dcs[i] = (int16_t)(o[0] & 0xFFFF);  // the DC plane k_prog_smooth reads
-  }
+  for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < nb; i += (int64_t)gridDim.y * 256) dcs[i] = coef[i * 64];
 }
 
 // pred = num / (Q << 8) rounded half away from zero, clamped below 2^Al when Al > 0
@@ -753,7 +730,7 @@ __device__ __forceinline__ int smooth_pred(int64_t num, int64_t q, int al) {
 // last scan (ImgDesc::smooth, k_prog): jdcoefct.c decompress_smooth_data, one thread per block of the
 // image in decode order.  Zero coefficients AC01 AC10 AC20 AC11 AC02 (and AC03 AC12 AC21 AC30 and
 // the DC itself when the component has no AC data at all) get estimates from the DC values of the
-// block's 5x5 neighbourhood, read from the DC plane k_prog_unzig copied into the (not yet written)
+// block's 5x5 neighbourhood, read from the DC plane k_prog_dcs copied into the (not yet written)
 // plane area -- libjpeg likewise reads the neighbours unmodified while it smooths a copy of the block.
 // Rows: jdcoefct.c's per-iMCU-row choice (the last iMCU row's real rows only); columns clamped to the
 // component's width in blocks (tests/test_gpu_parity.py: bit-exact against the Pillow-pinned CPU restatement).
@@ -819,9 +796,10 @@ __global__ void __launch_bounds__(256) k_prog_smooth(const ImgDesc* __restrict__
     int16_t* blk = coef + g * 64;
     // DCnn of jdcoefct.c: DC01 .. DC25 row by row (DC13 = this block)
 #define SD(n) DC[((n) - 1) / 5][((n) - 1) % 5]
+    // coefficient zz (zigzag = coef_bits index; the blocks are in zigzag order), quantiser at natural index nat
     auto est = [&](int nat, int zz, int64_t num) {
       const int al = cb[zz];
-      if (al != 0 && blk[nat] == 0) blk[nat] = (int16_t)smooth_pred(Q00 * num, qt[nat], al);
+      if (al != 0 && blk[zz] == 0) blk[zz] = (int16_t)smooth_pred(Q00 * num, qt[nat], al);
     };
     est(1, 1,
         change_dc ? (-SD(1) - SD(2) + SD(4) + SD(5) - 3 * SD(6) + 13 * SD(7) - 13 * SD(9) + 3 * SD(10) - 3 * SD(11) +
@@ -887,7 +865,7 @@ hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* 
   hipLaunchKernelGGL(k_prog_zero, dim3(n, 16), dim3(256), 0, s, descs, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog, dim3((n + kProgLanes - 1) / kProgLanes), dim3(kProgLanes), 0, s, descs, tables, blob,
                      offsets, lengths, scratch, routes, cap);
-  hipLaunchKernelGGL(k_prog_unzig, dim3(n, 8), dim3(256), 0, s, descs, scratch, routes, cap);
+  hipLaunchKernelGGL(k_prog_dcs, dim3(n, 8), dim3(256), 0, s, descs, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog_smooth, dim3(n, 8), dim3(256), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }

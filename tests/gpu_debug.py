@@ -38,7 +38,8 @@ class ImgDescC(ctypes.Structure):
                 ("warm_bits", i32), ("scan_end_code", i32), ("scan_end_raw", i64),
                 ("rgb_pitch", i32), ("ent_groups", i32),
                 ("progressive", i32), ("lat", i32), ("sos_pos", i64), ("off_ptab", i64),
-                ("off_tiles", i64), ("ntiles", i32), ("rs_lay", i32), ("plan_base", i64)]
+                ("off_tiles", i64), ("ntiles", i32), ("rs_lay", i32), ("plan_base", i64),
+                ("smooth", i32), ("sm_good", i32), ("sm_bits", ctypes.c_int8 * 60), ("sm_pad", ctypes.c_int8 * 4)]
 
 
 def _memcpy_d2h(ptr: int, nbytes: int) -> np.ndarray:
@@ -82,8 +83,13 @@ def stage_report(engine, jpg: bytes, resolution=(256, 256)) -> list[str]:
     lines.append(f"desc: {d.width}x{d.height} ncomp={d.ncomp} bpm={d.bpm} mcu={d.mcux}x{d.mcuy} nseg={d.nseg} "
                  f"ulen={d.ulen} nsub={d.nsub} sub_bits={d.sub_bits} geo={d.geo} crop=({d.cx0},{d.cy0},{d.cw},{d.ch}) "
                  f"need_h={d.need_h} need_v={d.need_v} yf={d.yf} yl={d.yl} status={d.status}")
-    # coefficients: device layout is decode order [g][64] natural order
-    coef = fetch(d.off_coef, d.total_blocks * 128).view(np.int16).reshape(-1, 64)
+    # coefficients: device layout is decode order [g][64] in zigzag order; natural order for the comparison
+    zz = fetch(d.off_coef, d.total_blocks * 128).view(np.int16).reshape(-1, 64)
+    nat = [0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5, 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7, 14,
+           21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60,
+           61, 54, 47, 55, 62, 63]
+    coef = np.zeros_like(zz)
+    coef[:, nat] = zz
     for c in range(d.ncomp):
         ref = O.coefficients(jpg, c)  # [bh][bw][64]
         cd = d.comp[c]
