@@ -29,7 +29,10 @@ constexpr int kDecodeThreads = SDSJ_DECODE_THREADS;  // threads (subsequences) p
 static_assert((kDecodeThreads & (kDecodeThreads - 1)) == 0 && kDecodeThreads >= 64 && kDecodeThreads <= 256,
               "a power of two number of waves");
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
-constexpr int kWarmBits = 3000;       // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
+#ifndef SDSJ_WARM_BITS
+#define SDSJ_WARM_BITS 3000
+#endif
+constexpr int kWarmBits = SDSJ_WARM_BITS;  // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
 constexpr int kWarmBitsSmall = 4000;  // ... for lanes of fewer than kWarmSmallLane images (the sync pass is
 constexpr int kWarmSmallLane = 512;   //     hidden by less concurrent work there, so it pays to shorten it)
 constexpr int kWarmDiv = 3;           // ... or sub_bits / kWarmDiv when that is larger
