@@ -11,6 +11,8 @@ on the training process's GPU:
     decode = GpuDecodeBatch("jpg", (256, 256), device="cuda")
     for batch in loader:              # or MultiStreamDataLoader's Batch (sds/dataloader.py:49-58)
         batch = decode(batch)         # batch["image"]: [B', 3, 256, 256] on the GPU
+    for batch in decode.stream(loader):   # the same, batch k + 1 staged and copied while k decodes
+        ...
 
 torch's default collate leaves ``bytes`` fields as a list, so ``batch[image_field]`` arrives as the
 B encoded images.  Values equal the per-sample pipeline's (presets.py:716-744) stacked the way
@@ -22,7 +24,7 @@ OSError makes ``_iter_chunks_`` skip it, dataset.py:366-371) is dropped from eve
 """
 from __future__ import annotations
 
-from typing import Any, Optional, Sequence
+from typing import Any, Iterable, Iterator, Optional, Sequence
 
 import torch
 
@@ -87,19 +89,73 @@ class GpuDecodeBatch:
         self.as_video = bool(return_image_as_single_frame_video)
         self.video_output_field = video_output_field
 
-    def __call__(self, batch: dict) -> dict:
+    def _inputs(self, batch: dict):
+        """The batch's encoded images and their hflip coins (one torch.rand(1) per sample, batch order)."""
         assert self.image_field in batch, f"Field '{self.image_field}' not found in batch with keys {list(batch.keys())}."
         encoded = batch[self.image_field]
         if isinstance(encoded, (bytes, bytearray, memoryview)):
             encoded = [encoded]
         encoded = [bytes(e) for e in encoded]
-        n = len(encoded)
-        flip = [bool(torch.rand(1) < self.hflip_prob) for _ in range(n)] if self.hflip_prob > 0.0 else None
+        flip = [bool(torch.rand(1) < self.hflip_prob) for _ in encoded] if self.hflip_prob > 0.0 else None
+        return encoded, flip
+
+    def _opts(self) -> dict:
         kw = self.resize_kwargs
-        eng = get_engine(self.device)
-        opts = dict(crop_before_resize=kw.get("crop_before_resize", True),
+        return dict(crop_before_resize=kw.get("crop_before_resize", True),
                     filter=F.filter_name(kw.get("interpolation_mode", "bilinear")), normalize=self.normalize)
-        images, status = eng.decode_resize(encoded, self.resolution, flip=flip, **opts)
+
+    def __call__(self, batch: dict) -> dict:
+        encoded, flip = self._inputs(batch)
+        eng = get_engine(self.device)
+        images, status = eng.decode_resize(encoded, self.resolution, flip=flip, **self._opts())
+        return self._finish(eng, batch, encoded, flip, images, status)
+
+    def stream(self, batches: Iterable[dict]) -> Iterator[dict]:
+        """Yields ``self(batch)`` for each collated batch, with one batch in flight: batch k + 1's host
+        staging, H2D copy and decode are queued (engine.submit, double-buffered pinned slots) before
+        batch k is collected (engine.wait), so the copy and the host work of one batch overlap the
+        other's decode.  Values and RNG draws equal the synchronous calls'; a batch larger than the
+        engine's max_batch is decoded synchronously in its turn.
+
+            for batch in GpuDecodeBatch("jpg", (256, 256), device="cuda").stream(loader): ...
+        """
+        eng = get_engine(self.device)
+        cap = getattr(eng, "max_batch", None)
+        pending = None  # (slot, batch, encoded, flip) of the batch in flight
+        k = 0
+        try:
+            for batch in batches:
+                encoded, flip = self._inputs(batch)
+                if cap is not None and len(encoded) > cap:
+                    if pending is not None:
+                        prev, pending = pending, None
+                        yield self._collect(eng, prev)
+                    images, status = eng.decode_resize(encoded, self.resolution, flip=flip, **self._opts())
+                    yield self._finish(eng, batch, encoded, flip, images, status)
+                    continue
+                slot = k % _lib.SLOTS
+                k += 1
+                eng.submit(slot, encoded, self.resolution, flip=flip, **self._opts())
+                prev, pending = pending, (slot, batch, encoded, flip)
+                if prev is not None:
+                    yield self._collect(eng, prev)
+            if pending is not None:
+                prev, pending = pending, None
+                yield self._collect(eng, prev)
+        finally:
+            if pending is not None:  # (the consumer stopped early, or a batch raised): drain the slot
+                eng.wait(pending[0])
+
+    def _collect(self, eng, inflight) -> dict:
+        slot, batch, encoded, flip = inflight
+        images, status = eng.wait(slot)
+        return self._finish(eng, batch, encoded, flip, images, status)
+
+    def _finish(self, eng, batch: dict, encoded: list, flip, images: torch.Tensor, status) -> dict:
+        """Host decode of the samples the kernels do not take, then the drop / raise rule and the
+        output fields."""
+        n = len(encoded)
+        opts = self._opts()
         errors: dict[int, BaseException] = {}
         for i in range(n):
             st = int(status[i])

@@ -19,6 +19,19 @@ from tests import goldens as G
 
 
 class _StandInEngine:
+    max_batch = 4
+
+    def __init__(self):
+        self.slots = {}
+
+    def submit(self, slot, jpgs, resolution, **kw):
+        assert slot not in self.slots and len(jpgs) <= self.max_batch
+        self.slots[slot] = self.decode_resize(jpgs, resolution, **kw)
+        return self.slots[slot][0]
+
+    def wait(self, slot):
+        return self.slots.pop(slot)
+
     def decode_resize(self, jpgs, resolution, crop_before_resize=True, filter="bilinear", normalize=False,
                       flip=None, layout="chw", out=None):
         outs, status = [], []
@@ -62,7 +75,9 @@ def _deferred_batch(samples):
 @pytest.fixture()
 def standin(monkeypatch):
     import sds_amd.batched as B
-    monkeypatch.setattr(B, "get_engine", lambda device=None: _StandInEngine())
+    eng = _StandInEngine()
+    monkeypatch.setattr(B, "get_engine", lambda device=None: eng)
+    return eng
 
 
 def test_batch_equals_per_sample_pipeline_stacked(standin):
@@ -102,6 +117,32 @@ def test_hflip_coins_in_batch_order_and_video_branch(standin):
         assert torch.equal(out["video"][k, 0], torch.flip(base, dims=[2]) if flips[k] else base)
 
 
+def _equal_batches(a: dict, b: dict) -> bool:
+    return list(a) == list(b) and all(torch.equal(a[k], b[k]) if isinstance(a[k], torch.Tensor) else a[k] == b[k]
+                                      for k in a)
+
+
+def test_stream_equals_synchronous_calls(standin):
+    """GpuDecodeBatch.stream (one batch in flight through engine.submit / wait) yields what the
+    synchronous calls give -- values, dropped samples, hflip coins in batch order -- including a batch
+    larger than the engine's max_batch (decoded synchronously in its turn), and leaves no slot in flight."""
+    from sds_amd.batched import GpuDecodeBatch
+    samples = _samples(True)
+    batches = [_deferred_batch(samples[:3]), _deferred_batch(samples), _deferred_batch(samples[3:]),
+               _deferred_batch(samples[1:4])]
+    dec = GpuDecodeBatch("jpg", (40, 40), hflip_prob=0.5)
+    torch.manual_seed(11)
+    ref = [dec(dict(b)) for b in batches]
+    torch.manual_seed(11)
+    got = list(dec.stream(dict(b) for b in batches))
+    assert len(got) == len(ref) and all(_equal_batches(a, b) for a, b in zip(got, ref))
+    assert [b["index"].tolist() for b in got] == [[0, 1], [0, 1, 3, 4], [3, 4], [1, 3]]
+    assert standin.slots == {}
+    with pytest.raises(OSError):  # on_error="raise": the exception reaches the consumer, the other slot drains
+        list(GpuDecodeBatch("jpg", (40, 40), on_error="raise").stream(dict(b) for b in batches))
+    assert standin.slots == {}
+
+
 def test_per_sample_target_sizes_are_rejected():
     from sds_amd.batched import GpuDecodeBatch
     with pytest.raises(ValueError):
@@ -120,3 +161,20 @@ def test_gpu_batch_matches_oracle():
     for k, i in enumerate([0, 1, 3, 4]):
         ref = O.pipeline(open(samples[i]["jpg"], "rb").read(), (256, 256))
         np.testing.assert_array_equal(out["image"][k].cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_gpu_stream_matches_oracle():
+    """f1 pipelined: GpuDecodeBatch.stream over several collated batches on the MI355X, bit-exact against
+    the oracle, the damaged sample dropped from its batch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from sds_amd.batched import GpuDecodeBatch
+    samples = _samples(True)
+    batches = [_deferred_batch(samples[:3]), _deferred_batch(samples), _deferred_batch(samples[2:])]
+    got = list(GpuDecodeBatch("jpg", (128, 96), device="cuda:0").stream(batches))
+    assert [b["index"].tolist() for b in got] == [[0, 1], [0, 1, 3, 4], [3, 4]]
+    for b in got:
+        for k, i in enumerate(b["index"].tolist()):
+            ref = O.pipeline(open(samples[i]["jpg"], "rb").read(), (128, 96))
+            np.testing.assert_array_equal(b["image"][k].cpu().numpy(), ref)
