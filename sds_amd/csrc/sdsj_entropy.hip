@@ -1147,6 +1147,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     uint32_t end_bit = 0, lim = 0;
     int s_int = 0;
     bool writing = false, last_of_seg = false, run = false;
+    uint32_t stop_pos = 0, stop_blk = 0;
     if (active) {
       const SubState& S = sub[j];
       const int s = S.seg;
@@ -1172,6 +1173,10 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       // the interval's last subsequence decodes every remaining block; when its data runs out
       // (bits past lim, read as zeros) it finishes that MCU and stops: jdhuff.c insufficient_data
       run = g < gend && (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
+      // one stop rule for both kinds: at a block boundary (z = 0) whose MCU position blk is in stop_blk
+      // (the interval's last subsequence: MCU boundaries only) once pos >= stop_pos
+      stop_pos = last_of_seg ? lim + 1 : end_bit;
+      stop_blk = last_of_seg ? 1u : 0xFFFFFFFFu;
     }
     while (__builtin_amdgcn_ballot_w64(run)) {
       if (run) bits_fill(b);
@@ -1207,9 +1212,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           sac = ctx_ac(K, blk);
           g += done ? 1 : 0;
           writing = writing | done;
-          const bool more_last = !((z == 0) & (blk == 0) & (b.pos > lim));
-          const bool more_mid = (b.pos < end_bit) | (z != 0);
-          run = (g < gend) & (last_of_seg ? more_last : more_mid);
+          run = (g < gend) & !((z == 0) & ((stop_blk >> blk) & 1u) & (b.pos >= stop_pos));
         }
         // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
         const uint64_t m = __builtin_amdgcn_ballot_w64(ready);

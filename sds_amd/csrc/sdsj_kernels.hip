@@ -128,7 +128,8 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
   d->rs_fast = 0;
   d->rs_lay = kRs420;
   if (d->fused && d->need_h && d->need_v && d->ksh >= 3 && d->ksh <= 11 && (d->ksh & 1) &&
-      d->ring_rows <= kRingMaxRows && d->ksv <= kVTapsF && d->comp[0].rh == 1 && d->comp[0].rv == 1) {
+      d->ring_rows <= rs_ring_rows(d->ksh) && d->ksv <= rs_vtaps(d->ksh) && d->tile_w * d->ring_rows <= rs_ring_dw(d->ksh) &&
+      d->comp[0].rh == 1 && d->comp[0].rv == 1) {
     const CompDesc &c1 = d->comp[1], &c2 = d->comp[2];
     const bool same = d->ncomp == 3 && c2.rh == c1.rh && c2.rv == c1.rv && c2.dw == c1.dw && c2.dh == c1.dh;
     int lay = -1;

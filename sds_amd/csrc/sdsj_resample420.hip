@@ -48,13 +48,13 @@ struct FGeo {
   static constexpr int kRows = kFRows + 2 * kCRows;  // staged rows per step at most
 };
 
-template <int LAY>
+template <int LAY, int KT>
 struct LdsF {
   uint32_t st[FGeo<LAY>::kStageDW];                          // step's plane rows: 4 luma, then Cb, Cr
   uint8_t rgb[FGeo<LAY>::kRgbRows > 0 ? FGeo<LAY>::kRgbRows : 1][3][kFRgbW];  // converted rows, planar
-  uint32_t ring[kRingDW];                                    // per column: H results of the last R rows
+  uint32_t ring[rs_ring_dw(KT)];                             // per column: H results of the last R rows
   int32_t vb[kMaxStrip][2];                                  // strip rows: vertical window (first, count)
-  int32_t vw[kMaxStrip][kVTapsF];                            // strip rows: vertical weights
+  int32_t vw[kMaxStrip][rs_vtaps(KT)];                       // strip rows: vertical weights
   int32_t rinfo[kFRows][8];                                  // step row q: byte offsets of its staged rows
 };
 
@@ -82,11 +82,14 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
                           void* __restrict__ out, const float* __restrict__ lut);
 
 // Route (LAY, KT): a small grid strides over the route's list (an empty route costs one short launch).
-#ifdef SDSJ_RS_WAVES  // occupancy target (waves per SIMD); the 9- and 11-tap kernels at most 5 (their windows spill at 6)
-#define SDSJ_RS_OCC __attribute__((amdgpu_waves_per_eu(KT <= 7 ? SDSJ_RS_WAVES : (SDSJ_RS_WAVES > 5 ? 5 : SDSJ_RS_WAVES))))
-#else
-#define SDSJ_RS_OCC
+// Occupancy: the KT <= 7 kernels' LDS (30.6 KB: the smaller ring and weight table) fits 5 workgroups
+// per CU, and 5 waves per SIMD fit their registers without spills (95 VGPRs): k_rs420<5> 9.95 -> 9.23 ms
+// per 16,384 images (profiles/r03b_rs420_occupancy_ab.txt).  The 9- and 11-tap kernels and 4:4:4 (whose
+// full-width chroma rows take 34 KB) keep 4.
+#ifndef SDSJ_RS_WAVES
+#define SDSJ_RS_WAVES 5
 #endif
+#define SDSJ_RS_OCC __attribute__((amdgpu_waves_per_eu(KT <= 7 && LAY != kRs444 ? SDSJ_RS_WAVES : 4)))
 template <int KT, int LAY>
 __global__ void __launch_bounds__(kFThreads) SDSJ_RS_OCC k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                       int strip_h, const uint8_t* __restrict__ scratch,
@@ -111,7 +114,8 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
   const int oy0 = blockIdx.y * strip_h;
   if (oy0 >= oh) return;
   const int oy1 = oy0 + strip_h < oh ? oy0 + strip_h : oh;
-  __shared__ LdsF<LAY> L;
+  __shared__ LdsF<LAY, KT> L;
+  constexpr int kVT = rs_vtaps(KT);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t plane = (int64_t)oh * ow;
   OutMap om;
@@ -125,7 +129,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
   const int32_t* bv = reinterpret_cast<const int32_t*>(scratch + d->off_kv);
   const int32_t* kv = bv + 2 * oh;
   const int ksv = d->ksv, cx0 = d->cx0, cy0 = d->cy0, tw = d->tile_w;
-  const int rmask = d->ring_rows - 1, rstride = kRingDW / d->ring_rows;
+  const int rmask = d->ring_rows - 1, rstride = rs_ring_dw(KT) / d->ring_rows;
   const int dwc = LAY == kRsGray ? 0 : d->comp[1].dw, dhc = LAY == kRsGray ? 0 : d->comp[1].dh;
   const uint8_t* pY = scratch + d->off_planes + d->comp[0].plane_off;
   const uint8_t* pCb = LAY == kRsGray ? pY : scratch + d->off_planes + d->comp[1].plane_off;
@@ -134,8 +138,8 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
   const int ntiles = (ow + tw - 1) / tw;
   const int r_lo = bv[2 * oy0], r_hi = bv[2 * (oy1 - 1)] + bv[2 * (oy1 - 1) + 1];
   // the strip's vertical windows and weights
-  for (int i = t; i < (oy1 - oy0) * kVTapsF; i += kFThreads) {
-    const int b = i / kVTapsF, k = i % kVTapsF, oy = oy0 + b;
+  for (int i = t; i < (oy1 - oy0) * kVT; i += kFThreads) {
+    const int b = i / kVT, k = i % kVT, oy = oy0 + b;
     if (k == 0) {
       L.vb[b][0] = bv[2 * oy];
       L.vb[b][1] = bv[2 * oy + 1];
