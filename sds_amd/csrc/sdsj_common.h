@@ -230,10 +230,12 @@ struct SubState {
 };
 
 // Table state of the progressive decoder (k_prog), one per progressive image in scratch: the
-// Huffman specs of the 4 DC and 4 AC slots as DHT segments define them (the scan's derived tables
-// live in LDS), the current DQT tables and which components have latched theirs (jdinput.c
-// latch_quant_tables).
+// Huffman specs of the 4 DC and 4 AC slots as DHT segments define them (the scan's lookahead tables
+// live in LDS, its canonical bounds here), the current DQT tables and which components have
+// latched theirs (jdinput.c latch_quant_tables).
 struct ProgTables {
+  int32_t maxcode[8][17];  // the scan's derived tables (jdhuff.c jpeg_make_d_derived_tbl): [slot][l],
+  int32_t valoff[8][17];   // l = 1..16, for codes longer than the LDS lookahead's 9 bits
   uint8_t vals[8][256];
   uint8_t bits[8][17];
   uint8_t defined[8];

@@ -327,9 +327,13 @@ static_assert(kSpecGroup < kQ && kWriteGroup < kQ, "a fresh refill must pass the
 #endif
 constexpr int kRefillSpec = SDSJ_REFILL_SLACK ? 32 * (kSpecGroup + 1) : 27 * (kSpecGroup - 1) + 32;
 #ifndef SDSJ_REC_STORE
-#define SDSJ_REC_STORE kRec
+#define SDSJ_REC_STORE 16
 #endif
-constexpr int kRecStore = SDSJ_REC_STORE;  // records the speculative pass keeps (<= kRec; experiments)
+// Records the speculative pass keeps per subsequence (<= kRec): the first 16 block boundaries.  With
+// the warm-up, a subsequence's entry is almost always right and k_entsync reads none of them; when
+// it is not, paths merge within a few blocks.  16 instead of 64: k_entspec 7.45 -> 7.22 ms per 16,384
+// (fewer scattered 8-byte stores; profiles/r03d_ab.txt).
+constexpr int kRecStore = SDSJ_REC_STORE;
 static_assert(kRecStore <= kRec, "records fit their scratch");
 constexpr int kRefillWrite = SDSJ_REFILL_SLACK ? 32 * (kWriteGroup + 1) : 27 * (kWriteGroup - 1) + 32;
 

@@ -998,7 +998,11 @@ constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides
 // Work unit = a group: 8 horizontally adjacent blocks of one component, one per thread, so each of
 // a block's 8 row stores joins the group's other 7 in 64 contiguous bytes of a plane row.  The
 // block stays in registers through both passes (64 values), so there is no LDS transpose.
-__global__ void __launch_bounds__(kIdctThreads) k_idct(int n, const ImgDesc* __restrict__ descs,
+#ifndef SDSJ_IDCT_WAVES
+#define SDSJ_IDCT_WAVES 4  // waves per SIMD the register budget targets (124 VGPRs at 4)
+#endif
+__global__ void __launch_bounds__(kIdctThreads) __attribute__((amdgpu_waves_per_eu(SDSJ_IDCT_WAVES)))
+k_idct(int n, const ImgDesc* __restrict__ descs,
                                                        const ImgTables* __restrict__ tables,
                                                        uint8_t* __restrict__ scratch) {
   const int img = blockIdx.y;

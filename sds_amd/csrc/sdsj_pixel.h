@@ -46,6 +46,25 @@ struct OutMap {
   bool f32;
 };
 
+// put3 for output row `row` (uniform: the row's first pixel index) and column x: the row's channel
+// bases are uniform, so each store is a scalar base plus the lane's 32-bit offset.
+__device__ __forceinline__ void put3_row(void* out, const OutMap& m, const float* lut, int64_t row, int x, int v0, int v1,
+                                         int v2) {
+  const int64_t e = m.base + row * m.ps;
+  const uint32_t o = (uint32_t)(x * m.ps);
+  if (m.f32) {
+    float* b = reinterpret_cast<float*>(out) + e;
+    b[o] = lut[v0];
+    (b + m.cs)[o] = lut[v1];
+    (b + 2 * m.cs)[o] = lut[v2];
+  } else {
+    uint8_t* b = reinterpret_cast<uint8_t*>(out) + e;
+    b[o] = (uint8_t)v0;
+    (b + m.cs)[o] = (uint8_t)v1;
+    (b + 2 * m.cs)[o] = (uint8_t)v2;
+  }
+}
+
 __device__ __forceinline__ void put3(void* out, const OutMap& m, const float* lut, int64_t pix, int v0, int v1, int v2) {
   const int64_t e = m.base + pix * m.ps;
   if (m.f32) {

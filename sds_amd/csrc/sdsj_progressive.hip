@@ -118,11 +118,11 @@ __device__ __forceinline__ int pgetbits(PBits& b, int n) {
   return v;
 }
 
-// The derived tables of the scan being decoded, in LDS (one slot per lane = per image).
+// The lookahead tables of the scan being decoded, in LDS (one slot per lane = per image); the
+// canonical bounds and symbols that codes of more than 9 bits need stay in ProgTables (global
+// memory: such codes are rare, and 4.3 KB of LDS per image instead of 7.4 KB lets more images run
+// per CU).
 struct PLds {
-  int32_t maxcode[8][17];  // [slot][l], l = 1..16 (index 0 unused)
-  int32_t valoff[8][17];
-  uint8_t vals[8][256];
   uint16_t look[4][1 << 9];  // per scan position: (length << 8) | symbol of the codes of <= 9 bits, 0 = longer
   alignas(16) int16_t blk[64];  // the block an AC refinement scan updates (read-modify-write in LDS)
   int32_t qh[4], qv[4], qbo[4], qdsl[4], ldc[4];  // interleaved DC scans: per scan position h, v, block
@@ -137,7 +137,7 @@ struct PLds {
 // a bit-serial decode.
 // The buffer holds >= 32 bits when the symbol starts, so its extra bits (<= 15, or 1 + a correction
 // bit) need no second check.
-__device__ __forceinline__ int phuff(PBits& b, const PLds& L, int slot, int q) {
+__device__ __forceinline__ int phuff(PBits& b, const PLds& L, const ProgTables* __restrict__ T, int slot, int q) {
   if (b.nbits < 32) pfill(b);
   const uint32_t e = L.look[q][(uint32_t)(b.buf >> 55)];
   if (e) {
@@ -150,12 +150,12 @@ __device__ __forceinline__ int phuff(PBits& b, const PLds& L, int slot, int q) {
   const uint32_t peek = (uint32_t)(b.buf >> 47);
   int l = 17;
 #pragma unroll
-  for (int k = 16; k >= 10; k--) l = (int32_t)(peek >> (17 - k)) <= L.maxcode[slot][k] ? k : l;
+  for (int k = 16; k >= 10; k--) l = (int32_t)(peek >> (17 - k)) <= T->maxcode[slot][k] ? k : l;
   b.buf <<= l;
   b.nbits -= l;
   if (b.nbits < b.pad_bits) b.insufficient = 1;
   if (l > 16) return 0;
-  return L.vals[slot][((int32_t)(peek >> (17 - l)) + L.valoff[slot][l]) & 0xFF];
+  return T->vals[slot][((int32_t)(peek >> (17 - l)) + T->valoff[slot][l]) & 0xFF];
 }
 
 __device__ int pextend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)((~0u << s) + 1) : x; }
@@ -231,13 +231,13 @@ __device__ int rd16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 // jdhuff.c jpeg_make_d_derived_tbl for slot (0..3 DC, 4..7 AC) and scan position q: canonical
 // bounds plus the 9-bit lookahead table (a code of length l <= 9 fills its 2^(9-l) entries); false
 // when the code assignment overflows (JERR_BAD_HUFF_TABLE), or a DC table holds a symbol > 15
-__device__ bool pderive(const ProgTables* P, PLds& L, int slot, int q) {
+__device__ bool pderive(ProgTables* P, PLds& L, int slot, int q) {
   if (!P->defined[slot]) return false;
   int code = 0, p = 0;
   for (int l = 1; l <= 16; l++) {
     const int cnt = P->bits[slot][l];
-    L.maxcode[slot][l] = cnt ? code + cnt - 1 : -1;
-    L.valoff[slot][l] = cnt ? p - code : 0;
+    P->maxcode[slot][l] = cnt ? code + cnt - 1 : -1;
+    P->valoff[slot][l] = cnt ? p - code : 0;
     p += cnt;
     code += cnt;
     if (cnt && code >= (1 << l)) return false;  // (the all-ones code is reserved)
@@ -247,7 +247,6 @@ __device__ bool pderive(const ProgTables* P, PLds& L, int slot, int q) {
   if (slot < 4)
     for (int i = 0; i < p; i++)
       if (P->vals[slot][i] > 15) return false;
-  for (int i = 0; i < 256; i++) L.vals[slot][i] = P->vals[slot][i];
   uint4* lk = reinterpret_cast<uint4*>(L.look[q]);
   for (int i = 0; i < 64; i++) lk[i] = make_uint4(0, 0, 0, 0);
   code = 0;
@@ -306,11 +305,11 @@ __device__ int pread_dqt(ProgTables* P, const uint8_t* s, int sl) {
 __device__ __forceinline__ int zig(int k) { return k < 63 ? k : 63; }
 
 // One block of a DC scan or an AC first scan (jdphuff.c decode_mcu_DC_first / _DC_refine / _AC_first).
-__device__ __forceinline__ void pblock(PBits& b, const PLds& P, int dslot, int aslot, int lq, int16_t* blk, int ss, int se,
+__device__ __forceinline__ void pblock(PBits& b, const PLds& P, const ProgTables* __restrict__ T, int dslot, int aslot, int lq, int16_t* blk, int ss, int se,
                        int ah, int al, int* last_dc, int* eobrun) {
   if (ss == 0) {
     if (ah == 0) {  // decode_mcu_DC_first
-      int s = phuff(b, P, dslot, lq);
+      int s = phuff(b, P, T, dslot, lq);
       if (s) s = pextend(pgetbits_nc(b, s), s);
       s += *last_dc;
       *last_dc = s;
@@ -326,7 +325,7 @@ __device__ __forceinline__ void pblock(PBits& b, const PLds& P, int dslot, int a
     return;
   }
   for (int k = ss; k <= se; k++) {
-    const int sym = phuff(b, P, aslot, lq);
+    const int sym = phuff(b, P, T, aslot, lq);
     const int r = sym >> 4, s = sym & 15;
     if (s) {
       k += r;
@@ -396,7 +395,7 @@ __device__ __forceinline__ void pcorrect(PBits& b, int16_t* blk, uint64_t span, 
 // non-zero coefficients replaces the coefficient-by-coefficient walk: the stop of a run of r zeros
 // is the (r + 1)-th zero bit at or after k, and the non-zero coefficients passed on the way each
 // take one correction bit.
-__device__ __forceinline__ void prefine(PBits& b, PLds& P, int aslot, int16_t* gblk, int ss, int se, int al, int* eobrun) {
+__device__ __forceinline__ void prefine(PBits& b, PLds& P, const ProgTables* __restrict__ T, int aslot, int16_t* gblk, int ss, int se, int al, int* eobrun) {
   uint4 v[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) v[i] = reinterpret_cast<const uint4*>(gblk)[i];
@@ -417,7 +416,7 @@ __device__ __forceinline__ void prefine(PBits& b, PLds& P, int aslot, int16_t* g
   int k = ss;
   if (*eobrun == 0) {
     for (; k <= se; k++) {
-      const int sym = phuff(b, P, aslot, 0);
+      const int sym = phuff(b, P, T, aslot, 0);
       const int r = sym >> 4;
       int s = sym & 15;
       if (s) {
@@ -463,6 +462,9 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
   }
   for (int c = 0; c < kMaxComp; c++) P->latched[c] = 0;
   d->t_spec = d->t_sync = d->t_scan = d->t_write = 0;
+#ifdef SDSJ_PROG_STATS
+  d->sym_spec = d->sym_sync = d->sym_write = d->it_write = 0;
+#endif
   // block smoothing state (jdphuff.c start_pass_phuff_decoder coef_bits / prev_coef_bits)
   d->smooth = 0;
   for (int c = 0; c < kMaxComp; c++)
@@ -568,6 +570,10 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
       return ncomp == 1 ? (int64_t)by * bw0 + bx : ((int64_t)my * mcux + mx) * bpm + bo0 + sy * ch0 + sx;
     };
     const bool refine = ss != 0 && ah != 0;
+#ifdef SDSJ_PROG_STATS  // (tools/prog_stats.py: shader cycles and bytes per scan kind)
+    const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
+    const int64_t st_p0 = b.pos;
+#endif
     int64_t gn = ns == 1 ? gpos() : 0;
     L.ins_m = -1;
     for (int m = 0; m < nmcu; m++) {
@@ -601,7 +607,7 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
       // (L.ins_m: the MCU in which this scan ran out of data -- the one before the first MCU skipped
       // or restarted with insufficient data)
       if (refine) {
-        if (!b.insufficient) prefine(b, L, asl0, coef + g1 * 64, ss, se, al, &eobrun);
+        if (!b.insufficient) prefine(b, L, P, asl0, coef + g1 * 64, ss, se, al, &eobrun);
         else if (L.ins_m < 0) L.ins_m = m - 1;
         continue;
       }
@@ -610,7 +616,7 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
         continue;
       }
       if (ns == 1) {
-        pblock(b, L, dsl0, asl0, 0, coef + g1 * 64, ss, se, ah, al, &ldc0, &eobrun);
+        pblock(b, L, P, dsl0, asl0, 0, coef + g1 * 64, ss, se, ah, al, &ldc0, &eobrun);
         continue;
       }
       for (int q = 0; q < ns; q++) {
@@ -626,10 +632,20 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
             } else {
               g = (int64_t)m * bpm + L.qbo[q] + v * ch + h;
             }
-            pblock(b, L, L.qdsl[q], 4, q, coef + g * 64, ss, se, ah, al, &L.ldc[q], &eobrun);
+            pblock(b, L, P, L.qdsl[q], 4, q, coef + g * 64, ss, se, ah, al, &L.ldc[q], &eobrun);
           }
       }
     }
+#ifdef SDSJ_PROG_STATS
+    {
+      const int kind = ss == 0 ? (ah == 0 ? 0 : 2) : (ah == 0 ? 1 : 3);
+      const int64_t dt = (int64_t)(__builtin_amdgcn_s_memtime() - st_t0), db = b.pos - st_p0;
+      int64_t* tt = kind == 0 ? &d->t_spec : kind == 1 ? &d->t_sync : kind == 2 ? &d->t_scan : &d->t_write;
+      int64_t* bb = kind == 0 ? &d->sym_spec : kind == 1 ? &d->sym_sync : kind == 2 ? &d->sym_write : &d->it_write;
+      *tt += dt;
+      *bb += db;
+    }
+#endif
     if (b.insufficient && L.ins_m < 0) L.ins_m = nmcu - 1;
     if (L.ins_m >= 0) {  // later iMCU rows keep the previous scan's smoothing parameters
       const int r = ns == 1 ? L.ins_m / cwb : L.ins_m / mcux;
@@ -841,8 +857,11 @@ __global__ void __launch_bounds__(256) k_prog_smooth(const ImgDesc* __restrict__
 
 // One wave per progressive image: its lane walks all the scans (see the header); kProgLanes images per workgroup,
 // each with its derived tables in LDS.
+#ifndef SDSJ_PROG_WAVES
+#define SDSJ_PROG_WAVES 5
+#endif
 constexpr int kProgLanes = 1;  // (lanes of one wave walking different images would diverge on every branch)
-__global__ void __launch_bounds__(kProgLanes) __attribute__((amdgpu_waves_per_eu(5))) k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables,
+__global__ void __launch_bounds__(kProgLanes) __attribute__((amdgpu_waves_per_eu(SDSJ_PROG_WAVES))) k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables,
                                              const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
                                              const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
                                              const int32_t* __restrict__ routes, int cap) {

@@ -76,6 +76,44 @@ __device__ __forceinline__ int htaps(const uint32_t* w, int hsh, const int32_t* 
   return rs_clip8(acc);
 }
 
+// Pillow vertical pass of one output pixel from the ring (KT <= 7: 8 rows of 256 columns), window
+// starting at ring row P: every tap's row is a compile-time offset from the lane's column, so the
+// reads need no address arithmetic (rsf_image picks P = vmin & 7 with a uniform switch).
+template <int KT, int P, bool GRAY>
+__device__ __forceinline__ void vtaps8(const uint32_t* ring, int lane_col, const int32_t* wk, int32_t& v0, int32_t& v1,
+                                       int32_t& v2) {
+  // (the empty asm keeps the column index a value of this block, so each tap's row becomes the
+  // read's immediate offset instead of one of 8 addresses held in registers through the loop)
+  asm volatile("" : "+v"(lane_col));
+#pragma unroll
+  for (int k = 0; k < KT; k++) {
+    const uint32_t h = ring[lane_col + ((P + k) & 7) * 256];
+    const int32_t w = wk[k];
+    if (GRAY) {
+      v0 += tap((int32_t)h, w);
+    } else {
+      v0 += tap((int32_t)(h & 0xFF), w);
+      v1 += tap((int32_t)((h >> 8) & 0xFF), w);
+      v2 += tap((int32_t)(h >> 16), w);
+    }
+  }
+}
+
+template <int KT, bool GRAY>
+__device__ __forceinline__ void vtaps8_at(int p, const uint32_t* ring, int lane_col, const int32_t* wk, int32_t& v0,
+                                          int32_t& v1, int32_t& v2) {
+  switch (__builtin_amdgcn_readfirstlane(p)) {  // (uniform: scalar compares, no exec masking)
+    case 0: vtaps8<KT, 0, GRAY>(ring, lane_col, wk, v0, v1, v2); break;
+    case 1: vtaps8<KT, 1, GRAY>(ring, lane_col, wk, v0, v1, v2); break;
+    case 2: vtaps8<KT, 2, GRAY>(ring, lane_col, wk, v0, v1, v2); break;
+    case 3: vtaps8<KT, 3, GRAY>(ring, lane_col, wk, v0, v1, v2); break;
+    case 4: vtaps8<KT, 4, GRAY>(ring, lane_col, wk, v0, v1, v2); break;
+    case 5: vtaps8<KT, 5, GRAY>(ring, lane_col, wk, v0, v1, v2); break;
+    case 6: vtaps8<KT, 6, GRAY>(ring, lane_col, wk, v0, v1, v2); break;
+    default: vtaps8<KT, 7, GRAY>(ring, lane_col, wk, v0, v1, v2); break;
+  }
+}
+
 template <int KT, int LAY>
 __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
                           const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
@@ -129,7 +167,11 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
   const int32_t* bv = reinterpret_cast<const int32_t*>(scratch + d->off_kv);
   const int32_t* kv = bv + 2 * oh;
   const int ksv = d->ksv, cx0 = d->cx0, cy0 = d->cy0, tw = d->tile_w;
-  const int rmask = d->ring_rows - 1, rstride = rs_ring_dw(KT) / d->ring_rows;
+  // KT <= 7: the ring is always 8 rows of 256 columns (plan_image: ksv <= 8, tile_w <= 256), so its
+  // row offsets are compile-time constants
+  constexpr bool kRing8 = KT <= 7;
+  static_assert(!kRing8 || (rs_ring_rows(KT) == 8 && rs_ring_dw(KT) == 8 * 256), "ring geometry");
+  const int rmask = kRing8 ? 7 : d->ring_rows - 1, rstride = kRing8 ? 256 : rs_ring_dw(KT) / d->ring_rows;
   const int dwc = LAY == kRsGray ? 0 : d->comp[1].dw, dhc = LAY == kRsGray ? 0 : d->comp[1].dh;
   const uint8_t* pY = scratch + d->off_planes + d->comp[0].plane_off;
   const uint8_t* pCb = LAY == kRsGray ? pY : scratch + d->off_planes + d->comp[1].plane_off;
@@ -269,6 +311,13 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
     issue(cur);
     commit(cur);
     __syncthreads();
+    // the next output row's window (uniform, carried in scalars): first row, and one past its last
+    auto window = [&](int row, int& vmin, int& vend) {
+      vmin = __builtin_amdgcn_readfirstlane(L.vb[row - oy0][0]);
+      vend = vmin + __builtin_amdgcn_readfirstlane(L.vb[row - oy0][1]);
+    };
+    int nvmin, nvend;
+    window(oy0, nvmin, nvend);
     for (int ra = r_lo; ra < r_hi; ra += kFRows) {
       const int nr = cur.nr;
       const bool more = ra + kFRows < r_hi;
@@ -387,42 +436,44 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
             ring[(r & rmask) * rstride] = pack3(s0, s1, s2);
           }
           // V. output rows whose window ends at row r
-          while (nb < oy1) {
-            const int vmin = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][0]);
-            const int vcnt = __builtin_amdgcn_readfirstlane(L.vb[nb - oy0][1]);
-            if (vmin + vcnt > r + 1) break;
+          while (nvend <= r + 1) {
+            const int vmin = nvmin, vcnt = nvend - nvmin;
             const int32_t* wk = L.vw[nb - oy0];
-            // ksv <= KT (square crops): KT taps unrolled, so their ring and weight reads issue together
-            // (the weights past the window are zero, k_coeffs; ring rows past it are finite values)
-            const bool unr = SDSJ_VUNROLL && ksv <= KT;
-            if (LAY == kRsGray) {
-              int32_t v0 = 1 << 21;
-              if (unr) {
-#pragma unroll
-                for (int k = 0; k < KT; k++) v0 += tap((int32_t)ring[((vmin + k) & rmask) * rstride], wk[k]);
-              } else {
-                for (int k = 0; k < vcnt; k++) v0 += tap((int32_t)ring[((vmin + k) & rmask) * rstride], wk[k]);
-              }
-              const int c = rs_clip8(v0);
-              put3(out, om, lut, (int64_t)nb * ow + ox, c, c, c);
+            int32_t v0 = 1 << 21, v1 = 1 << 21, v2 = 1 << 21;
+            if constexpr (kRing8) {
+              // all taps unrolled (KT of them, or 8 when ksv > KT): their ring and weight reads issue
+              // together (the weights past the window are zero, k_coeffs / the strip table; ring rows
+              // past it are finite values)
+              if (ksv <= KT) vtaps8_at<KT, LAY == kRsGray>(vmin & 7, L.ring, t, wk, v0, v1, v2);
+              else vtaps8_at<8, LAY == kRsGray>(vmin & 7, L.ring, t, wk, v0, v1, v2);
             } else {
-              int32_t v0 = 1 << 21, v1 = 1 << 21, v2 = 1 << 21;
               auto vtap = [&](int k) {
                 const uint32_t h = ring[((vmin + k) & rmask) * rstride];
                 const int32_t w = wk[k];
-                v0 += tap((int32_t)(h & 0xFF), w);
-                v1 += tap((int32_t)((h >> 8) & 0xFF), w);
-                v2 += tap((int32_t)(h >> 16), w);
+                if (LAY == kRsGray) {
+                  v0 += tap((int32_t)h, w);
+                } else {
+                  v0 += tap((int32_t)(h & 0xFF), w);
+                  v1 += tap((int32_t)((h >> 8) & 0xFF), w);
+                  v2 += tap((int32_t)(h >> 16), w);
+                }
               };
-              if (unr) {
+              if (SDSJ_VUNROLL && ksv <= KT) {
 #pragma unroll
                 for (int k = 0; k < KT; k++) vtap(k);
               } else {
                 for (int k = 0; k < vcnt; k++) vtap(k);
               }
-              put3(out, om, lut, (int64_t)nb * ow + ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
+            }
+            if (LAY == kRsGray) {
+              const int c = rs_clip8(v0);
+              put3_row(out, om, lut, (int64_t)nb * ow, ox, c, c, c);
+            } else {
+              put3_row(out, om, lut, (int64_t)nb * ow, ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
             }
             nb++;
+            if (nb < oy1) window(nb, nvmin, nvend);
+            else nvend = 1 << 30;
           }
         }
       }

@@ -76,6 +76,7 @@ def test_decode_stream_of_files_with_a_missing_file(engine):
     after = engine.counters()
     assert len(got) == 3
     assert after["other"] == before["other"] + 1  # the unreadable file, counted as such
+    assert after["corrupt"] == before["corrupt"] and after["unsupported"] == before["unsupported"]
     for b, (out, st) in enumerate(got):
         if b == 1:
             assert st[3] == _lib.EINVAL

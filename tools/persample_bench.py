@@ -27,7 +27,23 @@ MODES = {
     "dataloader_fork_workers8_device_out": (8, False, None, None),
     "dataloader_spawn_workers4_pinned_cpu_out": (4, True, "spawn", "cpu"),
     "main_process_per_sample": (0, False, None, None),
+    # the workers decode on the GPU but hand back only a tiny host tensor: the rate without the
+    # device-tensor IPC (CUDA IPC handles opened by the parent per batch)
+    "dataloader_fork_workers8_decode_only": (8, False, None, "discard"),
 }
+
+
+class _Discard(torch.utils.data.Dataset):
+    def __init__(self, ds):
+        self.ds = ds
+
+    def __len__(self):
+        return len(self.ds)
+
+    def __getitem__(self, i):
+        s = self.ds[i]
+        assert s["image"].is_cuda  # (the transform's status check has synchronised the decode)
+        return {"image": torch.zeros(3, 1, 1)}
 
 
 def run_mode(mode, n_files, seconds):
@@ -43,8 +59,11 @@ def run_mode(mode, n_files, seconds):
         with open(p, "wb") as f:
             f.write(jpgs[i % len(jpgs)])
         paths.append(p)
-    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device=odev)
+    discard = odev == "discard"
+    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device=None if discard else odev)
     ds = FolderDataset(paths, ts)
+    if discard:
+        ds = _Discard(ds)
     if nw:
         # persistent workers: forked once, before the parent receives its first device tensor
         src = DataLoader(ds, batch_size=4, num_workers=nw, pin_memory=pin, multiprocessing_context=ctx,
