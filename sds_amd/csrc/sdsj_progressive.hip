@@ -29,13 +29,21 @@ struct PBits {
   uint4 w;
 };
 
+// The aligned 16 bytes around p (address a).  Addressed from p itself, not from the integer a: a
+// pointer rebuilt from an integer is a flat pointer, whose loads the compiler must treat as
+// per-lane values -- the whole bit reader then runs on vector registers under exec masks.  From
+// the global pointer the window, and everything decoded from it, is wave-uniform.
+__device__ __forceinline__ uint4 pwindow(const uint8_t* p, uintptr_t a) {
+  return *reinterpret_cast<const uint4*>(p - (a & 15));
+}
+
 // Byte i of the stream (0 <= i < n) through the window: the aligned 16 bytes around it come in as
 // one load (the blob allocation holds the whole granule).
 __device__ __forceinline__ int pbyte(PBits& b, int64_t i) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(b.d + i), base = a & ~(uintptr_t)15;
   if (base != b.wbase) {
     b.wbase = base;
-    b.w = *reinterpret_cast<const uint4*>(base);
+    b.w = pwindow(b.d + i, a);
   }
   // (the window is picked from computed values, not from field loads: a select between loads of
   // b.w's fields becomes a select between their addresses, and the bit reader state then stays in
@@ -54,7 +62,7 @@ __device__ __forceinline__ void pfill(PBits& b) {
       if (o <= 12) {
         if (base != b.wbase) {
           b.wbase = base;
-          b.w = *reinterpret_cast<const uint4*>(base);
+          b.w = pwindow(b.d + b.pos, a);
         }
         // bytes o .. o + 3 of the 16-byte window (a 128-bit shift; see pbyte)
         const uint64_t lo = ((uint64_t)b.w.y << 32) | b.w.x, hi = ((uint64_t)b.w.w << 32) | b.w.z;
@@ -124,7 +132,6 @@ __device__ __forceinline__ int pgetbits(PBits& b, int n) {
 // per CU).
 struct PLds {
   uint16_t look[4][1 << 9];  // per scan position: (length << 8) | symbol of the codes of <= 9 bits, 0 = longer
-  alignas(16) int16_t blk[64];  // the block an AC refinement scan updates (read-modify-write in LDS)
   int32_t qh[4], qv[4], qbo[4], qdsl[4], ldc[4];  // interleaved DC scans: per scan position h, v, block
                                                   // offset in the MCU, DC table slot, DC predictor
   int32_t ins_m;  // the MCU in which the scan ran out of data (-1: none); in LDS, off the MCU loop's registers
@@ -158,7 +165,7 @@ __device__ __forceinline__ int phuff(PBits& b, const PLds& L, const ProgTables* 
   return T->vals[slot][((int32_t)(peek >> (17 - l)) + T->valoff[slot][l]) & 0xFF];
 }
 
-__device__ int pextend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)((~0u << s) + 1) : x; }
+__device__ __forceinline__ int pextend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)((~0u << s) + 1) : x; }
 
 // jdmarker.c next_marker from the byte cursor: pos ends on the marker's last FF; -1 at the end
 __device__ __forceinline__ int pnext_marker(PBits& b) {
@@ -226,18 +233,26 @@ __device__ __forceinline__ int pprocess_restart(PBits& b, int* next_num) {
   return 0;
 }
 
-__device__ int rd16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+__device__ __forceinline__ int rd16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
 // jdhuff.c jpeg_make_d_derived_tbl for slot (0..3 DC, 4..7 AC) and scan position q: canonical
-// bounds plus the 9-bit lookahead table (a code of length l <= 9 fills its 2^(9-l) entries); false
-// when the code assignment overflows (JERR_BAD_HUFF_TABLE), or a DC table holds a symbol > 15
-__device__ bool pderive(ProgTables* P, PLds& L, int slot, int q) {
+// bounds plus the 9-bit lookahead table (entry x: the code of length l <= 9 that is x's l-bit
+// prefix, found like jpeg_huff_decode's search; the lanes fill 8 entries each); false when the code
+// assignment overflows (JERR_BAD_HUFF_TABLE), or a DC table holds a symbol > 15
+__device__ __forceinline__ bool pderive(ProgTables* P, PLds& L, int slot, int q, int lane) {
   if (!P->defined[slot]) return false;
   int code = 0, p = 0;
+  int mc[10], vo[10];
+#pragma unroll
   for (int l = 1; l <= 16; l++) {
     const int cnt = P->bits[slot][l];
-    P->maxcode[slot][l] = cnt ? code + cnt - 1 : -1;
-    P->valoff[slot][l] = cnt ? p - code : 0;
+    const int m = cnt ? code + cnt - 1 : -1, o = cnt ? p - code : 0;
+    P->maxcode[slot][l] = m;
+    P->valoff[slot][l] = o;
+    if (l <= 9) {
+      mc[l] = m;
+      vo[l] = o;
+    }
     p += cnt;
     code += cnt;
     if (cnt && code >= (1 << l)) return false;  // (the all-ones code is reserved)
@@ -247,24 +262,25 @@ __device__ bool pderive(ProgTables* P, PLds& L, int slot, int q) {
   if (slot < 4)
     for (int i = 0; i < p; i++)
       if (P->vals[slot][i] > 15) return false;
-  uint4* lk = reinterpret_cast<uint4*>(L.look[q]);
-  for (int i = 0; i < 64; i++) lk[i] = make_uint4(0, 0, 0, 0);
-  code = 0;
-  p = 0;
-  for (int l = 1; l <= 9; l++) {
-    const int cnt = P->bits[slot][l], span = 1 << (9 - l);
-    for (int i = 0; i < cnt; i++, code++) {
-      const uint16_t e = (uint16_t)((l << 8) | P->vals[slot][p + i]);
-      for (int j = 0; j < span; j++) L.look[q][(code << (9 - l)) + j] = e;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int x = lane + 64 * k;
+    int ls = 0, vi = 0;  // (selects, no branches: one symbol load per entry)
+#pragma unroll
+    for (int l = 9; l >= 1; l--) {
+      const int c = x >> (9 - l);
+      const bool hit = c <= mc[l];
+      ls = hit ? l : ls;
+      vi = hit ? c + vo[l] : vi;
     }
-    p += cnt;
-    code <<= 1;
+    const int sym = P->vals[slot][vi & 0xFF];
+    L.look[q][x] = (uint16_t)(ls ? (ls << 8) | sym : 0);
   }
   return true;
 }
 
 // get_dht / get_dqt bodies
-__device__ int pread_dht(ProgTables* P, const uint8_t* s, int sl) {
+__device__ __forceinline__ int pread_dht(ProgTables* P, const uint8_t* s, int sl) {
   int k = 0;
   while (k < sl) {
     if (k + 17 > sl) return SDSJ_CORRUPT;
@@ -285,7 +301,7 @@ __device__ int pread_dht(ProgTables* P, const uint8_t* s, int sl) {
   return SDSJ_OK;
 }
 
-__device__ int pread_dqt(ProgTables* P, const uint8_t* s, int sl) {
+__device__ __forceinline__ int pread_dqt(ProgTables* P, const uint8_t* s, int sl) {
   int k = 0;
   while (k < sl) {
     const int pq = s[k] >> 4, tq = s[k] & 15;
@@ -303,6 +319,16 @@ __device__ int pread_dqt(ProgTables* P, const uint8_t* s, int sl) {
 // Blocks are kept in zigzag order (the order k_idct reads): zigzag index k is natural_order(k), and
 // natural_order's guard entries past 63 are all 63.
 __device__ __forceinline__ int zig(int k) { return k < 63 ? k : 63; }
+
+// n (1..32) bits as an unsigned word (the correction bits of up to 32 coefficients at once)
+__device__ __forceinline__ uint32_t pgetbits32(PBits& b, int n) {
+  if (b.nbits < n) pfill(b);  // (pfill leaves >= 57 bits)
+  const uint32_t v = (uint32_t)(b.buf >> (64 - n));
+  b.buf <<= n;
+  b.nbits -= n;
+  if (b.nbits < b.pad_bits) b.insufficient = 1;
+  return v;
+}
 
 // One block of a DC scan or an AC first scan (jdphuff.c decode_mcu_DC_first / _DC_refine / _AC_first).
 __device__ __forceinline__ void pblock(PBits& b, const PLds& P, const ProgTables* __restrict__ T, int dslot, int aslot, int lq, int16_t* blk, int ss, int se,
@@ -367,52 +393,39 @@ __device__ __forceinline__ int pnth_zero(uint64_t nz, uint64_t window, int r, in
   return pos;
 }
 
-// bit 0: the low halfword of x is non-zero; bit 1: the high one
-__device__ __forceinline__ uint32_t nz2(uint32_t x) {
-  const uint32_t y = ((x & 0x7FFF7FFFu) + 0x7FFF7FFFu) | x;
-  return ((y >> 15) & 1u) | ((y >> 30) & 2u);
+// One block of an AC refinement scan (jdphuff.c decode_mcu_AC_refine), lane-parallel: the wave walks
+// the block's symbols together (every lane decodes the same bits), and lane k holds the block's
+// zigzag coefficient k in a register.  A ballot gives the mask of non-zero coefficients; the stop of
+// a run of r zeros is the (r + 1)-th zero bit at or after k, and the non-zero coefficients passed on
+// the way each take one correction bit -- read in chunks of up to 32, the i-th lowest position of a
+// chunk taking its i-th bit from the top, each lane applying its own.
+// A ballot as a wave-uniform value (readfirstlane on each half: the compiler then knows the mask,
+// and everything the decode derives from it, is the same in every lane)
+__device__ __forceinline__ uint64_t uballot(bool x) {
+  const uint64_t m = __builtin_amdgcn_ballot_w64(x);
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(m >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)m);
 }
 
-// Correction bits for the non-zero coefficients flagged in span, in zigzag order (one bit each, read
-// in chunks of up to 16): a 1 adds p1 away from zero unless that bit is already set.
-__device__ __forceinline__ void pcorrect(PBits& b, int16_t* blk, uint64_t span, int p1) {
-  while (span) {
-    const int cnt = min(__popcll(span), 16);
-    const int bits = pgetbits(b, cnt);
-    for (int i = cnt - 1; i >= 0; i--) {
-      const int pos = __ffsll((unsigned long long)span) - 1;
-      span &= span - 1;
-      if ((bits >> i) & 1) {
-        const int c = blk[pos];
-        if ((c & p1) == 0) blk[pos] = (int16_t)(c >= 0 ? c + p1 : c - p1);
-      }
-    }
-  }
-}
-
-// One block of an AC refinement scan (jdphuff.c decode_mcu_AC_refine).  The block (zigzag order) is
-// staged in LDS and a 64-bit mask of its
-// non-zero coefficients replaces the coefficient-by-coefficient walk: the stop of a run of r zeros
-// is the (r + 1)-th zero bit at or after k, and the non-zero coefficients passed on the way each
-// take one correction bit.
-__device__ __forceinline__ void prefine(PBits& b, PLds& P, const ProgTables* __restrict__ T, int aslot, int16_t* gblk, int ss, int se, int al, int* eobrun) {
-  uint4 v[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) v[i] = reinterpret_cast<const uint4*>(gblk)[i];
-  uint4* lb = reinterpret_cast<uint4*>(P.blk);
-  uint32_t mlo = 0, mhi = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    lb[i] = v[i];
-    lb[i + 4] = v[i + 4];
-    mlo |= (nz2(v[i].x) | nz2(v[i].y) << 2 | nz2(v[i].z) << 4 | nz2(v[i].w) << 6) << (8 * i);
-    mhi |= (nz2(v[i + 4].x) | nz2(v[i + 4].y) << 2 | nz2(v[i + 4].z) << 4 | nz2(v[i + 4].w) << 6) << (8 * i);
-  }
-  uint64_t nz = ((uint64_t)mhi << 32) | mlo;
-  int16_t* blk = P.blk;
+__device__ __forceinline__ int prefine(PBits& b, const PLds& P, const ProgTables* __restrict__ T, int aslot, int v,
+                                       int lane, int ss, int se, int al, int* eobrun) {
   const int p1 = 1 << al, m1 = -(1 << al);
+  uint64_t nz = uballot(v != 0);
   const uint64_t band = se >= 63 ? ~0ull : ((1ull << (se + 1)) - 1);  // positions <= se
+  const uint64_t lower = (1ull << lane) - 1;                           // positions below this lane's
   auto below = [](int z) { return z >= 64 ? ~0ull : ((1ull << z) - 1); };
+  // correction bits for the non-zero coefficients flagged in span (jdphuff.c: a 1 adds p1 away
+  // from zero unless that bit is already set)
+  auto correct = [&](uint64_t span) {
+    while (span) {
+      const int cnt = min(__popcll(span), 32);
+      const uint32_t bits = pgetbits32(b, cnt);
+      const int rank = __popcll(span & lower);
+      const bool mine = ((span >> lane) & 1) != 0 && rank < cnt;
+      if (mine && ((bits >> (cnt - 1 - rank)) & 1) && (v & p1) == 0) v = v >= 0 ? v + p1 : v - p1;
+      span &= ~uballot(mine);
+    }
+  };
   int k = ss;
   if (*eobrun == 0) {
     for (; k <= se; k++) {
@@ -428,26 +441,24 @@ __device__ __forceinline__ void prefine(PBits& b, PLds& P, const ProgTables* __r
       }
       // skip r zero coefficients (correcting the non-zero ones passed), stop on the next zero
       const int z = pnth_zero(nz, band & (~0ull << k), r, se);
-      pcorrect(b, blk, nz & below(z) & (~0ull << k), p1);
+      correct(nz & below(z) & (~0ull << k));
       k = z;
       if (s) {
-        blk[zig(k)] = (int16_t)s;
+        if (lane == zig(k)) v = s;
         nz |= 1ull << zig(k);
       }
     }
   }
   if (*eobrun > 0) {
-    if (k <= se) pcorrect(b, blk, nz & band & (~0ull << k), p1);
+    if (k <= se) correct(nz & band & (~0ull << k));
     (*eobrun)--;
   }
-  uint4* dst = reinterpret_cast<uint4*>(gblk);
-#pragma unroll
-  for (int i = 0; i < 8; i++) dst[i] = lb[i];
+  return v;
 }
 
 // Every scan of image d, then the markers up to EOI.  Returns an SDSJ status.
-__device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, int64_t n, int16_t* coef,
-                                  ProgTables* P, PLds& L) {
+__device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, int64_t n, int16_t* coef,
+                                  ProgTables* P, PLds& L, int lane) {
   // table state as k_parse left it (the DHT / DQT segments before the first SOS)
   for (int q = 0; q < 4; q++) {
     P->qt_defined[q] = t->qt_defined[q];
@@ -513,9 +524,9 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
         P->latched[c] = 1;
       }
       if (ss == 0 && ah == 0) {
-        if (td[q] > 3 || !pderive(P, L, td[q], q)) return SDSJ_CORRUPT;
+        if (td[q] > 3 || !pderive(P, L, td[q], q, lane)) return SDSJ_CORRUPT;
       } else if (ss != 0) {
-        if (ta[q] > 3 || !pderive(P, L, 4 + ta[q], q)) return SDSJ_CORRUPT;
+        if (ta[q] > 3 || !pderive(P, L, 4 + ta[q], q, lane)) return SDSJ_CORRUPT;
       }
       // coef_bits of the band (the smoothing reads coefficients 0..9), the previous values kept
       for (int k = ss < 1 ? ss : 1; k < 10; k++) d->sm_bits[1][c][k] = nscans > 0 ? d->sm_bits[0][c][k] : 0;
@@ -576,6 +587,8 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
 #endif
     int64_t gn = ns == 1 ? gpos() : 0;
     L.ins_m = -1;
+    // refinement: lane k's coefficient k of the current block, and of the next one in flight
+    int vcur = refine && nmcu > 0 ? coef[gn * 64 + lane] : 0;
     for (int m = 0; m < nmcu; m++) {
       const int64_t g1 = gn;
       if (ns == 1) {
@@ -607,8 +620,10 @@ __device__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, 
       // (L.ins_m: the MCU in which this scan ran out of data -- the one before the first MCU skipped
       // or restarted with insufficient data)
       if (refine) {
-        if (!b.insufficient) prefine(b, L, P, asl0, coef + g1 * 64, ss, se, al, &eobrun);
+        const int vnext = m + 1 < nmcu ? coef[gn * 64 + lane] : 0;
+        if (!b.insufficient) coef[g1 * 64 + lane] = (int16_t)prefine(b, L, P, asl0, vcur, lane, ss, se, al, &eobrun);
         else if (L.ins_m < 0) L.ins_m = m - 1;
+        vcur = vnext;
         continue;
       }
       if (b.insufficient) {  // the MCU's coefficients stay as they are
@@ -855,26 +870,25 @@ __global__ void __launch_bounds__(256) k_prog_smooth(const ImgDesc* __restrict__
   }
 }
 
-// One wave per progressive image: its lane walks all the scans (see the header); kProgLanes images per workgroup,
-// each with its derived tables in LDS.
+// One wave per progressive image: the wave walks all the scans together (the header); the lanes split
+// the AC refinement scans' blocks coefficient by coefficient (prefine).  The derived tables in LDS.
 #ifndef SDSJ_PROG_WAVES
 #define SDSJ_PROG_WAVES 5
 #endif
-constexpr int kProgLanes = 1;  // (lanes of one wave walking different images would diverge on every branch)
-__global__ void __launch_bounds__(kProgLanes) __attribute__((amdgpu_waves_per_eu(SDSJ_PROG_WAVES))) k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables,
-                                             const uint8_t* __restrict__ blob, const int64_t* __restrict__ offsets,
-                                             const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
-                                             const int32_t* __restrict__ routes, int cap) {
-  __shared__ PLds lds[kProgLanes];
-  const int li = blockIdx.x * kProgLanes + threadIdx.x;
-  if (li >= routes[kRtProg]) return;
-  const int img = route_list(routes, cap, kRtProg)[li];
+constexpr int kProgThreads = 64;
+__global__ void __launch_bounds__(kProgThreads) __attribute__((amdgpu_waves_per_eu(SDSJ_PROG_WAVES)))
+k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables, const uint8_t* __restrict__ blob,
+       const int64_t* __restrict__ offsets, const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
+       const int32_t* __restrict__ routes, int cap) {
+  __shared__ PLds lds;
+  if ((int)blockIdx.x >= routes[kRtProg]) return;
+  const int img = route_list(routes, cap, kRtProg)[blockIdx.x];
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
   const int st = decode_progressive(d, &tables[img], blob + offsets[img], lengths[img],
                                     reinterpret_cast<int16_t*>(scratch + d->off_coef),
-                                    reinterpret_cast<ProgTables*>(scratch + d->off_ptab), lds[threadIdx.x]);
-  if (st != SDSJ_OK) d->status = st;
+                                    reinterpret_cast<ProgTables*>(scratch + d->off_ptab), lds, threadIdx.x);
+  if (st != SDSJ_OK && threadIdx.x == 0) d->status = st;
 }
 
 hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* blob, const int64_t* offsets,
@@ -882,7 +896,7 @@ hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* 
                        uint64_t rm) {
   if (!route_on(rm, kRtProg)) return hipSuccess;
   hipLaunchKernelGGL(k_prog_zero, dim3(n, 16), dim3(256), 0, s, descs, scratch, routes, cap);
-  hipLaunchKernelGGL(k_prog, dim3((n + kProgLanes - 1) / kProgLanes), dim3(kProgLanes), 0, s, descs, tables, blob,
+  hipLaunchKernelGGL(k_prog, dim3(n), dim3(kProgThreads), 0, s, descs, tables, blob,
                      offsets, lengths, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog_dcs, dim3(n, 8), dim3(256), 0, s, descs, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog_smooth, dim3(n, 8), dim3(256), 0, s, descs, tables, scratch, routes, cap);

@@ -33,17 +33,14 @@ MODES = {
 }
 
 
-class _Discard(torch.utils.data.Dataset):
+class _Discard(torch.utils.data.IterableDataset):
     def __init__(self, ds):
         self.ds = ds
 
-    def __len__(self):
-        return len(self.ds)
-
-    def __getitem__(self, i):
-        s = self.ds[i]
-        assert s["image"].is_cuda  # (the transform's status check has synchronised the decode)
-        return {"image": torch.zeros(3, 1, 1)}
+    def __iter__(self):
+        for s in self.ds:
+            assert s["image"].is_cuda  # (the transform's status check has synchronised the decode)
+            yield {"image": torch.zeros(3, 1, 1)}
 
 
 def run_mode(mode, n_files, seconds):

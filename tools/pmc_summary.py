@@ -9,7 +9,8 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for path in glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
+prefix = sys.argv[4] if len(sys.argv) > 4 else "pmc"  # (run directories <root>/<prefix>_<pass>)
+for path in glob.glob(os.path.join(root, prefix + "_*", "**", "*counter_collection.csv"), recursive=True):
     per = collections.defaultdict(float)  # (kernel, dispatch, counter) -> summed value
     with open(path) as f:
         for row in csv.DictReader(f):

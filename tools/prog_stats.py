@@ -18,7 +18,7 @@ pool = [encode_jpeg(synth_rgb(np.random.default_rng(1234 + i), 640, 480), 90, pr
 jpgs = [pool[i % len(pool)] for i in range(n)]
 eng = JpegEngine(max_batch=n)
 out, st = eng.decode_resize(jpgs, (256, 256))
-assert (st.cpu().numpy() == 0).all()
+assert (np.asarray(st) == 0).all()
 descs, _ = snapshot(eng, n)
 kinds = {"dc_first": ("t_spec", "sym_spec"), "ac_first": ("t_sync", "sym_sync"), "dc_refine": ("t_scan", "sym_write"),
          "ac_refine": ("t_write", "it_write")}
