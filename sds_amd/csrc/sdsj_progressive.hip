@@ -22,7 +22,7 @@ namespace {
 // bytes skipped; a marker stops the data (zeros are fed from there); the input ending first is eof.
 struct PBits {
   const uint8_t* d;
-  int64_t n, pos;
+  int n, pos;  // (32-bit: the scans' data is far below 2 GB; fewer scalar registers)
   uint64_t buf;
   int nbits, hit_marker, marker, pad_bits, insufficient, eof;
   uintptr_t wbase;  // 16-byte window of the stream held in registers (one load per 16 bytes)
@@ -39,7 +39,7 @@ __device__ __forceinline__ uint4 pwindow(const uint8_t* p, uintptr_t a) {
 
 // Byte i of the stream (0 <= i < n) through the window: the aligned 16 bytes around it come in as
 // one load (the blob allocation holds the whole granule).
-__device__ __forceinline__ int pbyte(PBits& b, int64_t i) {
+__device__ __forceinline__ int pbyte(PBits& b, int i) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(b.d + i), base = a & ~(uintptr_t)15;
   if (base != b.wbase) {
     b.wbase = base;
@@ -172,7 +172,7 @@ __device__ __forceinline__ int pnext_marker(PBits& b) {
   for (;;) {
     while (b.pos < b.n && pbyte(b, b.pos) != 0xFF) b.pos++;
     if (b.pos >= b.n) return -1;
-    int64_t p = b.pos + 1;
+    int p = b.pos + 1;
     while (p < b.n && pbyte(b, p) == 0xFF) p++;
     if (p >= b.n) return -1;
     const int m = pbyte(b, p);
@@ -368,31 +368,6 @@ __device__ __forceinline__ void pblock(PBits& b, const PLds& P, const ProgTables
   }
 }
 
-// Position of the (r + 1)-th zero bit of nz within window (popcount binary search, no loop over r);
-// se + 1 when the window holds r or fewer zeros.
-__device__ __forceinline__ int pnth_zero(uint64_t nz, uint64_t window, int r, int se) {
-  const uint64_t zeros = ~nz & window;
-  if (__popcll(zeros) <= r) return se + 1;
-  uint32_t w = (uint32_t)zeros;
-  int pos = 0;
-  const int c32 = __popc(w);
-  if (r >= c32) {
-    r -= c32;
-    w = (uint32_t)(zeros >> 32);
-    pos = 32;
-  }
-#pragma unroll
-  for (int h = 16; h >= 1; h >>= 1) {
-    const int c = __popc(w & ((1u << h) - 1));
-    if (r >= c) {
-      r -= c;
-      w >>= h;
-      pos += h;
-    }
-  }
-  return pos;
-}
-
 // One block of an AC refinement scan (jdphuff.c decode_mcu_AC_refine), lane-parallel: the wave walks
 // the block's symbols together (every lane decodes the same bits), and lane k holds the block's
 // zigzag coefficient k in a register.  A ballot gives the mask of non-zero coefficients; the stop of
@@ -418,6 +393,8 @@ __device__ __forceinline__ int prefine(PBits& b, const PLds& P, const ProgTables
   // from zero unless that bit is already set)
   auto correct = [&](uint64_t span) {
     while (span) {
+      // (min() here resolves to the double overload; an integer select measured 12 % slower overall
+      // -- code generation, profiles/r03e_prog_lanes_ab.txt -- so it stays)
       const int cnt = min(__popcll(span), 32);
       const uint32_t bits = pgetbits32(b, cnt);
       const int rank = __popcll(span & lower);
@@ -439,8 +416,14 @@ __device__ __forceinline__ int prefine(PBits& b, const PLds& P, const ProgTables
         if (r) *eobrun += pgetbits_nc(b, r);
         break;
       }
-      // skip r zero coefficients (correcting the non-zero ones passed), stop on the next zero
-      const int z = pnth_zero(nz, band & (~0ull << k), r, se);
+      // skip r zero coefficients (correcting the non-zero ones passed), stop on the next zero: the
+      // zero lane of rank r among the zero lanes in [k, se] (v != 0 exactly where nz has a bit)
+      int z;
+      {
+        const bool zl = v == 0 && lane >= k && lane <= se;
+        const uint64_t zeros = uballot(zl);
+        z = __popcll(zeros) <= r ? se + 1 : __ffsll((unsigned long long)uballot(zl && __popcll(zeros & lower) == r)) - 1;
+      }
       correct(nz & below(z) & (~0ull << k));
       k = z;
       if (s) {
@@ -457,7 +440,7 @@ __device__ __forceinline__ int prefine(PBits& b, const PLds& P, const ProgTables
 }
 
 // Every scan of image d, then the markers up to EOI.  Returns an SDSJ status.
-__device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, int64_t n, int16_t* coef,
+__device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, const uint8_t* raw, int n, int16_t* coef,
                                   ProgTables* P, PLds& L, int lane) {
   // table state as k_parse left it (the DHT / DQT segments before the first SOS)
   for (int q = 0; q < 4; q++) {
@@ -485,7 +468,7 @@ __device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, cons
   // first block of components 1 and 2 within an MCU
   const int boff1 = d->ncomp > 1 ? d->comp[0].h * d->comp[0].v : 0;
   const int boff2 = d->ncomp > 2 ? boff1 + d->comp[1].h * d->comp[1].v : 0;
-  int64_t pos = d->sos_pos;
+  int pos = (int)d->sos_pos;
   for (;;) {
     if (pos + 2 > n) return SDSJ_CORRUPT;
     const int len = rd16(raw + pos), sl = len - 2;
@@ -577,20 +560,40 @@ __device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, cons
     int bx = 0, by = 0, mx = 0, my = 0, sx = 0, sy = 0;
     const int ch0 = sh[0], cv0 = sv[0], bw0 = sbw[0], bo0 = sbo[0];
     const int dsl0 = td[0] & 3, asl0 = 4 + (ta[0] & 3);
-    auto gpos = [&]() -> int64_t {
-      return ncomp == 1 ? (int64_t)by * bw0 + bx : ((int64_t)my * mcux + mx) * bpm + bo0 + sy * ch0 + sx;
+    auto gpos = [&]() -> int {
+      return ncomp == 1 ? by * bw0 + bx : (my * mcux + mx) * bpm + bo0 + sy * ch0 + sx;
     };
     const bool refine = ss != 0 && ah != 0;
 #ifdef SDSJ_PROG_STATS  // (tools/prog_stats.py: shader cycles and bytes per scan kind)
     const uint64_t st_t0 = __builtin_amdgcn_s_memtime();
     const int64_t st_p0 = b.pos;
 #endif
-    int64_t gn = ns == 1 ? gpos() : 0;
+    int gn = ns == 1 ? gpos() : 0;
     L.ins_m = -1;
     // refinement: lane k's coefficient k of the current block, and of the next one in flight
     int vcur = refine && nmcu > 0 ? coef[gn * 64 + lane] : 0;
-    for (int m = 0; m < nmcu; m++) {
-      const int64_t g1 = gn;
+    // DC refinement over all components in frame order without restart intervals: one bit per block
+    // in decode order (block g of MCU-order storage), so 32 blocks take one read and a lane each
+    bool dc_fast = ss == 0 && ah != 0 && ns == ncomp && ncomp > 1 && restart_interval == 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) dc_fast = dc_fast && (q >= ns || comps[q] == q);
+    if (dc_fast) {
+      const int nblk = nmcu * bpm;
+      for (int j0 = 0; j0 < nblk && !b.insufficient; j0 += 32) {
+        const int cnt = nblk - j0 < 32 ? nblk - j0 : 32;
+        if (b.nbits < cnt) pfill(b);
+        const int real = b.nbits - b.pad_bits;  // bits before the inserted zeros
+        const uint32_t bits = pgetbits32(b, cnt);
+        if (lane < cnt && ((bits >> (cnt - 1 - lane)) & 1)) {
+          int16_t* p = coef + (j0 + lane) * 64;
+          *p = (int16_t)(*p | (1 << al));
+        }
+        // the data ran out at block j0 + real: its MCU finished, the next ones are skipped
+        if (b.insufficient && L.ins_m < 0) L.ins_m = (j0 + real) / bpm;
+      }
+    }
+    for (int m = 0; m < (dc_fast ? 0 : nmcu); m++) {
+      const int g1 = gn;
       if (ns == 1) {
         bx++;
         if (++sx == ch0) {
@@ -631,6 +634,28 @@ __device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, cons
         continue;
       }
       if (ns == 1) {
+        if (ss != 0 && eobrun > 0) {
+          // AC first scan inside an EOB run: this block and the next eobrun - 1 ones stay empty
+          // (decode_mcu_AC_first only counts the run down), up to the scan's or the restart
+          // interval's end -- skipped at once, the block cursor recomputed for the block after
+          int skip = eobrun;
+          if (skip > nmcu - m) skip = nmcu - m;
+          if (restart_interval && skip > restarts_left + 1) skip = restarts_left + 1;
+          eobrun -= skip;
+          if (skip > 1) {
+            if (restart_interval) restarts_left -= skip - 1;
+            m += skip - 1;
+            const int nb = m + 1;
+            bx = nb % cwb;
+            by = nb / cwb;
+            mx = bx / ch0;
+            sx = bx - mx * ch0;
+            my = by / cv0;
+            sy = by - my * cv0;
+            gn = gpos();
+          }
+          continue;
+        }
         pblock(b, L, P, dsl0, asl0, 0, coef + g1 * 64, ss, se, ah, al, &ldc0, &eobrun);
         continue;
       }
@@ -640,12 +665,12 @@ __device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, cons
           for (int h = 0; h < ch; h++) {
             // block (h, v) of component c in MCU m: ((by / cv) * mcux + bx / ch) * bpm + ... with
             // bx = (m % mcux) * ch + h, by = (m / mcux) * cv + v reduces to m * bpm + ...
-            int64_t g;
+            int g;
             if (ncomp == 1) {  // (a single-component frame lists its component more than once)
               const int gx = (m % mcux) * ch + h, gy = (m / mcux) * cv + v;
-              g = (int64_t)gy * sbw[q] + gx;
+              g = gy * sbw[q] + gx;
             } else {
-              g = (int64_t)m * bpm + L.qbo[q] + v * ch + h;
+              g = m * bpm + L.qbo[q] + v * ch + h;
             }
             pblock(b, L, P, L.qdsl[q], 4, q, coef + g * 64, ss, se, ah, al, &L.ldc[q], &eobrun);
           }
@@ -672,7 +697,7 @@ __device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, cons
     for (;;) {
       if (b.pos + 1 >= n) return SDSJ_CORRUPT;
       const int m = pbyte(b, b.pos + 1);
-      const int64_t body = b.pos + 2;
+      const int body = b.pos + 2;
       if (m == 0xD9) {
         // k_idct reads each component's latched table from slot c
         for (int c = 0; c < d->ncomp; c++) d->comp[c].tq = c;

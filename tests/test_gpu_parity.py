@@ -308,6 +308,34 @@ def test_progressive_incomplete_scans_smoothing_vs_oracle(engine):
         np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res, flip=flips[k]), err_msg=f"case {k}")
 
 
+def test_progressive_truncated_inside_scans_vs_oracle(engine):
+    """Progressive images cut inside each scan's entropy-coded data (then EOI): the scan runs out of
+    data mid-way (jdhuff.c insufficient_data -- the rest reads as zeros, later MCUs are skipped), which
+    every scan kind meets here -- the lane-parallel AC refinement and the 32-blocks-per-read DC
+    refinement included -- and the smoothing takes the row where the data ended.  Against the oracle
+    (statuses and pixels, crop + resize)."""
+    from tests.golden.synth import progressive_jpegs
+    cases = []
+    for seed, mw, mh in ((11, 400, 300), (13, 64, 48)):
+        for j in progressive_jpegs(seed, 4, mw, mh):
+            sos = [i for i in range(2, len(j) - 1) if j[i] == 0xFF and j[i + 1] == 0xDA]
+            ends = sos[1:] + [len(j) - 2]
+            for a, e in zip(sos, ends):
+                for f in (0.2, 0.55, 0.9):
+                    cases.append(j[:a + 14 + int((e - a - 14) * f)] + b"\xff\xd9")
+    res = (40, 48)
+    got, st = engine.decode_resize(cases, res)
+    host = got.cpu().numpy()
+    for k, j in enumerate(cases):
+        try:
+            ref, rst = O.pipeline(j, res), 0
+        except O.OracleError as e:
+            ref, rst = None, e.status
+        assert st[k] == rst, (k, st[k], rst)
+        if ref is not None:
+            np.testing.assert_array_equal(host[k], ref, err_msg=f"case {k}")
+
+
 def test_progressive_dri_between_scans_vs_oracle(engine):
     """A DRI segment between the scans of a progressive image (restart intervals that change per
     scan, jdmarker.c get_dri), with non-zero and zero intervals, against the oracle: status, and
