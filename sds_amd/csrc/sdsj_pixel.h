@@ -19,6 +19,14 @@ __device__ __forceinline__ int clamp255i(int v) { return v < 0 ? 0 : v > 255 ? 2
 
 // jdcolor.c ycc_rgb_convert (its tables evaluated arithmetically); cb, cr already minus 128
 // (24-bit multiplies: |constant| < 2^17, |cb|, |cr| <= 128 -- exact, full rate)
+// ycc_px on cb, cr without the 128 subtracted (the offsets folded into the constants: the same
+// integers, so the same results)
+__device__ __forceinline__ void ycc_raw(int y, int cb, int cr, int& r, int& g, int& b) {
+  r = clamp255i(y + ((__mul24(91881, cr) - 11728000) >> 16));
+  g = clamp255i(y + ((__mul24(-46802, cr) + __mul24(-22554, cb) + 8910336) >> 16));
+  b = clamp255i(y + ((__mul24(116130, cb) - 14831872) >> 16));
+}
+
 __device__ __forceinline__ void ycc_px(int y, int cb, int cr, int& r, int& g, int& b) {
   r = clamp255i(y + ((__mul24(91881, cr) + 32768) >> 16));
   g = clamp255i(y + ((__mul24(-46802, cr) + (__mul24(-22554, cb) + 32768)) >> 16));

@@ -6,8 +6,11 @@
 // scans (DHT / DQT / DRI may change from one scan to the next) up to EOI, and the bit reader /
 // restart / resynchronisation rules the baseline path shares (jdhuff.c jpeg_fill_bit_buffer,
 // read_restart_marker + jpeg_resync_to_restart).  Each image's scans depend on one another, so one
-// lane walks an image's whole file; the coefficients land in the same MCU-ordered array the
-// baseline entropy kernels write, and k_idct / the resample kernels take it from there.
+// wave walks an image's whole file (its decoder state wave-uniform, in scalar registers) and its
+// lanes split the work that is parallel within a block: the AC refinement scans coefficient by
+// coefficient, the DC refinement scan block by block (k_prog).  The coefficients land in the same
+// MCU-ordered array the baseline entropy kernels write, and k_idct / the resample kernels take it
+// from there.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

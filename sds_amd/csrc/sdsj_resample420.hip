@@ -349,37 +349,78 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
               wg[k >> 2] |= (uint32_t)g << sh;
               wb[k >> 2] |= (uint32_t)b << sh;
             }
+          } else if (LAY == kRs420) {
+            // h2v2 fancy upsampling (jdsample.c): the chroma column sums 3 * row_i + row_f of columns
+            // jg - 1 .. jg + 4, then per output pixel (3 * own + neighbour + 8 or 7) >> 4.  Interior
+            // items take two columns per 32-bit op (16-bit halves: sums <= 4,088, no carries); items
+            // at the plane's edges (repeated columns) the per-column path.
+            const int oBf = L.rinfo[q][2], oRf = L.rinfo[q][4];
+            int ube[4], ubo[4], ure[4], uro[4];  // upsampled Cb / Cr of the even / odd pixel of column jg + k
+            auto up = [&](int oi, int of, int* ue, int* uo) {
+              const uint32_t i0 = sw[(oi + jg - 4) >> 2], i1 = sw[(oi + jg) >> 2], i2 = sw[(oi + jg + 4) >> 2];
+              const uint32_t f0 = sw[(of + jg - 4) >> 2], f1 = sw[(of + jg) >> 2], f2 = sw[(of + jg + 4) >> 2];
+              if (jg > 0 && jg + 4 <= dwc - 1) {
+                constexpr uint32_t M = 0x00FF00FFu;
+                const uint32_t E = (i1 & M) * 3 + (f1 & M), O = ((i1 >> 8) & M) * 3 + ((f1 >> 8) & M);  // [jg, jg+2], [jg+1, jg+3]
+                const uint32_t l = (i0 >> 24) * 3 + (f0 >> 24), rr = (i2 & 0xFF) * 3 + (f2 & 0xFF);    // jg - 1, jg + 4
+                const uint32_t A = E * 3 + (l | (O << 16)) + 0x00080008u;
+                const uint32_t B = E * 3 + O + 0x00070007u;
+                const uint32_t C = O * 3 + E + 0x00080008u;
+                const uint32_t D = O * 3 + ((E >> 16) | (rr << 16)) + 0x00070007u;
+                ue[0] = (int)((A >> 4) & 0xFFF);
+                ue[1] = (int)((C >> 4) & 0xFFF);
+                ue[2] = (int)(A >> 20);
+                ue[3] = (int)(C >> 20);
+                uo[0] = (int)((B >> 4) & 0xFFF);
+                uo[1] = (int)((D >> 4) & 0xFFF);
+                uo[2] = (int)(B >> 20);
+                uo[3] = (int)(D >> 20);
+              } else {
+                int c[6];
+                c[0] = (int)(i0 >> 24) * 3 + (int)(f0 >> 24);
+#pragma unroll
+                for (int k = 0; k < 4; k++) c[1 + k] = (int)((i1 >> (8 * k)) & 0xFF) * 3 + (int)((f1 >> (8 * k)) & 0xFF);
+                c[5] = (int)(i2 & 0xFF) * 3 + (int)(f2 & 0xFF);
+                if (jg == 0) c[0] = c[1];
+#pragma unroll
+                for (int k = 0; k < 4; k++)  // right edge: column j + 1 past dwc - 1 repeats column j
+                  if (jg + k + 1 > dwc - 1) c[2 + k] = c[1 + k];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                  ue[k] = (c[1 + k] * 3 + c[k] + 8) >> 4;
+                  uo[k] = (c[1 + k] * 3 + c[2 + k] + 7) >> 4;
+                }
+              }
+            };
+            up(oBi, oBf, ube, ubo);
+            up(oRi, oRf, ure, uro);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const uint32_t yw = k < 2 ? y0 : y1;
+              const int ye = (int)((yw >> (16 * (k & 1))) & 0xFF), yo = (int)((yw >> (16 * (k & 1) + 8)) & 0xFF);
+              int r0, g0, b0, r1, g1, b1;
+              ycc_raw(ye, ube[k], ure[k], r0, g0, b0);
+              ycc_raw(yo, ubo[k], uro[k], r1, g1, b1);
+              const int sh = 16 * (k & 1);
+              wr[k >> 1] |= (uint32_t)(r0 | (r1 << 8)) << sh;
+              wg[k >> 1] |= (uint32_t)(g0 | (g1 << 8)) << sh;
+              wb[k >> 1] |= (uint32_t)(b0 | (b1 << 8)) << sh;
+            }
           } else {
-            // chroma column values for columns jg - 1 .. jg + 4: 4:2:0 the column sums
-            // 3 * row_i + row_f, 4:2:2 the row itself (edges repeat column 0 / dwc - 1)
+            // 4:2:2: the chroma row's columns jg - 1 .. jg + 4 (edges repeat column 0 / dwc - 1)
             int cb[6], cr[6];
             {
               const uint32_t bi0 = sw[(oBi + jg - 4) >> 2], bi1 = sw[(oBi + jg) >> 2], bi2 = sw[(oBi + jg + 4) >> 2];
               const uint32_t ri0 = sw[(oRi + jg - 4) >> 2], ri1 = sw[(oRi + jg) >> 2], ri2 = sw[(oRi + jg + 4) >> 2];
-              if (LAY == kRs420) {
-                const int oBf = L.rinfo[q][2], oRf = L.rinfo[q][4];
-                const uint32_t bf0 = sw[(oBf + jg - 4) >> 2], bf1 = sw[(oBf + jg) >> 2], bf2 = sw[(oBf + jg + 4) >> 2];
-                const uint32_t rf0 = sw[(oRf + jg - 4) >> 2], rf1 = sw[(oRf + jg) >> 2], rf2 = sw[(oRf + jg + 4) >> 2];
-                cb[0] = (int)(bi0 >> 24) * 3 + (int)(bf0 >> 24);
-                cr[0] = (int)(ri0 >> 24) * 3 + (int)(rf0 >> 24);
+              cb[0] = (int)(bi0 >> 24);
+              cr[0] = (int)(ri0 >> 24);
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                  cb[1 + k] = (int)((bi1 >> (8 * k)) & 0xFF) * 3 + (int)((bf1 >> (8 * k)) & 0xFF);
-                  cr[1 + k] = (int)((ri1 >> (8 * k)) & 0xFF) * 3 + (int)((rf1 >> (8 * k)) & 0xFF);
-                }
-                cb[5] = (int)(bi2 & 0xFF) * 3 + (int)(bf2 & 0xFF);
-                cr[5] = (int)(ri2 & 0xFF) * 3 + (int)(rf2 & 0xFF);
-              } else {
-                cb[0] = (int)(bi0 >> 24);
-                cr[0] = (int)(ri0 >> 24);
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                  cb[1 + k] = (int)((bi1 >> (8 * k)) & 0xFF);
-                  cr[1 + k] = (int)((ri1 >> (8 * k)) & 0xFF);
-                }
-                cb[5] = (int)(bi2 & 0xFF);
-                cr[5] = (int)(ri2 & 0xFF);
+              for (int k = 0; k < 4; k++) {
+                cb[1 + k] = (int)((bi1 >> (8 * k)) & 0xFF);
+                cr[1 + k] = (int)((ri1 >> (8 * k)) & 0xFF);
               }
+              cb[5] = (int)(bi2 & 0xFF);
+              cr[5] = (int)(ri2 & 0xFF);
               if (jg == 0) {
                 cb[0] = cb[1];
                 cr[0] = cr[1];
@@ -397,13 +438,9 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
               const uint32_t yw = k < 2 ? y0 : y1;
               const int ye = (int)((yw >> (16 * (k & 1))) & 0xFF), yo = (int)((yw >> (16 * (k & 1) + 8)) & 0xFF);
               int r0, g0, b0, r1, g1, b1;
-              if (LAY == kRs420) {  // jdsample.c h2v2_fancy_upsample
-                ycc_px(ye, ((c0 * 3 + cb[k] + 8) >> 4) - 128, ((d0 * 3 + cr[k] + 8) >> 4) - 128, r0, g0, b0);
-                ycc_px(yo, ((c0 * 3 + cb[2 + k] + 7) >> 4) - 128, ((d0 * 3 + cr[2 + k] + 7) >> 4) - 128, r1, g1, b1);
-              } else {  // jdsample.c h2v1_fancy_upsample
-                ycc_px(ye, ((c0 * 3 + cb[k] + 1) >> 2) - 128, ((d0 * 3 + cr[k] + 1) >> 2) - 128, r0, g0, b0);
-                ycc_px(yo, ((c0 * 3 + cb[2 + k] + 2) >> 2) - 128, ((d0 * 3 + cr[2 + k] + 2) >> 2) - 128, r1, g1, b1);
-              }
+              // jdsample.c h2v1_fancy_upsample
+              ycc_px(ye, ((c0 * 3 + cb[k] + 1) >> 2) - 128, ((d0 * 3 + cr[k] + 1) >> 2) - 128, r0, g0, b0);
+              ycc_px(yo, ((c0 * 3 + cb[2 + k] + 2) >> 2) - 128, ((d0 * 3 + cr[2 + k] + 2) >> 2) - 128, r1, g1, b1);
               const int sh = 16 * (k & 1);
               wr[k >> 1] |= (uint32_t)(r0 | (r1 << 8)) << sh;
               wg[k >> 1] |= (uint32_t)(g0 | (g1 << 8)) << sh;
