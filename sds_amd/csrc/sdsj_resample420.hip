@@ -407,40 +407,53 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
               wb[k >> 1] |= (uint32_t)(b0 | (b1 << 8)) << sh;
             }
           } else {
-            // 4:2:2: the chroma row's columns jg - 1 .. jg + 4 (edges repeat column 0 / dwc - 1)
-            int cb[6], cr[6];
-            {
-              const uint32_t bi0 = sw[(oBi + jg - 4) >> 2], bi1 = sw[(oBi + jg) >> 2], bi2 = sw[(oBi + jg + 4) >> 2];
-              const uint32_t ri0 = sw[(oRi + jg - 4) >> 2], ri1 = sw[(oRi + jg) >> 2], ri2 = sw[(oRi + jg + 4) >> 2];
-              cb[0] = (int)(bi0 >> 24);
-              cr[0] = (int)(ri0 >> 24);
+            // 4:2:2 (jdsample.c h2v1_fancy_upsample): the chroma row's columns jg - 1 .. jg + 4, per
+            // output pixel (3 * own + neighbour + 1 or 2) >> 2; interior items two columns per op
+            int ube[4], ubo[4], ure[4], uro[4];
+            auto up = [&](int oi, int* ue, int* uo) {
+              const uint32_t i0 = sw[(oi + jg - 4) >> 2], i1 = sw[(oi + jg) >> 2], i2 = sw[(oi + jg + 4) >> 2];
+              if (jg > 0 && jg + 4 <= dwc - 1) {
+                constexpr uint32_t M = 0x00FF00FFu;
+                const uint32_t E = i1 & M, O = (i1 >> 8) & M;  // columns [jg, jg+2], [jg+1, jg+3]
+                const uint32_t l = i0 >> 24, rr = i2 & 0xFF;    // jg - 1, jg + 4
+                const uint32_t A = E * 3 + (l | (O << 16)) + 0x00010001u;
+                const uint32_t B = E * 3 + O + 0x00020002u;
+                const uint32_t C = O * 3 + E + 0x00010001u;
+                const uint32_t D = O * 3 + ((E >> 16) | (rr << 16)) + 0x00020002u;
+                ue[0] = (int)((A >> 2) & 0x3FFF);
+                ue[1] = (int)((C >> 2) & 0x3FFF);
+                ue[2] = (int)(A >> 18);
+                ue[3] = (int)(C >> 18);
+                uo[0] = (int)((B >> 2) & 0x3FFF);
+                uo[1] = (int)((D >> 2) & 0x3FFF);
+                uo[2] = (int)(B >> 18);
+                uo[3] = (int)(D >> 18);
+              } else {
+                int c[6];
+                c[0] = (int)(i0 >> 24);
 #pragma unroll
-              for (int k = 0; k < 4; k++) {
-                cb[1 + k] = (int)((bi1 >> (8 * k)) & 0xFF);
-                cr[1 + k] = (int)((ri1 >> (8 * k)) & 0xFF);
-              }
-              cb[5] = (int)(bi2 & 0xFF);
-              cr[5] = (int)(ri2 & 0xFF);
-              if (jg == 0) {
-                cb[0] = cb[1];
-                cr[0] = cr[1];
-              }
+                for (int k = 0; k < 4; k++) c[1 + k] = (int)((i1 >> (8 * k)) & 0xFF);
+                c[5] = (int)(i2 & 0xFF);
+                if (jg == 0) c[0] = c[1];
 #pragma unroll
-              for (int k = 0; k < 4; k++)  // right edge: column j + 1 past dwc - 1 repeats column j
-                if (jg + k + 1 > dwc - 1) {
-                  cb[2 + k] = cb[1 + k];
-                  cr[2 + k] = cr[1 + k];
+                for (int k = 0; k < 4; k++)  // right edge: column j + 1 past dwc - 1 repeats column j
+                  if (jg + k + 1 > dwc - 1) c[2 + k] = c[1 + k];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                  ue[k] = (c[1 + k] * 3 + c[k] + 1) >> 2;
+                  uo[k] = (c[1 + k] * 3 + c[2 + k] + 2) >> 2;
                 }
-            }
+              }
+            };
+            up(oBi, ube, ubo);
+            up(oRi, ure, uro);
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-              const int c0 = cb[1 + k], d0 = cr[1 + k];
               const uint32_t yw = k < 2 ? y0 : y1;
               const int ye = (int)((yw >> (16 * (k & 1))) & 0xFF), yo = (int)((yw >> (16 * (k & 1) + 8)) & 0xFF);
               int r0, g0, b0, r1, g1, b1;
-              // jdsample.c h2v1_fancy_upsample
-              ycc_px(ye, ((c0 * 3 + cb[k] + 1) >> 2) - 128, ((d0 * 3 + cr[k] + 1) >> 2) - 128, r0, g0, b0);
-              ycc_px(yo, ((c0 * 3 + cb[2 + k] + 2) >> 2) - 128, ((d0 * 3 + cr[2 + k] + 2) >> 2) - 128, r1, g1, b1);
+              ycc_raw(ye, ube[k], ure[k], r0, g0, b0);
+              ycc_raw(yo, ubo[k], uro[k], r1, g1, b1);
               const int sh = 16 * (k & 1);
               wr[k >> 1] |= (uint32_t)(r0 | (r1 << 8)) << sh;
               wg[k >> 1] |= (uint32_t)(g0 | (g1 << 8)) << sh;
