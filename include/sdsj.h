@@ -52,6 +52,7 @@ extern "C" {
 #define SDSJ_FILTER_HAMMING 2
 #define SDSJ_FILTER_BICUBIC 3
 #define SDSJ_FILTER_LANCZOS 4
+#define SDSJ_FILTER_NEAREST 5 /* Pillow NEAREST (ImagingScaleAffine), torchvision 'nearest' / 'nearest-exact' on PIL */
 
 #define SDSJ_DTYPE_U8 0  /* uint8 samples, as ConvertImageToByteTensorTransform */
 #define SDSJ_DTYPE_F32 1 /* float32 x/127.5-1, as NormalizeFramesTransform */

@@ -24,7 +24,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libsdsj_oracle.so")
 
 OK, EINVAL, UNSUPPORTED, CORRUPT, ENOMEM = 0, -1, -2, -3, -4
-FILTERS = {"box": 0, "bilinear": 1, "hamming": 2, "bicubic": 3, "lanczos": 4}
+FILTERS = {"box": 0, "bilinear": 1, "hamming": 2, "bicubic": 3, "lanczos": 4, "nearest": 5}
 
 
 class OracleInfo(ctypes.Structure):

@@ -23,7 +23,7 @@ SDSJ_ABI_VERSION = 2
 OK, EINVAL, UNSUPPORTED, CORRUPT, ENOMEM, EHIP, ECAPACITY = 0, -1, -2, -3, -4, -5, -6
 STATUS_NAMES = {OK: "OK", EINVAL: "EINVAL", UNSUPPORTED: "UNSUPPORTED", CORRUPT: "CORRUPT", ENOMEM: "ENOMEM",
                 EHIP: "EHIP", ECAPACITY: "ECAPACITY"}
-FILTERS = {"box": 0, "bilinear": 1, "hamming": 2, "bicubic": 3, "lanczos": 4}
+FILTERS = {"box": 0, "bilinear": 1, "hamming": 2, "bicubic": 3, "lanczos": 4, "nearest": 5}
 DTYPE_U8, DTYPE_F32 = 0, 1
 LAYOUT_CHW, LAYOUT_HWC = 0, 1
 

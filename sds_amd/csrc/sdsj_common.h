@@ -586,6 +586,18 @@ SDSJ_HD inline int resample_ksize(int in_size, int out_size, double filter_suppo
   return c * 2 + 1;
 }
 
+// Pillow _imaging.c _resize, NEAREST branch -> ImagingTransform(AFFINE, fill = 1) -> Geometry.c
+// ImagingScaleAffine: output index xx samples source index COORD(xo), xo = scale * 0.5 advanced by
+// `xo += scale` per index (a running double sum, kept as such: (xx + 0.5) * scale can round
+// differently), COORD(v) = v < 0 ? -1 : (int)v; -1 = outside [0, in): the pixel keeps the fill value 0.
+SDSJ_HD inline int nearest_src(int in_size, int out_size, int xx) {
+  const double a = (double)in_size / out_size;
+  double xo = 0.0 + a * 0.5;
+  for (int i = 0; i < xx; i++) xo += a;
+  const int xin = xo < 0.0 ? -1 : (int)xo;
+  return (xin >= 0 && xin < in_size) ? xin : -1;
+}
+
 SDSJ_HD inline double filter_support(int filter) {
   switch (filter) {
     case SDSJ_FILTER_BOX: return 0.5;

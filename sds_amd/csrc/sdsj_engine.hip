@@ -160,7 +160,7 @@ int ensure_scratch(sdsj_engine* e, int64_t need) {
 
 bool valid_op(const sdsj_op* op) {
   return op && op->out_h > 0 && op->out_w > 0 && op->out_h <= 65535 && op->out_w <= 65535 && op->filter >= 0 &&
-         op->filter <= SDSJ_FILTER_LANCZOS && (op->out_dtype == SDSJ_DTYPE_U8 || op->out_dtype == SDSJ_DTYPE_F32) &&
+         op->filter <= SDSJ_FILTER_NEAREST && (op->out_dtype == SDSJ_DTYPE_U8 || op->out_dtype == SDSJ_DTYPE_F32) &&
          (op->layout == SDSJ_LAYOUT_CHW || op->layout == SDSJ_LAYOUT_HWC);
 }
 

@@ -81,11 +81,18 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
   }
   d->need_h = d->geo == kGeoResize && d->cw != op.out_w;
   d->need_v = d->geo == kGeoResize && d->ch != op.out_h;
+  // NEAREST (Pillow ImagingScaleAffine) runs as a one-tap resample through the unfused passes: tap
+  // weight 1 << 22 at the source index nearest_src picks, none where it is outside (fill value 0)
+  const bool nearest = op.filter == SDSJ_FILTER_NEAREST;
   double sup = filter_support(op.filter);
-  d->ksh = d->need_h ? resample_ksize(d->cw, op.out_w, sup) : 0;
-  d->ksv = d->need_v ? resample_ksize(d->ch, op.out_h, sup) : 0;
+  d->ksh = d->need_h ? (nearest ? 1 : resample_ksize(d->cw, op.out_w, sup)) : 0;
+  d->ksv = d->need_v ? (nearest ? 1 : resample_ksize(d->ch, op.out_h, sup)) : 0;
   if (d->geo == kGeoZeros) {
     d->yf = d->yl = 0;
+  } else if (d->need_v && nearest) {
+    const int a = nearest_src(d->ch, op.out_h, 0), b = nearest_src(d->ch, op.out_h, op.out_h - 1);
+    d->yf = a < 0 || b < 0 ? 0 : a;
+    d->yl = a < 0 || b < 0 ? d->ch : b + 1;
   } else if (d->need_v) {
     int a0, a1, b0, b1;
     resample_bounds(d->ch, op.out_h, sup, 0, &a0, &a1);
@@ -106,7 +113,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
   d->tile_w = 0;
   d->ring_rows = 1;
   while (d->ring_rows < d->ksv) d->ring_rows *= 2;  // vertical window rows kept per column
-  if (d->geo != kGeoZeros && d->ring_rows <= kRingMaxRows) {
+  if (d->geo != kGeoZeros && d->ring_rows <= kRingMaxRows && !nearest) {
     const double scale = d->need_h ? (double)d->cw / op.out_w : 1.0;
     const double supp = d->need_h ? sup * (scale < 1.0 ? 1.0 : scale) : 0.0;
     int tw = op.out_w < 256 ? op.out_w : 256;
@@ -1256,6 +1263,13 @@ __device__ double filt_eval(int filter, double x) {
 }
 
 __device__ void coeffs_one(int in_size, int out_size, int filter, int ksize, int xx, int32_t* bounds, int32_t* kk) {
+  if (filter == SDSJ_FILTER_NEAREST) {  // one tap of weight 1.0 (ksize 1), or none (fill value 0)
+    const int s = nearest_src(in_size, out_size, xx);
+    kk[xx] = 1 << 22;
+    bounds[2 * xx] = s < 0 ? 0 : s;
+    bounds[2 * xx + 1] = s < 0 ? 0 : 1;
+    return;
+  }
   const double scale = (double)in_size / out_size;
   const double filterscale = scale < 1.0 ? 1.0 : scale;
   const double support = filter_support(filter) * filterscale;

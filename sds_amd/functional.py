@@ -11,16 +11,22 @@ from . import _lib
 _RESIZE_KWARGS = {"crop_before_resize", "allow_vertical", "random_resize", "interpolation_mode"}
 
 
+# torchvision's pil_modes_mapping: NEAREST_EXACT resizes a PIL image with PIL NEAREST, as NEAREST does
+_TV_TO_PIL = {"nearest-exact": "nearest"}
+
+
 def filter_name(mode) -> str:
     """torchvision InterpolationMode (enum or its string value) -> engine filter name.
 
-    The reference resizes PIL images, so TVF.resize delegates to PIL.Image.resize with the same
-    filter; every Pillow separable filter is implemented.  NEAREST uses a different Pillow code
-    path and is not implemented."""
+    The reference resizes PIL images (functional.py:84), so TVF.resize delegates to PIL.Image.resize
+    with the mapped Pillow filter: every Pillow separable filter (Resample.c) and NEAREST
+    (Geometry.c ImagingScaleAffine, for both 'nearest' and 'nearest-exact') are implemented.  A name
+    InterpolationMode does not define raises ValueError, as ``TVF.InterpolationMode(name)`` does."""
     name = getattr(mode, "value", mode)
     name = str(name).lower()
+    name = _TV_TO_PIL.get(name, name)
     if name not in _lib.FILTERS:
-        raise NotImplementedError(f"interpolation_mode={mode!r} is not implemented on the MI355X path")
+        raise ValueError(f"{mode!r} is not a valid InterpolationMode")
     return name
 
 

@@ -196,6 +196,9 @@ class GpuDecodeResizeImageTransform(BaseTransform):
         eng = _engine_in_worker(self.device)
         need_size = bool(kw.get("allow_vertical")) or kw.get("random_resize") is not None
         resolution = self.resolution
+        # taken before target_resolution's np.random.choice, so that a rerun on the host (which draws
+        # again, after PIL's decode, as the reference does) leaves the RNGs one draw ahead, not two
+        rng = _RngSnapshot(kw.get("random_resize") is not None, self.hflip_prob > 0.0)
         if need_size:
             st, info = _lib.probe(data)
             if st != _lib.OK or info.width <= 0 or info.height <= 0:  # not a JPEG this path decodes
@@ -204,7 +207,6 @@ class GpuDecodeResizeImageTransform(BaseTransform):
                 return sample
             resolution = F.target_resolution(int(info.width), int(info.height), self.resolution,
                                              kw.get("allow_vertical", False), kw.get("random_resize"))
-        rng = _RngSnapshot(kw.get("random_resize") is not None, self.hflip_prob > 0.0)
         flip = [bool(torch.rand(1) < self.hflip_prob)] if self.hflip_prob > 0.0 else None
         out, status = eng.decode_resize([data], resolution, crop_before_resize=kw.get("crop_before_resize", True),
                                         filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),

@@ -10,7 +10,8 @@ unmodified from /root/reference.  Four of its imports are absent from this image
 stubbed in a temporary directory (never inside /root/reference): ``loguru`` (no-op logger),
 ``beartype`` (identity decorator), ``boto3`` and ``av`` (empty modules, unused on the image
 path), plus ``torchvision.transforms.functional.resize`` restated as torchvision's PIL branch
-(``img.resize((w, h), PIL_MODE[interpolation])`` with its same-size shortcut).  The
+(``img.resize((w, h), PIL_MODE[interpolation])`` with its same-size shortcut; PIL_MODE is torchvision's
+``pil_modes_mapping``, which sends both NEAREST and NEAREST_EXACT to PIL NEAREST).  The
 arithmetic therefore comes from Pillow 12.2.0 + libjpeg-turbo 3.1.4 exactly as in the
 reference's deployment.  Bytecode writing is disabled so nothing lands in /root/reference.
 
@@ -54,7 +55,8 @@ STUBS = {
         "class InterpolationMode(enum.Enum):\n"
         "    NEAREST = 'nearest'; NEAREST_EXACT = 'nearest-exact'; BILINEAR = 'bilinear'\n"
         "    BICUBIC = 'bicubic'; BOX = 'box'; HAMMING = 'hamming'; LANCZOS = 'lanczos'\n"
-        "_PIL = {InterpolationMode.NEAREST: Image.NEAREST, InterpolationMode.BILINEAR: Image.BILINEAR,\n"
+        "_PIL = {InterpolationMode.NEAREST: Image.NEAREST, InterpolationMode.NEAREST_EXACT: Image.NEAREST,\n"
+        "        InterpolationMode.BILINEAR: Image.BILINEAR,\n"
         "        InterpolationMode.BICUBIC: Image.BICUBIC, InterpolationMode.BOX: Image.BOX,\n"
         "        InterpolationMode.HAMMING: Image.HAMMING, InterpolationMode.LANCZOS: Image.LANCZOS}\n"
         "def resize(img, size, interpolation=InterpolationMode.BILINEAR, max_size=None, antialias=True):\n"

@@ -167,6 +167,69 @@ def test_fallback_in_gpu_decode_batch():
         GpuDecodeBatch("img", (32, 32), device="cuda", on_error="raise")({"img": enc})
 
 
+def _g7_data(case, g1, g2, g3, z):
+    if case["source"] == "g1":
+        return g1[case["name"]]
+    if case["source"] == "g2":
+        return g2[case["index"]]
+    if case["source"] == "g3":
+        return g3[case["index"]]
+    return z[f"{case['name']}__bytes"].tobytes()
+
+
+def test_nearest_interpolation_matches_reference_g7():
+    """resize_kwargs interpolation_mode 'nearest' / 'nearest-exact' (functional.py:84: torchvision maps both
+    to PIL NEAREST for PIL images): Pillow's ImagingScaleAffine source indices as one-tap GPU resamples,
+    equal to G7 (tests/golden/make_nearest.py, made by the reference pipeline) -- G2 at 256, G3's mixed
+    sizes at 512 (allow_vertical on the portrait ones), small 4:2:0 / 4:2:2 / 4:4:4 / gray / progressive
+    JPEGs with upscaling, no crop and normalize, and a PNG through the host-decode route."""
+    from sds_amd.presets import create_standard_image_pipeline
+    meta = G.load_json("g7_nearest.json")
+    z = np.load(os.path.join(G.GOLDEN, "g7_nearest.npz"))
+    g1 = {c["name"]: jpg for c, jpg, _ in G.g1()}
+    g2, g3 = G.g2_jpegs()[1], G.g3_jpegs()[1]
+    tmp = tempfile.mkdtemp()
+    n = 0
+    for case in meta["cases"]:
+        p = _write(tmp, case["name"], _g7_data(case, g1, g2, g3, z))
+        for vname, ref in case["variants"].items():
+            ts = create_standard_image_pipeline("img", tuple(ref["resolution"]), device="cuda", **ref["kwargs"])
+            if not ref["ok"]:
+                with pytest.raises(OSError):
+                    _run(ts, {"img": p})
+                continue
+            img = _run(ts, {"img": p})["image"]
+            assert img.device.type == "cuda" and list(img.shape) == ref["shape"], (case["name"], vname)
+            got = img.cpu().contiguous().numpy()
+            key = f"{case['name']}__{vname}"
+            if key in z.files:
+                np.testing.assert_array_equal(got, z[key], err_msg=key)
+            assert G.sha(got) == ref["sha256"], key
+            n += 1
+    assert n >= 70
+
+
+def test_corrupt_jpeg_with_random_resize_draws_the_np_rng_once():
+    """A JPEG the GPU reports CORRUPT while its header probes fine (no EOI, which Pillow decodes) reruns
+    on PIL: with random_resize the reference draws np.random.choice once, after its decode
+    (functional.py:69-74), so the global numpy state afterwards equals one draw from the state before."""
+    from sds_amd.presets import create_standard_image_pipeline
+    meta, z = _g6()
+    data = z["jpeg_no_eoi_64x48__bytes"].tobytes()
+    p = _write(tempfile.mkdtemp(), "no_eoi.jpg", data)
+    rr = {(16, 16): 0.25, (24, 32): 0.25, (32, 32): 0.5}
+    ts = create_standard_image_pipeline("img", (32, 32), device="cuda", resize_kwargs={"random_resize": rr})
+    for seed in range(6):
+        np.random.seed(seed)
+        img = _run(ts, {"img": p})["image"]
+        got_state = np.random.get_state()[1].copy()
+        np.random.seed(seed)
+        res, probs = zip(*rr.items())
+        choice = res[np.random.choice(len(res), p=np.array(probs) / sum(probs))]
+        assert np.array_equal(got_state, np.random.get_state()[1]), seed
+        assert tuple(img.shape[1:]) == tuple(choice), (seed, choice)
+
+
 def _case(name):
     env = dict(os.environ)
     r = subprocess.run([sys.executable, "-m", "tests.loader_cases", name], capture_output=True, text=True,

@@ -45,7 +45,8 @@ def _ref(frame, res, filt="bilinear", crop=True, flip=False, normalize=False):
 
 @pytest.mark.parametrize("size,res,filt", [((97, 61), (64, 80), "bilinear"), ((640, 360), (256, 256), "bilinear"),
                                            ((320, 240), (512, 512), "bilinear"), ((200, 150), (100, 60), "bicubic"),
-                                           ((64, 48), (48, 64), "lanczos")])
+                                           ((64, 48), (48, 64), "lanczos"), ((97, 61), (131, 40), "nearest"),
+                                           ((640, 360), (256, 256), "nearest")])
 def test_frames_match_oracle(engine, size, res, filt):
     w, h = size
     fr = _frames(7, 5, w, h)

@@ -141,12 +141,29 @@ def test_random_batch_vs_oracle(engine, seed):
         np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res), err_msg=f"image {k}")
 
 
-@pytest.mark.parametrize("filt", ["box", "bicubic", "hamming", "lanczos"])
+@pytest.mark.parametrize("filt", ["box", "bicubic", "hamming", "lanczos", "nearest"])
 def test_other_pillow_filters(engine, filt):
     _, jpgs = G.g2_jpegs()
     got, st = engine.decode_resize(jpgs[:2], (200, 150), filter=filt)
     for k in range(2):
         np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(jpgs[k], (200, 150), filter=filt))
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_nearest_random_batches_vs_oracle(engine, seed):
+    """NEAREST (Pillow ImagingScaleAffine as one-tap resamples) on random JPEGs (samplings, restarts,
+    optimized tables) at random up- and down-scaled resolutions, crop and no crop, flips and HWC."""
+    jpgs = _random_jpegs(seed, 48)
+    rng = np.random.default_rng(seed + 7)
+    for crop in (True, False):
+        res = (int(rng.integers(1, 300)), int(rng.integers(1, 300)))
+        flip = [bool(v) for v in rng.integers(0, 2, len(jpgs))]
+        got, st = engine.decode_resize(jpgs, res, filter="nearest", crop_before_resize=crop, flip=flip)
+        assert (st == 0).all()
+        for k, j in enumerate(jpgs):
+            np.testing.assert_array_equal(got[k].cpu().numpy(),
+                                          O.pipeline(j, res, crop_before_resize=crop, filter="nearest", flip=flip[k]),
+                                          err_msg=f"image {k} res {res} crop {crop}")
 
 
 def test_4k_vs_oracle(engine):

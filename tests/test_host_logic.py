@@ -41,8 +41,15 @@ def test_filter_names():
     class Mode:  # torchvision InterpolationMode stand-in
         value = "bicubic"
     assert F.filter_name(Mode()) == "bicubic"
-    with pytest.raises(NotImplementedError):
-        F.filter_name("nearest")
+    # torchvision pil_modes_mapping: NEAREST and NEAREST_EXACT both resize PIL images with PIL NEAREST
+    assert F.filter_name("nearest") == "nearest"
+    assert F.filter_name("nearest-exact") == "nearest"
+
+    class Exact:
+        value = "nearest-exact"
+    assert F.filter_name(Exact()) == "nearest"
+    with pytest.raises(ValueError):  # TVF.InterpolationMode('cubic') raises ValueError
+        F.filter_name("cubic")
     with pytest.raises(TypeError):
         F.check_resize_kwargs({"antialias": True})
 

@@ -216,3 +216,57 @@ def test_oracle_frame_resize_matches_g6_fallback_goldens():
             np.testing.assert_array_equal(rgb.transpose(2, 0, 1), z[key], err_msg=key)
             checked += 1
     assert checked >= 30
+
+
+def test_oracle_nearest_matches_pil_on_random_shapes():
+    """interpolation_mode 'nearest' / 'nearest-exact' (torchvision -> PIL NEAREST): the oracle's restatement
+    of ImagingScaleAffine (running double sum of the scale, COORD truncation) equals Image.resize(NEAREST)
+    on random up- and down-scales."""
+    from PIL import Image
+    rng = np.random.default_rng(44)
+    for _ in range(300):
+        w, h = (int(v) for v in rng.integers(1, 300, 2))
+        ow, oh = (int(v) for v in rng.integers(1, 300, 2))
+        a = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        ref = np.asarray(Image.fromarray(a).resize((ow, oh), Image.NEAREST))
+        np.testing.assert_array_equal(O.resize(a, oh, ow, "nearest"), ref, err_msg=f"{w}x{h} -> {ow}x{oh}")
+
+
+def test_oracle_matches_g7_nearest_goldens():
+    """G7 (tests/golden/make_nearest.py, the reference pipeline with interpolation_mode nearest /
+    nearest-exact): the oracle pipeline (decode, crop, NEAREST resize, flip-free, LUT normalise) equals the
+    reference's outputs for every JPEG case; the PNG case through PIL's decode + the oracle's resize."""
+    import io
+
+    from PIL import Image
+    meta = G.load_json("g7_nearest.json")
+    z = np.load(f"{G.GOLDEN}/g7_nearest.npz")
+    g1 = {c["name"]: jpg for c, jpg, _ in G.g1()}
+    g2, g3 = G.g2_jpegs()[1], G.g3_jpegs()[1]
+    checked = 0
+    for case in meta["cases"]:
+        src = case["source"]
+        data = g1[case["name"]] if src == "g1" else g2[case["index"]] if src == "g2" else \
+            g3[case["index"]] if src == "g3" else z[f"{case['name']}__bytes"].tobytes()
+        for vname, ref in case["variants"].items():
+            kw = ref["kwargs"]
+            rk = kw.get("resize_kwargs", {})
+            res = tuple(ref["resolution"])
+            rgb = np.asarray(Image.open(io.BytesIO(data)).convert("RGB")) if src == "npz bytes" else O.decode(data)
+            h, w = rgb.shape[:2]
+            out_h, out_w = res
+            if rk.get("allow_vertical") and h > w:
+                out_h, out_w = max(res), min(res)
+            if (w, h) != (out_w, out_h):
+                if rk.get("crop_before_resize", True):
+                    x0, y0, x1, y1 = O.crop_box(w, h, out_h, out_w)
+                    rgb = rgb[y0:y1, x0:x1]
+                # an empty crop (1x1 -> 48x64) resizes to zeros: every source index is outside the image
+                rgb = O.resize(np.ascontiguousarray(rgb), out_h, out_w, "nearest") if rgb.size else \
+                    np.zeros((out_h, out_w, 3), np.uint8)
+            chw = np.ascontiguousarray(rgb.transpose(2, 0, 1))
+            if kw.get("normalize"):
+                chw = O.normalize_lut()[chw]
+            assert G.sha(chw) == ref["sha256"], (case["name"], vname)
+            checked += 1
+    assert checked >= 70
