@@ -616,6 +616,7 @@ __device__ void finish_scan(ImgDesc* d, const SegView sv, const uint8_t* raw, in
 struct UsClass {
   uint32_t u[9];
   uint32_t emit, stuffed, split, endm, vmask;
+  uint32_t fillstuff;  // stuffed zeros preceded by two or more FF bytes (FF FF .. 00)
 };
 __device__ __forceinline__ int us_byte(const UsClass& c, int k) {
   uint32_t dw = 0;
@@ -658,6 +659,14 @@ __device__ __forceinline__ void us_classify(const uint8_t* e, int64_t L, int64_t
   c.vmask = nvalid >= kUsBytes ? 0xFFFFFFFFu : (nvalid <= 0 ? 0u : ((1u << nvalid) - 1u));
   const uint32_t marker = prevff & ~isz & ~isff & c.vmask;
   c.stuffed = prevff & isz;
+  // FF FF .. 00 (fill bytes before a stuffed zero; not valid JPEG, jdhuff.c jpeg_fill_bit_buffer reads it
+  // as one FF data byte): libjpeg-turbo's decode_mcu_fast takes the first FF FF for a marker, decodes the
+  // rest of that MCU from zero bits into the coefficient blocks, then decode_mcu_slow re-decodes the MCU
+  // over them -- coefficients the slow path leaves zero keep the fast path's values.  Streams that hold it
+  // are reported SDSJ_CORRUPT (the transforms rerun them on PIL).
+  const uint32_t prev2ff = (isff << 2) | ((my0 > 0 && (c.u[0] >> 24) == 0xFF) ? 2u : 0u) |
+                           ((my0 > 0 && ((c.u[0] >> 16) & 0xFF) == 0xFF) ? 1u : 0u);
+  c.fillstuff = c.stuffed & prev2ff;
   c.emit = ~isff & ~marker & c.vmask;
   c.split = marker & issp;
   c.endm = (marker & ~issp) | ~c.vmask;  // the first byte past the input ends the data as well
@@ -811,6 +820,8 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_us_serial(const uint8_t* __
       const int tile_end = us_tile_end(my_end, t, wmin);
       const bool ends = tile_end != kUsNone;
       if (ends && my_end == tile_end) s_code = us_end_code(c, t, tile_end);
+      // (restart intervals: libjpeg-turbo decodes every MCU with decode_mcu_slow, no divergence)
+      if ((c.fillstuff & us_below(tile_end, t)) && d->restart_interval == 0) d->status = SDSJ_CORRUPT;
       const int tot = us_place(c, my0, t, tile_end, obase, nsplit, ends || j == ntiles - 1, out, sv, buf, wsum);
       obase += tot & 0xFFFF;
       nsplit += tot >> 16;
@@ -958,7 +969,7 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_us_write(const uint8_t* __r
   const int32_t* lst = route_list(routes, cap, kRtUsBig);
   for (int v = blockIdx.x; v < cnt * kUsGrid; v += gridDim.x) {
     const int img = lst[v / kUsGrid];
-    const ImgDesc* d = &descs[img];
+    ImgDesc* d = &descs[img];
     if (d->status != SDSJ_OK) continue;  // (split-marker overflow found by pass 2)
     const int ntiles = d->ntiles;
     const uint8_t* e = blob + offsets[img] + d->entropy_off;
@@ -974,6 +985,8 @@ __global__ void __launch_bounds__(kUnstuffThreads) k_us_write(const uint8_t* __r
       UsClass c;
       us_load(e, L, my0, raw);
       us_classify(e, L, my0, raw, c);
+      if ((c.fillstuff & us_below(r.end, t)) && d->restart_interval == 0)
+        d->status = SDSJ_CORRUPT;  // FF FF .. 00 (us_classify)
       us_place(c, my0, t, r.end, r.emit, r.split, r.code == kUsFinal, out, sv, buf, wsum);
       if (r.code == kUsFinal) break;
       __syncthreads();  // buf and wsum reused
@@ -994,7 +1007,8 @@ __global__ void __launch_bounds__(64) k_scanmap(int n, const uint8_t* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// k_idct: dequantisation + jpeg_idct_islow; one block per thread, 256 blocks per iteration.
+// k_idct: dequantisation + ISLOW IDCT with the SIMD version's 16-bit semantics (sdsj_idct.h); one block per
+// thread, 256 blocks per iteration.
 // ------------------------------------------------------------------------------------------
 constexpr int kIdctThreads = 256;
 #ifndef SDSJ_IDCT_GRID
@@ -1109,7 +1123,14 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
     uint4 raw[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) raw[i] = zb ? make_uint4(0, 0, 0, 0) : src[i];
-    // DEQUANTIZE: coef * quantval, zigzag position k into row-major natural_order(k)
+    // `ac`: any raw coefficient outside row 0 (the SIMD pass 1's zero test); row 0 is zigzag positions
+    // 0, 1, 5, 6, 14, 15, 27 and 28
+    uint32_t ac = raw[0].y | (raw[0].z & 0xFFFFu) | (raw[0].w & 0xFFFF0000u) | raw[1].x | raw[1].y | raw[1].z |
+                  raw[3].x | (raw[3].y & 0xFFFFu) | (raw[3].z & 0xFFFF0000u) | raw[3].w;
+#pragma unroll
+    for (int i = 2; i < 8; i++) ac |= i == 3 ? 0u : (raw[i].x | raw[i].y | raw[i].z | raw[i].w);
+    // DEQUANTIZE as vpmullw: the low 16 bits of coef * quantval, zigzag position k into row-major
+    // natural_order(k)
     int x[64];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -1117,30 +1138,37 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
       const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
       const int q[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
-      for (int k = 0; k < 8; k++)
-        x[natural_order(i * 8 + k)] = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFF) * q[k];
+      for (int k = 0; k < 8; k++) {
+        const int cv = (int)(int16_t)((w[k >> 1] >> ((k & 1) * 16)) & 0xFFFF);
+        x[natural_order(i * 8 + k)] = wrap16(cv * q[k]);
+      }
     }
-    // pass 1: columns (a column without AC terms: DC << PASS1_BITS, jidctint.c's shortcut)
+    // pass 1: columns.  A block whose rows 1..7 are all zero takes the SIMD shortcut (vpsllw: every
+    // column is the dequantised DC << PASS1_BITS, wrapped to 16 bits); otherwise every column runs the
+    // butterfly, saturated to 16 bits.  On such a block the butterfly of column k gives sat16(4 x[k]) in
+    // every row, so the shortcut is the butterfly on x[k] = wrap16(4 x[k]) / 4 (exact: a multiple of 4).
+    if (!ac) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) x[k] = wrap16(x[k] * 4) >> 2;
+    }
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      int o[8];
+      uint32_t o[8];
       islow_1d(x[k], x[8 + k], x[16 + k], x[24 + k], x[32 + k], x[40 + k], x[48 + k], x[56 + k], o);
-      const bool dc_only = (x[8 + k] | x[16 + k] | x[24 + k] | x[32 + k] | x[40 + k] | x[48 + k] | x[56 + k]) == 0;
-      const int dc4 = x[k] * 4;
 #pragma unroll
-      for (int j = 0; j < 8; j++) x[j * 8 + k] = dc_only ? dc4 : (o[j] + (1 << 10)) >> 11;  // DESCALE(, CONST_BITS-PASS1_BITS)
+      for (int j = 0; j < 8; j++) x[j * 8 + k] = descale_p1(o[j]);
     }
     // pass 2: rows -> 8 bytes of plane row by * 8 + r
     uint8_t* dst = planes + cplane[c] + (int64_t)(by * 8) * cpitch[c] + bx * 8;
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-      int o[8];
+      uint32_t o[8];
       islow_1d(x[r * 8], x[r * 8 + 1], x[r * 8 + 2], x[r * 8 + 3], x[r * 8 + 4], x[r * 8 + 5], x[r * 8 + 6], x[r * 8 + 7], o);
       uint32_t lo = 0, hi = 0;
 #pragma unroll
-      for (int k = 0; k < 4; k++) lo |= range_limit((o[k] + (1 << 17)) >> 18) << (8 * k);
+      for (int k = 0; k < 4; k++) lo |= descale_p2(o[k]) << (8 * k);
 #pragma unroll
-      for (int k = 0; k < 4; k++) hi |= range_limit((o[k + 4] + (1 << 17)) >> 18) << (8 * k);
+      for (int k = 0; k < 4; k++) hi |= descale_p2(o[k + 4]) << (8 * k);
       *reinterpret_cast<uint2*>(dst + (int64_t)r * cpitch[c]) = make_uint2(lo, hi);
     }
   }

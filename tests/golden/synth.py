@@ -80,6 +80,44 @@ def mutated_jpegs(seed: int, n: int) -> list[bytes]:
     return out
 
 
+def has_fill_stuffing(jpg: bytes) -> bool:
+    """True if a baseline JPEG without restart intervals holds FF FF .. 00 (fill bytes before a stuffed
+    zero) inside its scan -- before the first marker that ends it (RSTn and codes below SOF0 do not).
+    jdhuff.c's slow path reads it as one FF data byte; libjpeg-turbo's decode_mcu_fast takes it for a
+    marker and leaves that MCU's fast-path coefficients under the slow path's, so the MI355X kernels
+    report such streams SDSJ_CORRUPT and the transforms rerun them on PIL (sdsj_kernels.hip us_classify)."""
+    d, i, ri = jpg, 2, 0
+    while i + 4 <= len(d) and d[i] == 0xFF:
+        m, ln = d[i + 1], (d[i + 2] << 8) | d[i + 3]
+        if m == 0xDD and ln == 4:
+            ri = (d[i + 4] << 8) | d[i + 5]
+        if m == 0xC2 or ri:
+            return False
+        if m == 0xDA:
+            i += 2 + ln
+            break
+        i += 2 + ln
+    else:
+        return False
+    n = len(d)
+    while i < n:
+        if d[i] != 0xFF:
+            i += 1
+            continue
+        j = i + 1
+        while j < n and d[j] == 0xFF:
+            j += 1
+        if j >= n:
+            return False
+        if d[j] == 0:
+            if j - i >= 2:
+                return True
+        elif not (0xD0 <= d[j] <= 0xD7 or d[j] < 0xC0):
+            return False
+        i = j + 1
+    return False
+
+
 def progressive_jpegs(seed: int, n: int, max_w: int = 400, max_h: int = 300) -> list[bytes]:
     """Progressive JPEGs (PIL/libjpeg-turbo's default scan script) of random sizes, sampling,
     quality, optimized tables and restart intervals, grayscale every fifth."""

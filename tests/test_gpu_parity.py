@@ -205,16 +205,74 @@ def _oracle_result(jpg, res):
 
 @pytest.mark.parametrize("seed", [11, 12])
 def test_mutated_streams_match_oracle_status_and_pixels(engine, seed):
-    """Status per sample equals the oracle's (OK / CORRUPT); OK samples are bit-exact."""
-    from tests.golden.synth import mutated_jpegs
+    """Status per sample equals the oracle's (OK / CORRUPT); OK samples are bit-exact.  Streams with fill
+    bytes before a stuffed zero (FF FF .. 00, no restart intervals) report CORRUPT (libjpeg-turbo's fast
+    path decodes them differently from the slow path the oracle restates; the transforms rerun them on PIL)."""
+    from tests.golden.synth import has_fill_stuffing, mutated_jpegs
     jpgs = mutated_jpegs(seed, 40)
     res = (48, 64)
     got, st = engine.decode_resize(jpgs, res)
     for k, j in enumerate(jpgs):
         ost, ref = _oracle_result(j, res)
+        if ost == O.OK and has_fill_stuffing(j):
+            ost = O.CORRUPT
         assert int(st[k]) == ost, f"sample {k}: gpu {int(st[k])} vs oracle {ost}"
         if ost == O.OK:
             np.testing.assert_array_equal(got[k].cpu().numpy(), ref, err_msg=f"sample {k}")
+
+
+def test_simd_idct_semantics_on_extreme_coefficients_vs_oracle(engine):
+    """k_idct's 16-bit lane semantics (libjpeg-turbo's x86 SIMD ISLOW, which Pillow runs): JPEGs whose
+    dequantised coefficients leave 16 bits (tests/golden/coefjpeg.py; the oracle equals PIL on them,
+    test_oracle_simd_idct_matches_pil_on_extreme_coefficients) -- full-resolution HWC decodes, and
+    crop + resize with flips -- bit-exact against the oracle."""
+    from tests.golden.coefjpeg import extreme_jpegs
+    jpgs = extreme_jpegs(202, 96)
+    for j in jpgs[:24]:
+        ref = O.decode(j)
+        got, st = engine.decode_resize([j], ref.shape[:2], layout="hwc")
+        assert st[0] == 0
+        np.testing.assert_array_equal(got[0].cpu().numpy(), ref)
+    res = (24, 20)
+    flips = [k % 2 == 1 for k in range(len(jpgs))]
+    got, st = engine.decode_resize(jpgs, res, flip=flips)
+    assert (st == 0).all(), st
+    for k, j in enumerate(jpgs):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res, flip=flips[k]), err_msg=f"image {k}")
+
+
+def test_fill_stuffed_streams_rerun_on_pil_through_the_transform():
+    """FF FF .. 00 inside a baseline scan: the GPU reports CORRUPT, the per-sample transform reruns the
+    sample on PIL, so the output equals the reference's PIL decode + resize."""
+    import io
+    import tempfile
+
+    from PIL import Image
+
+    from sds_amd.presets import create_standard_image_pipeline
+    from tests.golden.synth import encode_jpeg, has_fill_stuffing, synth_rgb
+    tmp = tempfile.mkdtemp()
+    n = 0
+    for seed in range(6):
+        j = encode_jpeg(synth_rgb(np.random.default_rng(seed), 160, 120), 90)
+        sos = j.index(b"\xff\xda")
+        p = sos + 2 + ((j[sos + 2] << 8) | j[sos + 3]) + 200 + 37 * seed
+        jb = j[:p] + b"\xff\xff\xff\x00" + j[p:]
+        assert has_fill_stuffing(jb)
+        _, st = engine.decode_resize([jb], (32, 32))
+        assert st[0] == O.CORRUPT
+        path = f"{tmp}/{seed}.jpg"
+        with open(path, "wb") as f:
+            f.write(jb)
+        img = {"jpg": path}
+        for t in create_standard_image_pipeline("jpg", (32, 32), device="cuda"):
+            img = t(img)
+        pil = Image.open(io.BytesIO(jb)).convert("RGB")
+        x0, y0, x1, y1 = O.crop_box(160, 120, 32, 32)
+        ref = np.asarray(pil.crop((x0, y0, x1, y1)).resize((32, 32), Image.BILINEAR)).transpose(2, 0, 1)
+        np.testing.assert_array_equal(img["image"].cpu().contiguous().numpy(), ref)
+        n += 1
+    assert n == 6
 
 
 def test_empty_batch_and_single_pixel(engine):
