@@ -186,6 +186,54 @@ int sdsj_engine_stage_times(const sdsj_engine* eng, float* ms, int cap, int* n_s
 
 const char* sdsj_last_error(const sdsj_engine* eng);
 
+/* Node-local decode service (SURVEY.md §8(f) f1 for the reference's own loader shape: sds runs the
+ * transform list per sample inside forked DataLoader workers, sds/dataset.py:535-561, with
+ * DataLoader(num_workers=2, pin_memory=True), examples/iter_image_dataset.py:72-80 /
+ * sds/dataloader.py:191-193 -- workers that cannot initialise HIP after their parent did).  One
+ * process per GPU owns `engines` engines (each its own stream and scratch, one batch in flight each);
+ * the per-sample transform in every worker sends its encoded bytes through a shared-memory region and
+ * a SOCK_SEQPACKET request, and the service coalesces the requests of all workers into batched engine
+ * calls and writes host outputs (the reference's tensor type) back into the worker's region.
+ *
+ * Wire protocol (little-endian, fixed-size packets on an AF_UNIX SOCK_SEQPACKET connection):
+ *   client -> service  sdsj_svc_req.  kind MAP carries the client's region (memfd) as SCM_RIGHTS, in_len =
+ *                      its size; the service maps it and replies.  kind DECODE: the JPEG is region[0,
+ *                      in_len), the output (op->out_h * out_w * 3 elements of op->out_dtype, op->layout) is
+ *                      written to region[out_off, ...).  kind FRAME: region[0, in_len) is a uint8 HWC RGB
+ *                      frame of width x height (a sample decoded by PIL), cropped / resized as DECODE does.
+ *   service -> client  sdsj_svc_rep {seq, status}: status = the sample's SDSJ_* code (the output is in the
+ *                      region when SDSJ_OK). */
+#define SDSJ_SVC_MAGIC 0x4A534453u /* "SDSJ" */
+#define SDSJ_SVC_MAP 1
+#define SDSJ_SVC_DECODE 2
+#define SDSJ_SVC_FRAME 3
+typedef struct sdsj_svc_req {
+    uint32_t magic, kind;
+    uint64_t seq;
+    int64_t in_len, out_off;
+    int32_t width, height; /* FRAME only */
+    sdsj_op op;
+    int32_t flip;
+    int32_t reserved;
+} sdsj_svc_req; /* 72 bytes */
+typedef struct sdsj_svc_rep {
+    uint64_t seq;
+    int32_t status, reserved;
+} sdsj_svc_rep; /* 16 bytes */
+
+typedef struct sdsj_service_cfg {
+    int32_t abi_version; /* SDSJ_ABI_VERSION */
+    int32_t device;      /* HIP device */
+    int32_t engines;     /* batches in flight at once (0 = 4) */
+    int32_t max_batch;   /* requests per batch (0 = 64) */
+    int32_t listen_fd;   /* a bound, listening AF_UNIX SOCK_SEQPACKET socket */
+    int32_t parent_pid;  /* the service returns when this process is gone (0 = never) */
+} sdsj_service_cfg;
+
+/* Serves requests until SIGTERM / SIGINT or the parent's exit; returns SDSJ_OK, or an error code with a
+ * message on stderr.  Runs in the calling thread (the service process's main thread). */
+int sdsj_service_serve(const sdsj_service_cfg* cfg);
+
 /* Diagnostics for tests: device pointers of the engine's scratch and per-image descriptor array of the
  * most recent chunk, and the byte size of one descriptor (layout: sds_amd/csrc/sdsj_common.h ImgDesc). */
 int sdsj_engine_debug_buffers(const sdsj_engine* eng, void** scratch, void** descs, int64_t* desc_bytes,

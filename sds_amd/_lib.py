@@ -33,7 +33,7 @@ EXPORTS = [
     "sdsj_decode_resize_batch_device", "sdsj_engine_set_timing", "sdsj_engine_stage_times", "sdsj_last_error",
     "sdsj_stage_name", "sdsj_engine_debug_buffers", "sdsj_resize_frames_device", "sdsj_submit_batch",
     "sdsj_submit_files", "sdsj_wait_batch", "sdsj_engine_counters", "sdsj_counter_name", "sdsj_engine_set_lanes",
-    "sdsj_engine_reserve", "sdsj_plan_need",
+    "sdsj_engine_reserve", "sdsj_plan_need", "sdsj_service_serve",
 ]
 NUM_COUNTERS = 10  # SDSJ_NUM_COUNTERS
 SLOTS = 2  # SDSJ_SLOTS: batches in flight on the asynchronous host path
@@ -57,6 +57,11 @@ class SdsjCfg(ctypes.Structure):
 class SdsjOp(ctypes.Structure):
     _fields_ = [("out_h", ctypes.c_int32), ("out_w", ctypes.c_int32), ("crop_before_resize", ctypes.c_int32),
                 ("filter", ctypes.c_int32), ("out_dtype", ctypes.c_int32), ("layout", ctypes.c_int32)]
+
+
+class SdsjServiceCfg(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("device", ctypes.c_int32), ("engines", ctypes.c_int32),
+                ("max_batch", ctypes.c_int32), ("listen_fd", ctypes.c_int32), ("parent_pid", ctypes.c_int32)]
 
 
 _lib = None
@@ -111,6 +116,7 @@ def load() -> ctypes.CDLL:
         lib.sdsj_engine_set_lanes.argtypes = [vp, ctypes.c_int]
         lib.sdsj_engine_reserve.argtypes = [vp, i64]
         lib.sdsj_plan_need.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(SdsjOp), ctypes.POINTER(i64)]
+        lib.sdsj_service_serve.argtypes = [ctypes.POINTER(SdsjServiceCfg)]
         for name in EXPORTS:
             getattr(lib, name)  # AttributeError if the library lacks a declared symbol
         if lib.sdsj_abi_version() != SDSJ_ABI_VERSION:

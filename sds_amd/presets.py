@@ -26,7 +26,8 @@ import torch
 
 from . import _lib
 from . import functional as F
-from .engine import ImageDecodeError, get_engine, raise_for_status
+from . import service as _service
+from .engine import ImageDecodeError, JpegEngine, get_engine, raise_for_status
 
 log = logging.getLogger("sds_amd")
 _fallback_seen = {"pid": None, "n": 0}
@@ -84,6 +85,23 @@ def _engine_in_worker(device):
             "start (device tensors received from the workers initialise HIP in the parent), or keep the workers on "
             "bytes and decode each collated batch in the main process with sds_amd.batched.GpuDecodeBatch "
             "(INTEGRATION.md §1).") from e
+
+def _service_address(service, device) -> Optional[str]:
+    """The decode-service address a transform's worker processes use (GpuDecodeResizeImageTransform's
+    ``service``).  "auto" starts the service only where a GPU exists; counting devices does not
+    initialise HIP in this process."""
+    if service is None or service is False:
+        return None
+    if isinstance(service, str) and service != "auto":
+        return service
+    if torch.cuda.device_count() == 0:
+        return None
+    d = torch.device(device) if device is not None else None
+    if d is not None and d.type != "cuda":
+        return None
+    idx = d.index if d is not None and d.index is not None else int(os.environ.get("LOCAL_RANK", 0))
+    return _service.ensure_service(idx)
+
 
 SampleData = dict  # sds/structs.py:68
 SampleTransform = Callable[[SampleData], Any]  # sds/structs.py:69
@@ -166,13 +184,19 @@ class GpuDecodeResizeImageTransform(BaseTransform):
     ``output_device`` (extension): None = the tensor stays on the decoding GPU; ``"cpu"`` = it is
     copied back to host memory -- the reference's own output type -- for DataLoaders with
     ``pin_memory=True`` (examples/iter_image_dataset.py:72-80), whose pin step rejects device
-    tensors.  Inside forked DataLoader workers the engine is created per worker; device tensors
-    reach the parent through HIP IPC.
+    tensors.
+
+    ``service`` (extension): ``"auto"`` (default) starts the node-local decode service
+    (sds_amd/service.py) when the transform is built on a machine with a GPU; the transform then
+    decodes in-process in the process that built it, and through the service in every other process --
+    the DataLoader workers -- which get host tensors (the reference's type; pin_memory pins them) and
+    never initialise HIP themselves.  ``None`` = every process creates its own engine (device outputs,
+    reaching the parent through HIP IPC); a string = the address of a running service.
     """
 
     def __init__(self, input_field: str, output_field: Optional[str] = None, resolution=(256, 256),
                  normalize: bool = False, device=None, hflip_prob: float = 0.0, output_device=None,
-                 **resize_kwargs):
+                 service="auto", **resize_kwargs):
         super().__init__(input_field, output_field)
         self.output_device = None if output_device is None else torch.device(output_device)
         self.resolution = tuple(int(v) for v in resolution)
@@ -182,9 +206,14 @@ class GpuDecodeResizeImageTransform(BaseTransform):
         self.hflip_prob = float(hflip_prob)
         self.resize_kwargs = dict(resize_kwargs)
         F.check_resize_kwargs(self.resize_kwargs)
+        self._owner_pid = os.getpid()
+        self.service_address = _service_address(service, device)
 
     def __getstate__(self):
         return dict(self.__dict__)  # no native handle is ever stored on the transform
+
+    def _served(self) -> bool:
+        return self.service_address is not None and os.getpid() != self._owner_pid
 
     def __call__(self, sample: SampleData) -> SampleData:
         _validate_fields(sample, present=[self.input_field], absent=[])
@@ -193,7 +222,7 @@ class GpuDecodeResizeImageTransform(BaseTransform):
             raise TypeError(f"Field '{self.input_field}' must hold encoded image bytes, got {type(data)}")
         data = bytes(data)
         kw = self.resize_kwargs
-        eng = _engine_in_worker(self.device)
+        eng = None if self._served() else _engine_in_worker(self.device)
         need_size = bool(kw.get("allow_vertical")) or kw.get("random_resize") is not None
         resolution = self.resolution
         # taken before target_resolution's np.random.choice, so that a rerun on the host (which draws
@@ -208,18 +237,23 @@ class GpuDecodeResizeImageTransform(BaseTransform):
             resolution = F.target_resolution(int(info.width), int(info.height), self.resolution,
                                              kw.get("allow_vertical", False), kw.get("random_resize"))
         flip = [bool(torch.rand(1) < self.hflip_prob)] if self.hflip_prob > 0.0 else None
-        out, status = eng.decode_resize([data], resolution, crop_before_resize=kw.get("crop_before_resize", True),
-                                        filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),
-                                        normalize=self.normalize, flip=flip, layout="hwc")
-        st = int(status[0])
-        if st == _lib.OK:
+        if eng is None:  # a worker process: through the node-local decode service
+            op = JpegEngine.make_op(resolution, kw.get("crop_before_resize", True),
+                                    F.filter_name(kw.get("interpolation_mode", "bilinear")), self.normalize, "hwc")
+            st, arr = _service.client(self.service_address).decode(data, op, bool(flip and flip[0]))
+            img = torch.from_numpy(arr) if st == _lib.OK else None
+        else:
+            out, status = eng.decode_resize([data], resolution, crop_before_resize=kw.get("crop_before_resize", True),
+                                            filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),
+                                            normalize=self.normalize, flip=flip, layout="hwc")
+            st = int(status[0])
             img = out[0]
-        elif st in (_lib.UNSUPPORTED, _lib.CORRUPT):
+        if st in (_lib.UNSUPPORTED, _lib.CORRUPT):
             # the sample reruns on the reference's own PIL decode (bit-exact by
             # definition); PIL raises for what it cannot decode, as functional.py:100 would
             rng.restore()
             img = self._host(eng, data)
-        else:
+        elif st != _lib.OK:
             raise_for_status(st)
         if self.output_device is not None and self.output_device != img.device:
             img = img.to(self.output_device)
@@ -236,6 +270,16 @@ class GpuDecodeResizeImageTransform(BaseTransform):
         resolution = F.target_resolution(w, h, self.resolution, kw.get("allow_vertical", False),
                                          kw.get("random_resize"))
         flip = [bool(torch.rand(1) < self.hflip_prob)] if self.hflip_prob > 0.0 else None
+        if eng is None:  # through the service's frame path
+            op = JpegEngine.make_op(resolution, kw.get("crop_before_resize", True),
+                                    F.filter_name(kw.get("interpolation_mode", "bilinear")), self.normalize, "hwc")
+            st, arr = _service.client(self.service_address).resize_frame(np.asarray(pil), op, bool(flip and flip[0]))
+            raise_for_status(st)
+            _note_fallback(data, self.input_field)
+            img = torch.from_numpy(arr)
+            if self.output_device is not None and self.output_device != img.device:
+                img = img.to(self.output_device)
+            return img
         frames = _frames_to_device([pil], torch.device("cuda", eng.device))
         out, status = eng.resize_frames(frames, resolution, crop_before_resize=kw.get("crop_before_resize", True),
                                         filter=F.filter_name(kw.get("interpolation_mode", "bilinear")),
@@ -404,13 +448,15 @@ def create_standard_image_pipeline(
     device=None,
     hflip_prob: float = 0.0,
     output_device=None,
+    service="auto",
 ) -> Sequence[SampleTransform]:
-    """presets.py:716-744 with the decode/resize/to-tensor/normalise chain fused on the GPU."""
+    """presets.py:716-744 with the decode/resize/to-tensor/normalise chain fused on the GPU.  ``service``:
+    see GpuDecodeResizeImageTransform (the decode service for DataLoader workers)."""
     transforms: list = [
         LoadFromDiskTransform([image_field]),
         GpuDecodeResizeImageTransform(input_field=image_field, output_field=output_field, resolution=resolution,
                                       normalize=normalize, device=device, hflip_prob=hflip_prob,
-                                      output_device=output_device, **resize_kwargs),
+                                      output_device=output_device, service=service, **resize_kwargs),
     ]
     if return_image_as_single_frame_video:
         transforms.extend([

@@ -32,7 +32,103 @@ class FolderDataset(IterableDataset):
             yield s
 
 
+def run_service_case(case: str) -> dict:
+    """Cases of the node-local decode service (sds_amd/service.py): the pipeline's default service="auto"."""
+    import numpy as np
+
+    from sds_amd.presets import create_standard_image_pipeline
+    from tests import goldens as G
+    rec = {"case": case}
+    d = tempfile.mkdtemp()
+    try:
+        if case in ("service_reference_shape", "service_parent_touched_gpu"):
+            meta, jpgs = G.g2_jpegs()
+            paths = []
+            for i, j in enumerate(jpgs):
+                p = os.path.join(d, f"{i}.jpg")
+                with open(p, "wb") as f:
+                    f.write(j)
+                paths.append(p)
+            ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda")
+            rec["service"] = ts[1].service_address is not None
+            if case == "service_parent_touched_gpu":
+                torch.zeros(1, device="cuda")  # HIP initialised in the parent before the workers fork
+            # examples/iter_image_dataset.py:72-80's DataLoader arguments: fork, 2 workers, pin_memory=True
+            dl = DataLoader(FolderDataset(paths, ts), batch_size=4, num_workers=2, pin_memory=True, drop_last=True)
+            got = {}
+            for b in dl:
+                rec["device"] = str(b["image"].device)
+                rec["pinned"] = bool(b["image"].is_pinned())
+                rec["stride"] = list(b["image"].stride())
+                for i, im in zip(b["index"].tolist(), b["image"]):
+                    got[i] = G.sha(im.contiguous().numpy())
+            rec["n"] = len(got)
+            rec["equal_to_goldens"] = len(got) == len(jpgs) and all(
+                got[i] == meta["images"][i]["u8_256_sha256"] for i in range(len(jpgs)))
+        elif case == "service_g3_flip_normalize":
+            meta, jpgs = G.g3_jpegs()
+            paths = []
+            for i, j in enumerate(jpgs):
+                p = os.path.join(d, f"{i}.jpg")
+                with open(p, "wb") as f:
+                    f.write(j)
+                paths.append(p)
+            ok = True
+            for flip in (False, True):
+                for norm in (False, True):
+                    ts = create_standard_image_pipeline("jpg", (512, 512), normalize=norm, device="cuda",
+                                                        hflip_prob=1.0 if flip else 0.0)
+                    sel = [i for i, im in enumerate(meta["images"]) if im["flip"] == flip]
+                    dl = DataLoader(FolderDataset([paths[i] for i in sel], ts), batch_size=None, num_workers=3)
+                    for k, s in enumerate(dl):
+                        im = meta["images"][sel[s["index"]]]
+                        key = "f32_512_sha256" if norm else "u8_512_sha256"
+                        ok &= s["image"].device.type == "cpu" and G.sha(s["image"].contiguous().numpy()) == im[key]
+            rec["equal_to_goldens"] = bool(ok)
+        elif case == "service_fallback_g6":
+            meta = G.load_json("g6_fallback.json")
+            z = np.load(os.path.join(G.GOLDEN, "g6_fallback.npz"))
+            ok, n = True, 0
+            for vname, res, kw in meta["variants"]:
+                paths, refs = [], []
+                for c in meta["cases"]:
+                    p = os.path.join(d, c["name"])
+                    with open(p, "wb") as f:
+                        f.write(z[f"{c['name']}__bytes"].tobytes())
+                    paths.append(p)
+                    refs.append(c["variants"][vname])
+                ts = create_standard_image_pipeline("img", tuple(res), device="cuda", **kw)
+
+                class _One(IterableDataset):
+                    def __iter__(self):
+                        wi = get_worker_info()
+                        for i in range(wi.id, len(paths), wi.num_workers):
+                            s = {"img": paths[i]}
+                            try:
+                                for t in ts:
+                                    s = t(s)
+                                yield {"i": i, "ok": True, "img": s["image"]}
+                            except OSError:
+                                yield {"i": i, "ok": False, "img": torch.zeros(1)}
+                for s in DataLoader(_One(), batch_size=None, num_workers=2):
+                    ref = refs[s["i"]]
+                    ok &= bool(s["ok"]) == ref["ok"]
+                    if ref["ok"]:
+                        ok &= list(s["img"].shape) == ref["shape"] and G.sha(s["img"].contiguous().numpy()) == ref["sha256"]
+                    n += 1
+            rec["n"] = n
+            rec["equal_to_goldens"] = bool(ok)
+        else:
+            raise SystemExit(f"unknown case {case}")
+    except Exception as e:  # noqa: BLE001  (the test inspects the error)
+        rec["error_type"] = type(e).__name__
+        rec["error"] = str(e)[-3000:]
+    return rec
+
+
 def run(case: str) -> dict:
+    if case.startswith("service_"):
+        return run_service_case(case)
     from sds_amd.presets import create_standard_image_pipeline
     from tests import goldens as G
     meta, jpgs = G.g2_jpegs()
@@ -43,7 +139,8 @@ def run(case: str) -> dict:
         with open(p, "wb") as f:
             f.write(j)
         paths.append(p)
-    kw, dl_kw = {}, {"num_workers": 2, "pin_memory": False}
+    # per-worker engines (service=None): each worker initialises HIP itself
+    kw, dl_kw = {"service": None}, {"num_workers": 2, "pin_memory": False}
     epochs = 1
     if case == "workers_device":
         pass

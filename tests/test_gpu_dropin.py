@@ -258,10 +258,40 @@ def test_dataloader_refork_after_device_tensors_fails_with_a_clear_error():
     assert "persistent" in rec.get("error", "") or "GpuDecodeBatch" in rec.get("error", ""), rec
 
 
-def test_dataloader_reference_shape_fails_with_a_clear_error():
-    """examples/iter_image_dataset.py:72-80 exactly (fork, num_workers=2, pin_memory=True): the
-    DataLoader queries the GPU in the parent before forking (pin_memory needs it), so a worker cannot
-    initialise HIP; the transform says so and names the working set-ups."""
+def test_dataloader_reference_shape_through_the_decode_service():
+    """examples/iter_image_dataset.py:72-80's DataLoader arguments unchanged (fork, num_workers=2,
+    pin_memory=True) over the default pipeline: the workers decode through the node-local service
+    (sds_amd/service.py) and yield pinned host tensors -- the reference's type -- equal to G2."""
+    rec = _case("service_reference_shape")
+    assert "error" not in rec, rec
+    assert rec["service"] and rec["device"] == "cpu" and rec["pinned"] and rec["n"] == 8, rec
+    assert rec["stride"] == [3 * 256 * 256, 256 * 256, 256, 1] and rec["equal_to_goldens"], rec  # (collated)
+
+
+def test_decode_service_after_parent_gpu_init():
+    """The parent initialises HIP after building the pipeline and before its workers fork: the workers
+    never touch HIP (the service decodes), so the fork is harmless."""
+    rec = _case("service_parent_touched_gpu")
+    assert "error" not in rec, rec
+    assert rec["pinned"] and rec["equal_to_goldens"], rec
+
+
+def test_decode_service_g3_mixed_sizes_flip_normalize():
+    rec = _case("service_g3_flip_normalize")
+    assert "error" not in rec and rec["equal_to_goldens"], rec
+
+
+def test_decode_service_fallback_formats_match_g6():
+    """PNG / WebP / GIF / BMP / TIFF / CMYK / no-EOI samples in service workers: PIL decodes them in the
+    worker, the service resizes the frame (SDSJ_SVC_FRAME); outputs and OSErrors equal G6."""
+    rec = _case("service_fallback_g6")
+    assert "error" not in rec and rec["equal_to_goldens"] and rec["n"] >= 40, rec
+
+
+def test_dataloader_reference_shape_without_service_fails_with_a_clear_error():
+    """service=None (every worker its own engine) in the reference's shape (fork, pin_memory=True): the
+    DataLoader queries the GPU in the parent before forking, so a worker cannot initialise HIP; the
+    transform says so and names the working set-ups."""
     rec = _case("workers_pinned_fork")
     assert "GpuDecodeBatch" in rec.get("error", "") and "pin_memory=True" in rec["error"], rec
 

@@ -1,7 +1,8 @@
 """Rate of the per-sample drop-in (create_standard_image_pipeline(..., device="cuda")) in the reference's
 loader shapes: the transform list applied sample by sample (sds/dataset.py:535-561) in the main
-process, and inside DataLoader workers (examples/iter_image_dataset.py:72-80: batch 4 here,
-num_workers 2 / 4 / 8, device outputs with pin_memory=False, host outputs with pin_memory=True).
+process, and inside DataLoader workers (examples/iter_image_dataset.py:72-80: batch 4 here, fork,
+pin_memory=True) -- through the node-local decode service (the default, host outputs), or with an engine
+per worker (service=None, device outputs with pin_memory=False).
 Inputs: a folder of synthetic 640x480 q90 JPEGs (configs[0] shape) -> 256x256 uint8.
 
 Run in a fresh process (the parent must not touch the GPU before the workers fork):
@@ -21,15 +22,19 @@ from torch.utils.data import DataLoader  # noqa: E402
 
 
 MODES = {
-    # name: (num_workers, pin_memory, multiprocessing_context, output_device)
-    "dataloader_fork_workers2_device_out": (2, False, None, None),
-    "dataloader_fork_workers4_device_out": (4, False, None, None),
-    "dataloader_fork_workers8_device_out": (8, False, None, None),
-    "dataloader_spawn_workers4_pinned_cpu_out": (4, True, "spawn", "cpu"),
-    "main_process_per_sample": (0, False, None, None),
+    # name: (num_workers, pin_memory, multiprocessing_context, output_device, service)
+    # the node-local decode service (the pipeline's default): the reference's loader shape unchanged
+    "service_fork_workers2_pinned": (2, True, None, None, "auto"),
+    "service_fork_workers4_pinned": (4, True, None, None, "auto"),
+    "service_fork_workers8_pinned": (8, True, None, None, "auto"),
+    "service_fork_workers16_pinned": (16, True, None, None, "auto"),
+    # per-worker engines (service=None)
+    "dataloader_fork_workers2_device_out": (2, False, None, None, None),
+    "dataloader_fork_workers8_device_out": (8, False, None, None, None),
+    "main_process_per_sample": (0, False, None, None, None),
     # the workers decode on the GPU but hand back only a tiny host tensor: the rate without the
     # device-tensor IPC (CUDA IPC handles opened by the parent per batch)
-    "dataloader_fork_workers8_decode_only": (8, False, None, "discard"),
+    "dataloader_fork_workers8_decode_only": (8, False, None, "discard", None),
 }
 
 
@@ -47,7 +52,7 @@ def run_mode(mode, n_files, seconds):
     from sds_amd.presets import create_standard_image_pipeline
     from tests.golden.synth import synth_jpegs
     from tests.loader_cases import FolderDataset
-    nw, pin, ctx, odev = MODES[mode]
+    nw, pin, ctx, odev, service = MODES[mode]
     jpgs = synth_jpegs(64, seed=2024)
     d = tempfile.mkdtemp()
     paths = []
@@ -57,14 +62,15 @@ def run_mode(mode, n_files, seconds):
             f.write(jpgs[i % len(jpgs)])
         paths.append(p)
     discard = odev == "discard"
-    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device=None if discard else odev)
+    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device=None if discard else odev,
+                                        service=service)
     ds = FolderDataset(paths, ts)
     if discard:
         ds = _Discard(ds)
     if nw:
         # persistent workers: forked once, before the parent receives its first device tensor
         src = DataLoader(ds, batch_size=4, num_workers=nw, pin_memory=pin, multiprocessing_context=ctx,
-                         persistent_workers=True)
+                         persistent_workers=True, prefetch_factor=4)
     else:
         src = ds
     n, t0, first = 0, time.perf_counter(), None
@@ -82,7 +88,8 @@ def run_mode(mode, n_files, seconds):
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     print(json.dumps({"mode": mode, "images_per_s": round(n / dt, 1), "images": n, "seconds": round(dt, 2),
-                      "num_workers": nw, "pin_memory": pin, "context": ctx or "fork", "output_device": odev or "cuda",
+                      "num_workers": nw, "pin_memory": pin, "context": ctx or "fork",
+                      "output_device": "cpu" if service else (odev or "cuda"), "service": bool(service),
                       "first_batch": first}), flush=True)
 
 
