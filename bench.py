@@ -9,10 +9,11 @@ by the C-ABI engine.  One step = one batch of ``--batch`` rows.
 
 Multi-GPU (configs[3]): one process per GPU.  ``--gpus N`` outside torchrun starts N fresh child
 processes (before anything touches the GPU here), each with RANK / WORLD_SIZE / LOCAL_RANK set;
-under torchrun the ranks come from its environment.  Rank r owns rows [r*N_r, (r+1)*N_r) of an
-R*N_r-row index (sds/index.py:227-246 INTER_NODE slicing), no collective on the data path
-("scaling": "weak"); the process group (RCCL) only carries the barriers and the max-over-ranks of
-the timed region.
+under torchrun the ranks come from its environment.  The index is a 1,000,000-row synthetic parquet
+file (100,000 rows on one GPU, configs[1]); rank r reads and owns rows [r*N/R, (r+1)*N/R)
+(sds/index.py:208-246 load_index_partition / compute_index_slice, INTER_NODE), no collective on the
+data path ("scaling": "weak": the batch per GPU is fixed); the process group (RCCL) only carries the
+barriers, the index slices and the max-over-ranks of the timed region.
 
 ``--workload mixed512`` is configs[2] (mixed VGA..4K -> 512 + hflip + float32 normalise, device-
 resident); ``--workload e2e512`` is configs[4]: each rank's rows as JPEG files in a local cache
@@ -300,7 +301,10 @@ def main():
                     help="vga256 = configs[1] (the headline metric); mixed512 = configs[2]: VGA..4K -> centre crop + "
                          "resize 512 + hflip(p=0.5) + CHW float normalise")
     ap.add_argument("--batch", type=int, default=None)
-    ap.add_argument("--rows", type=int, default=None, help="rows resident per GPU")
+    ap.add_argument("--rows", type=int, default=None, help="rows resident per GPU (sets --index-rows to rows x GPUs)")
+    ap.add_argument("--index-rows", type=int, default=None,
+                    help="rows of the synthetic parquet index the ranks slice (default: 100,000 on one GPU -- "
+                         "configs[1] -- and 1,000,000 on several -- configs[3])")
     ap.add_argument("--pool", type=int, default=None, help="distinct encoded images")
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
@@ -318,7 +322,7 @@ def main():
     # at 16384; configs[2]: 45.0k at 512, 59.8k at 2048 -- DESIGN.md §5)
     defaults = {"batch": 2048, "rows": 16384, "pool": 96, "res": 512} if mixed else \
         {"batch": 1024, "rows": 16384, "pool": 256, "res": 512} if e2e else \
-        {"batch": 16384, "rows": 100_000, "pool": 1024, "res": 256}
+        {"batch": 16384, "rows": None, "pool": 1024, "res": 256}
     for k, v in defaults.items():
         if getattr(args, k) is None:
             setattr(args, k, v)
@@ -354,15 +358,47 @@ def main():
 
     from sds_amd.distributed import compute_index_slice, max_over_ranks
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
     workers = max(1, cpu_share()[0] // max(1, world))
     pool = make_pool(args.pool, workers, _make_mixed_image if mixed else _make_pool_image)
 
-    # this rank's slice of the R*N-row index: row i holds pool image i % POOL.  The slice is laid
-    # out as a repeated template of one pool period (16-byte aligned rows), tiled on the device, so
-    # every row is its own copy in HBM.
-    total_rows = args.rows * world
-    r0, r1, _ = compute_index_slice(total_rows, rank, world)
+    # The sample index: a synthetic parquet file (sds's index layout, sds_amd/index.py) of
+    # total_rows rows, row i referring to pool image i % POOL, written once by rank 0; each rank reads
+    # its compute_index_slice rows from it (sds/index.py:208-246 load_index_partition) and checks them.
+    # The rank's rows are laid out as a repeated template of one pool period (16-byte aligned rows),
+    # tiled on the device, so every row is its own copy in HBM.
+    if args.index_rows is None:
+        args.index_rows = args.rows * world if args.rows else (1_000_000 if world > 1 else 100_000)
+    total_rows = args.index_rows
+    index_path = None
+    try:
+        import pyarrow  # noqa: F401
+        index_path = os.path.join(tempfile.gettempdir(), f"sdsj_index_{os.environ.get('MASTER_PORT', os.getpid())}_"
+                                                         f"{total_rows}_{args.pool}.parquet")
+    except ImportError:
+        pass
+    if index_path:
+        from sds_amd.index import load_index_partition, write_synthetic_index
+        if rank == 0:
+            write_synthetic_index(index_path + ".tmp", total_rows, args.pool)
+            os.replace(index_path + ".tmp", index_path)
+        barrier()
+        r0, r1, rows_tab = load_index_partition(index_path, total_rows, rank, world, columns=["index", "pool_image"])
+        ids = rows_tab.column("index").to_numpy()
+        if not (np.array_equal(ids, np.arange(r0, r1)) and
+                np.array_equal(rows_tab.column("pool_image").to_numpy(), ids % args.pool)):
+            raise SystemExit(f"rank {rank}: the parquet index slice [{r0}, {r1}) does not hold the expected rows")
+        del rows_tab, ids
+    else:
+        r0, r1, _ = compute_index_slice(total_rows, rank, world)
     nrows = r1 - r0
+    slices = [[r0, r1]]
+    if world > 1:
+        slices = [None] * world
+        dist.all_gather_object(slices, [r0, r1])
     period = [(r0 + k) % args.pool for k in range(min(args.pool, nrows))]
     t_lens = np.array([len(pool[p]) for p in period], np.int64)
     t_aligned = (t_lens + 15) // 16 * 16
@@ -372,13 +408,12 @@ def main():
     template = np.zeros(T, np.uint8)
     for k, p in enumerate(period):
         template[t_offs[k]:t_offs[k] + t_lens[k]] = np.frombuffer(pool[p], np.uint8)
-    reps = (nrows + len(period) - 1) // len(period)
+    # (the CPU stand-in engine reads nothing: its rows share one copy of the template)
+    reps = 1 if stub else (nrows + len(period) - 1) // len(period)
     d_tmpl = torch.from_numpy(template).to(dev)
-    blob = torch.empty(reps * T, dtype=torch.uint8, device=dev)
-    for r in range(reps):
-        blob[r * T:(r + 1) * T].copy_(d_tmpl)
+    blob = d_tmpl.repeat(reps)
     j = np.arange(nrows)
-    offs = (j // len(period)) * T + t_offs[j % len(period)]
+    offs = (j // len(period)) % reps * T + t_offs[j % len(period)]
     lens = t_lens[j % len(period)]
     d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_lens = torch.from_numpy(lens.astype(np.int32)).to(dev)
@@ -464,10 +499,6 @@ def main():
         raise SystemExit(f"rank {rank}: {n_bad} samples failed to decode")
     for _ in range(args.warmup):
         step()
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
 
     barrier()
     sync()
@@ -593,7 +624,8 @@ def main():
                     f"pinned host memory (two slots in flight)"
                     if e2e else
                     ("configs[3]: " if world > 1 else "configs[1]: ") +
-                    "synthetic 640x480 q90 4:2:0 baseline JPEGs resident in HBM -> "
+                    f"{total_rows:,}-row {'parquet' if index_path else 'in-memory'} index, one compute_index_slice "
+                    f"slice per GPU; synthetic 640x480 q90 4:2:0 baseline JPEGs resident in HBM -> "
                     f"centre crop + bilinear resize {args.res}x{args.res} uint8 CHW")
         line = {
             "metric": ("images/s device-resident JPEG decode+crop+resize@512+hflip+normalise (mixed VGA..4K)" if mixed
@@ -605,7 +637,11 @@ def main():
             "config": {"workload": workload,
                        "rows_per_gpu": nrows, "distinct_images": args.pool, "global_batch": B * world,
                        "batch_per_gpu": B, "mean_jpeg_bytes": round(mean_in, 1),
-                       "parallelism": f"index-sharded x{world}, no collective on the data path"},
+                       "parallelism": f"index-sharded x{world}, no collective on the data path",
+                       "index": {"rows": total_rows,
+                                 "source": "synthetic parquet read with pyarrow (sds_amd/index.py)" if index_path else
+                                           "in-memory index (pyarrow not importable)",
+                                 "slices": slices}},
             "per_rank_images_per_s": [round(B * args.steps / t, 1) for t in per_rank],
             "process_group": {"backend": args.backend if world > 1 else None, "world_size": world_seen,
                               "gpus_visible": ndev if not stub else 0},
@@ -633,6 +669,11 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if index_path and rank == 0:
+        try:
+            os.remove(index_path)
+        except OSError:
+            pass
 
 
 if __name__ == "__main__":

@@ -28,6 +28,9 @@ def test_two_rank_launch_reports_the_whole_job():
     assert line["process_group"] == {"backend": "gloo", "world_size": 2, "gpus_visible": 0}
     assert len(line["per_rank_images_per_s"]) == 2
     assert line["config"]["global_batch"] == 32 and line["config"]["rows_per_gpu"] == 64
+    # the parquet index the ranks sliced (sds/index.py:208-246): 2 x 64 rows, one contiguous slice each
+    assert line["config"]["index"]["rows"] == 128 and "parquet" in line["config"]["index"]["source"]
+    assert line["config"]["index"]["slices"] == [[0, 64], [64, 128]]
     # value = all ranks' images over the slowest rank's time
     slowest = min(line["per_rank_images_per_s"])
     assert abs(line["value"] - 2 * slowest) <= 0.01 * line["value"] + 1
@@ -37,3 +40,18 @@ def test_one_gpu_run_is_unchanged():
     line = _run(1)
     assert line["n_gpus"] == 1 and line["process_group"]["world_size"] == 1
     assert len(line["per_rank_images_per_s"]) == 1
+    assert line["config"]["index"]["slices"] == [[0, 64]]
+
+
+def test_default_index_is_a_million_rows_on_several_gpus():
+    """configs[3]: without --rows, --gpus N slices a 1,000,000-row parquet index (125,000 rows per rank at 8)."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--engine", "stub", "--backend",
+           "gloo", "--pool", "4", "--batch", "16", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+           "--roofline-steps", "1"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert line["config"]["index"]["rows"] == 1_000_000 and line["config"]["rows_per_gpu"] == 500_000
+    assert line["config"]["index"]["slices"] == [[0, 500_000], [500_000, 1_000_000]]
+    assert line["config"]["workload"].startswith("configs[3]: 1,000,000-row parquet index")

@@ -35,6 +35,9 @@ def test_bench_two_ranks_index_sharded_on_hip():
     assert d["process_group"]["backend"] == "gloo"
     assert d["config"]["workload"].startswith("configs[3]")
     assert d["config"]["global_batch"] == 2048 and d["config"]["rows_per_gpu"] == 4096
+    # each rank read its compute_index_slice rows (sds/index.py:235-246) from the parquet index
+    assert d["config"]["index"]["rows"] == 8192 and "parquet" in d["config"]["index"]["source"]
+    assert d["config"]["index"]["slices"] == [[0, 4096], [4096, 8192]]
     assert len(d["per_rank_images_per_s"]) == 2 and all(v > 0 for v in d["per_rank_images_per_s"])
     assert d["pixel_check"]["equal_to_pil"] and d["pixel_check"]["golden_sha256_match"]
     assert d["value"] > 0
