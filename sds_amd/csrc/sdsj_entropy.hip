@@ -375,11 +375,20 @@ __device__ __forceinline__ void bits_init(BitsQ<Q>& b, const uint32_t* src, uint
 }
 
 // Wave-synchronous refill: re-reads kQ words from wi (the ustream carries kUPad bytes of slack).
+#ifndef SDSJ_PARTIAL_REFILL
+#define SDSJ_PARTIAL_REFILL 0
+#endif
 template <int Q>
 __device__ __forceinline__ void bits_fill(BitsQ<Q>& b) {
   if ((b.wi + Q) * 32u <= b.lim) {  // the common case: all kQ words lie before the limit
 #pragma unroll
-    for (int k = 0; k < Q; k++) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+    for (int k = 0; k < Q; k++) {
+      if (SDSJ_PARTIAL_REFILL) {  // only the words not queued yet (q[0 .. nq) hold words wi .. wi + nq)
+        if (k >= b.nq) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+      } else {
+        b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+      }
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < Q; k++) b.q[k] = load_word(b.src, b.wi + k, b.lim);
