@@ -105,3 +105,33 @@ def test_pipeline_starts_no_service_without_a_gpu():
     from sds_amd.presets import create_standard_image_pipeline
     ts = create_standard_image_pipeline("jpg", (256, 256))
     assert ts[1].service_address is None and not S._handles
+
+
+def test_service_process_lifecycle_without_a_gpu():
+    """The launcher (sds_amd.service.ensure_service): the service process binds its address before
+    initialising anything (a client can connect at once), exits on SIGTERM while idle, and -- once a
+    client connects -- initialises HIP in its own process; without a GPU the native loop reports the
+    error and the process exits non-zero instead of hanging."""
+    import time
+    import torch
+    if torch.cuda.device_count():
+        pytest.skip("GPU present")
+    addr = S.ensure_service(0)
+    h = S._handles[(os.getpid(), 0)]
+    assert S.ensure_service(0) == addr  # one service per (process, device)
+    deadline = time.time() + 60
+    sock = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
+    while True:
+        try:
+            sock.connect(b"\0" + addr.encode())
+            break
+        except (ConnectionRefusedError, FileNotFoundError):
+            assert time.time() < deadline, "service never listened"
+            time.sleep(0.05)
+    assert h.proc.wait(timeout=120) != 0  # no GPU: sdsj_service_serve fails, the process exits
+    sock.close()
+    del S._handles[(os.getpid(), 0)]
+    h2 = S._Handle(0, 1, 8)  # idle (no client): SIGTERM ends it
+    time.sleep(0.5)
+    h2.stop()
+    assert h2.proc.returncode is not None
