@@ -5,17 +5,21 @@
 // sample at a time.  A worker forked after its parent initialised HIP cannot use the GPU itself, and one
 // image per engine call cannot fill the chip.  This service is the one process per GPU that decodes for
 // all of them: the worker-side transform (sds_amd/service.py) puts the encoded bytes into its shared
-// region and sends a request; the loop here gathers the requests of every worker into batches, runs up
-// to `engines` batches at once (one engine, stream and scratch each; a batch is whatever arrived while
-// the previous ones ran), and copies each output into its worker's region before replying.
+// region and sends a request; the service gathers the requests of every worker into batches, runs up to
+// `engines` batches at once (one engine, stream and scratch each; a batch is whatever arrived while the
+// previous ones ran), and copies each output into its worker's region before replying.
 //
-// One thread: epoll over the listening socket and the clients, completion by polling the engines'
-// events (a finished batch is answered at once; an idle loop blocks in epoll).
+// Threads: the caller's thread reads requests (epoll over the listening socket and the clients) into
+// one queue; one thread per engine takes a batch from it, submits it, waits for it (hipEventSynchronize)
+// and answers its requests.  (A single thread polling every engine's event measured no overlap between
+// the engines' batches: 2 clients got the rate of 1.)
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <pthread.h>
 #include <signal.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/epoll.h>
 #include <sys/mman.h>
@@ -24,9 +28,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "sdsj.h"
@@ -45,12 +54,51 @@ int64_t out_bytes(const sdsj_op& op) {
 
 bool same_op(const sdsj_op& a, const sdsj_op& b) { return memcmp(&a, &b, sizeof(sdsj_op)) == 0; }
 
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void log_err(const char* what, const char* detail) { fprintf(stderr, "sdsj_service: %s: %s\n", what, detail); }
+
+// A worker's connection and its shared region.  The region stays mapped while requests of the client
+// are queued or in a batch (inflight), even after the client went away (closed).
 struct Client {
   int fd = -1;
-  uint8_t* base = nullptr;  // the worker's region (MAP_SHARED memfd)
+  uint8_t* base = nullptr;  // MAP_SHARED memfd
   size_t size = 0;
-  int inflight = 0;  // requests queued or in a batch (the region stays mapped until they are done)
-  bool closed = false;
+  std::atomic<int> inflight{0};
+  std::atomic<bool> closed{false};
+  std::mutex mu;  // base / size / unmap
+
+  void reply(uint64_t seq, int status) {
+    if (closed.load()) return;
+    sdsj_svc_rep rep{seq, status, 0};
+    for (;;) {  // (SOCK_SEQPACKET: a packet is sent whole; concurrent senders do not interleave)
+      const ssize_t w = send(fd, &rep, sizeof(rep), MSG_NOSIGNAL);
+      if (w == (ssize_t)sizeof(rep)) return;
+      if (w < 0 && errno == EINTR) continue;
+      closed.store(true);  // the worker went away: its later requests are dropped
+      return;
+    }
+  }
+  bool region_ok(int64_t off, int64_t len) const {
+    return base && off >= 0 && len >= 0 && (uint64_t)off + (uint64_t)len <= size;
+  }
+  // The last reference of a client that went away unmaps its region and closes its socket (not
+  // earlier: a lane thread may still reply on it, and a closed descriptor number can be reused).
+  void finalize_locked() {
+    if (!closed.load() || inflight.load() != 0) return;
+    if (base) munmap(base, size);
+    base = nullptr;
+    if (fd >= 0) close(fd);
+    fd = -1;
+  }
+  void release() {
+    if (--inflight == 0 && closed.load()) {
+      std::lock_guard<std::mutex> g(mu);
+      finalize_locked();
+    }
+  }
 };
 
 struct Req {
@@ -58,42 +106,12 @@ struct Req {
   sdsj_svc_req r;
 };
 
-struct Lane {  // one engine, its stream, and the batch it runs
-  sdsj_engine* e = nullptr;
-  hipStream_t s = nullptr;
-  hipEvent_t done = nullptr;
-  uint8_t* d_out = nullptr;
-  uint8_t* h_out = nullptr;  // pinned
-  size_t out_cap = 0;
-  std::vector<Req> batch;
-  std::vector<int32_t> status;
-  int64_t ob = 0;
-  bool busy = false;
-};
-
-void log_err(const char* what, const char* detail) { fprintf(stderr, "sdsj_service: %s: %s\n", what, detail); }
-
-void reply(Client& c, uint64_t seq, int status) {
-  if (c.closed) return;
-  sdsj_svc_rep rep{seq, status, 0};
-  for (;;) {
-    const ssize_t w = send(c.fd, &rep, sizeof(rep), MSG_NOSIGNAL);
-    if (w == (ssize_t)sizeof(rep)) return;
-    if (w < 0 && errno == EINTR) continue;
-    c.closed = true;  // the worker went away: its later requests are dropped
-    return;
-  }
-}
-
-bool region_ok(const Client& c, int64_t off, int64_t len) {
-  return c.base && off >= 0 && len >= 0 && (uint64_t)off + (uint64_t)len <= c.size;
-}
-
 class Service {
  public:
   explicit Service(const sdsj_service_cfg& cfg) : cfg_(cfg) {}
 
   int run() {
+    trace_ = getenv("SDSJ_SERVICE_TRACE") != nullptr;
     if (hipSetDevice(cfg_.device) != hipSuccess) return fail("hipSetDevice", SDSJ_EHIP);
     const int nl = cfg_.engines > 0 ? cfg_.engines : 4;
     max_batch_ = cfg_.max_batch > 0 ? cfg_.max_batch : 64;
@@ -111,40 +129,54 @@ class Service {
     ev.events = EPOLLIN;
     ev.data.fd = cfg_.listen_fd;
     if (epoll_ctl(ep_, EPOLL_CTL_ADD, cfg_.listen_fd, &ev) != 0) return fail("epoll_ctl(listen)", SDSJ_EINVAL);
+    // engine threads with SIGTERM / SIGINT blocked: the signals reach this thread's epoll_wait
+    sigset_t block, old;
+    sigemptyset(&block);
+    sigaddset(&block, SIGTERM);
+    sigaddset(&block, SIGINT);
+    pthread_sigmask(SIG_BLOCK, &block, &old);
+    for (int k = 0; k < nl; k++) threads_.emplace_back([this, k] { lane_loop(lanes_[k]); });
+    pthread_sigmask(SIG_SETMASK, &old, nullptr);
     int rc = SDSJ_OK;
     while (!g_stop) {
       if (cfg_.parent_pid > 0 && getppid() != cfg_.parent_pid) break;
-      const bool busy = std::any_of(lanes_.begin(), lanes_.end(), [](const Lane& l) { return l.busy; });
       epoll_event evs[64];
-      const int n = epoll_wait(ep_, evs, 64, busy || !pending_.empty() ? 0 : 500);
+      const int n = epoll_wait(ep_, evs, 64, 500);
       if (n < 0 && errno != EINTR) {
-        rc = fail("epoll_wait", SDSJ_EINVAL);
+        rc = SDSJ_EINVAL;
+        log_err("epoll_wait", strerror(errno));
         break;
       }
       for (int i = 0; i < n; i++) {
         if (evs[i].data.fd == cfg_.listen_fd) accept_clients();
         else read_client(evs[i].data.fd);
       }
-      for (auto& l : lanes_)
-        if (l.busy && hipEventQuery(l.done) == hipSuccess) complete(l);
-      for (auto& l : lanes_) {
-        if (pending_.empty()) break;
-        if (!l.busy && (rc = submit(l)) != SDSJ_OK) break;
-      }
-      if (rc != SDSJ_OK) break;
-      if (busy && n == 0) sched_yield();
     }
-    for (auto& l : lanes_) {  // drain before the engines go
-      if (l.busy) {
-        (void)hipEventSynchronize(l.done);
-        complete(l);
-      }
+    {
+      std::lock_guard<std::mutex> g(qmu_);
+      stopping_ = true;
     }
+    qcv_.notify_all();
+    for (auto& t : threads_) t.join();  // each finishes (and answers) the batch it holds
     shutdown();
     return rc;
   }
 
  private:
+  struct Lane {  // one engine, its stream, and the batch it runs
+    sdsj_engine* e = nullptr;
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t* d_out = nullptr;
+    uint8_t* h_out = nullptr;  // pinned
+    size_t out_cap = 0;
+    std::vector<Req> batch;
+    std::vector<int32_t> status;
+    // frame path buffers (grow only)
+    uint8_t *fr_in = nullptr, *fr_out = nullptr, *fr_small = nullptr;
+    size_t fr_in_cap = 0, fr_out_cap = 0;
+  };
+
   int fail(const char* what, int code) {
     log_err(what, strerror(errno));
     shutdown();
@@ -160,25 +192,18 @@ class Service {
       if (l.done) (void)hipEventDestroy(l.done);
       (void)hipFree(l.d_out);
       (void)hipHostFree(l.h_out);
+      (void)hipFree(l.fr_in), (void)hipFree(l.fr_out), (void)hipFree(l.fr_small);
       l = Lane();
     }
-    (void)hipFree(fr_in_), (void)hipFree(fr_out_), (void)hipFree(fr_small_);
-    fr_in_ = fr_out_ = fr_small_ = nullptr;
     if (ep_ >= 0) close(ep_);
     ep_ = -1;
   }
 
   void drop(Client& c) {
-    if (c.fd >= 0) {
-      (void)epoll_ctl(ep_, EPOLL_CTL_DEL, c.fd, nullptr);
-      close(c.fd);
-    }
-    c.fd = -1;
-    c.closed = true;
-    if (c.inflight == 0 && c.base) {
-      munmap(c.base, c.size);
-      c.base = nullptr;
-    }
+    std::lock_guard<std::mutex> g(c.mu);
+    if (c.fd >= 0) (void)epoll_ctl(ep_, EPOLL_CTL_DEL, c.fd, nullptr);
+    c.closed.store(true);
+    c.finalize_locked();
   }
 
   void accept_clients() {
@@ -202,6 +227,7 @@ class Service {
     auto it = clients_.find(fd);
     if (it == clients_.end()) return;
     std::shared_ptr<Client> c = it->second;
+    int queued = 0;
     for (;;) {
       sdsj_svc_req r;
       char cbuf[CMSG_SPACE(sizeof(int))];
@@ -212,7 +238,7 @@ class Service {
       mh.msg_control = cbuf;
       mh.msg_controllen = sizeof(cbuf);
       const ssize_t got = recvmsg(fd, &mh, MSG_CMSG_CLOEXEC);
-      if (got < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return;
+      if (got < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
       if (got < 0 && errno == EINTR) continue;
       int passed = -1;
       for (cmsghdr* cm = CMSG_FIRSTHDR(&mh); cm; cm = CMSG_NXTHDR(&mh, cm))
@@ -221,11 +247,12 @@ class Service {
         if (passed >= 0) close(passed);
         clients_.erase(fd);
         drop(*c);
-        return;
+        break;
       }
       if (r.kind == SDSJ_SVC_MAP) {
         int st = SDSJ_EINVAL;
-        if (passed >= 0 && r.in_len > 0 && c->inflight == 0) {
+        if (passed >= 0 && r.in_len > 0 && c->inflight.load() == 0) {  // (a client maps between requests)
+          std::lock_guard<std::mutex> g(c->mu);
           if (c->base) munmap(c->base, c->size);
           c->base = nullptr;
           void* p = mmap(nullptr, (size_t)r.in_len, PROT_READ | PROT_WRITE, MAP_SHARED, passed, 0);
@@ -236,48 +263,79 @@ class Service {
           }
         }
         if (passed >= 0) close(passed);
-        reply(*c, r.seq, st);
-      } else if (r.kind == SDSJ_SVC_DECODE) {
-        if (!region_ok(*c, 0, r.in_len) || !region_ok(*c, r.out_off, out_bytes(r.op)) || r.op.out_h <= 0 || r.op.out_w <= 0) {
-          reply(*c, r.seq, SDSJ_EINVAL);
+        c->reply(r.seq, st);
+      } else if (r.kind == SDSJ_SVC_DECODE || r.kind == SDSJ_SVC_FRAME) {
+        const bool frame = r.kind == SDSJ_SVC_FRAME;
+        const int64_t in = frame ? (int64_t)r.width * r.height * 3 : r.in_len;
+        if (!c->region_ok(0, in) || !c->region_ok(r.out_off, out_bytes(r.op)) || r.op.out_h <= 0 || r.op.out_w <= 0 ||
+            (frame && (r.width <= 0 || r.height <= 0 || r.in_len < in))) {
+          c->reply(r.seq, SDSJ_EINVAL);
           continue;
         }
         c->inflight++;
+        std::lock_guard<std::mutex> g(qmu_);
         pending_.push_back(Req{c, r});
-      } else if (r.kind == SDSJ_SVC_FRAME) {
-        reply(*c, r.seq, frame(*c, r));
+        queued++;
       } else {
-        reply(*c, r.seq, SDSJ_EINVAL);
+        c->reply(r.seq, SDSJ_EINVAL);
       }
+    }
+    if (queued) qcv_.notify_all();
+  }
+
+  // Engine thread: the oldest pending request and every pending request with its op (up to max_batch)
+  // form a batch; a FRAME request goes alone through the frame path.
+  void lane_loop(Lane& l) {
+    (void)hipSetDevice(cfg_.device);
+    for (;;) {
+      bool frame = false;
+      {
+        std::unique_lock<std::mutex> g(qmu_);
+        qcv_.wait(g, [this] { return stopping_ || !pending_.empty(); });
+        if (pending_.empty()) return;  // stopping, nothing left
+        l.batch.clear();
+        if (pending_.front().r.kind == SDSJ_SVC_FRAME) {
+          l.batch.push_back(pending_.front());
+          pending_.pop_front();
+          frame = true;
+        } else {
+          const sdsj_op op = pending_.front().r.op;
+          for (auto it = pending_.begin(); it != pending_.end() && (int)l.batch.size() < max_batch_;) {
+            if (it->r.kind == SDSJ_SVC_DECODE && same_op(it->r.op, op)) {
+              l.batch.push_back(*it);
+              it = pending_.erase(it);
+            } else {
+              ++it;
+            }
+          }
+        }
+      }
+      if (frame) {
+        Req& q = l.batch[0];
+        q.c->reply(q.r.seq, run_frame(l, *q.c, q.r));
+        q.c->release();
+      } else {
+        run_batch(l);
+      }
+      l.batch.clear();
     }
   }
 
-  // One batch from the oldest pending request's op: every pending request with that op, up to max_batch.
-  int submit(Lane& l) {
-    const sdsj_op op = pending_.front().r.op;
-    l.batch.clear();
-    for (auto it = pending_.begin(); it != pending_.end() && (int)l.batch.size() < max_batch_;) {
-      if (same_op(it->r.op, op)) {
-        l.batch.push_back(*it);
-        it = pending_.erase(it);
-      } else {
-        ++it;
-      }
-    }
+  void run_batch(Lane& l) {
+    const double t0 = trace_ ? now_us() : 0;
     const int n = (int)l.batch.size();
-    l.ob = out_bytes(op);
-    const size_t need = (size_t)l.ob * n;
+    const sdsj_op op = l.batch[0].r.op;
+    const int64_t ob = out_bytes(op);
+    const size_t need = (size_t)ob * n;
+    int rc = SDSJ_OK;
     if (need > l.out_cap) {
       (void)hipFree(l.d_out);
       (void)hipHostFree(l.h_out);
       l.d_out = l.h_out = nullptr;
       l.out_cap = 0;
-      const size_t cap = std::max(need, (size_t)l.ob * max_batch_ / 4);
-      if (hipMalloc(&l.d_out, cap) != hipSuccess || hipHostMalloc(&l.h_out, cap) != hipSuccess) {
-        finish_failed(l, SDSJ_ENOMEM);
-        return SDSJ_OK;
-      }
-      l.out_cap = cap;
+      const size_t cap = std::max(need, (size_t)ob * max_batch_ / 4);
+      if (hipMalloc(&l.d_out, cap) != hipSuccess || hipHostMalloc(&l.h_out, cap) != hipSuccess) rc = SDSJ_ENOMEM;
+      else l.out_cap = cap;
     }
     std::vector<const uint8_t*> ptrs(n);
     std::vector<size_t> lens(n);
@@ -287,81 +345,53 @@ class Service {
       lens[i] = (size_t)l.batch[i].r.in_len;
       flips[i] = l.batch[i].r.flip ? 1 : 0;
     }
-    int rc = sdsj_submit_batch(l.e, 0, n, ptrs.data(), lens.data(), &op, flips.data(), l.d_out, l.s);
+    if (rc == SDSJ_OK) rc = sdsj_submit_batch(l.e, 0, n, ptrs.data(), lens.data(), &op, flips.data(), l.d_out, l.s);
     if (rc == SDSJ_OK && hipMemcpyAsync(l.h_out, l.d_out, need, hipMemcpyDeviceToHost, l.s) != hipSuccess) rc = SDSJ_EHIP;
     if (rc == SDSJ_OK && hipEventRecord(l.done, l.s) != hipSuccess) rc = SDSJ_EHIP;
+    const double t1 = trace_ ? now_us() : 0;
+    if (rc == SDSJ_OK && hipEventSynchronize(l.done) != hipSuccess) rc = SDSJ_EHIP;
+    if (rc == SDSJ_OK && sdsj_wait_batch(l.e, 0, l.status.data()) != SDSJ_OK) rc = SDSJ_EHIP;
     if (rc != SDSJ_OK) {
-      log_err("submit", sdsj_last_error(l.e));
+      log_err("batch", sdsj_last_error(l.e));
       (void)hipStreamSynchronize(l.s);
-      finish_failed(l, rc);
-      return SDSJ_OK;
+      std::fill(l.status.begin(), l.status.begin() + n, rc);
     }
-    l.busy = true;
-    return SDSJ_OK;
-  }
-
-  void finish_failed(Lane& l, int status) {
-    for (auto& q : l.batch) {
-      reply(*q.c, q.r.seq, status);
-      release(q.c);
-    }
-    l.batch.clear();
-  }
-
-  void release(const std::shared_ptr<Client>& c) {
-    if (--c->inflight == 0 && c->closed && c->base) {
-      munmap(c->base, c->size);
-      c->base = nullptr;
-    }
-  }
-
-  void complete(Lane& l) {
-    l.busy = false;
-    const int n = (int)l.batch.size();
-    if (sdsj_wait_batch(l.e, 0, l.status.data()) != SDSJ_OK)
-      std::fill(l.status.begin(), l.status.begin() + n, SDSJ_EHIP);
     for (int i = 0; i < n; i++) {
       Req& q = l.batch[i];
-      if (!q.c->closed && l.status[i] == SDSJ_OK) memcpy(q.c->base + q.r.out_off, l.h_out + (size_t)i * l.ob, l.ob);
-      reply(*q.c, q.r.seq, l.status[i]);
-      release(q.c);
+      if (!q.c->closed.load() && l.status[i] == SDSJ_OK) memcpy(q.c->base + q.r.out_off, l.h_out + (size_t)i * ob, ob);
+      q.c->reply(q.r.seq, l.status[i]);
+      q.c->release();
     }
-    l.batch.clear();
+    if (trace_)
+      fprintf(stderr, "sdsj_service: lane %d n %d submit %.1f us, wait %.1f us\n", (int)(&l - lanes_.data()), n, t1 - t0,
+              now_us() - t1);
   }
 
   // A frame PIL decoded in the worker (samples the JPEG kernels do not take): H2D, the frame path's
-  // crop / resize (sdsj_resize_frames_device), D2H -- synchronous on the first lane's engine once it is
-  // idle (rare: other formats and damaged streams).
-  int frame(Client& c, const sdsj_svc_req& r) {
+  // crop / resize (sdsj_resize_frames_device), D2H -- on this lane's engine.
+  int run_frame(Lane& l, Client& c, const sdsj_svc_req& r) {
     const int64_t fb = (int64_t)r.width * r.height * 3;
-    if (r.width <= 0 || r.height <= 0 || r.in_len < fb || !region_ok(c, 0, fb) || !region_ok(c, r.out_off, out_bytes(r.op)))
-      return SDSJ_EINVAL;
-    Lane& l = lanes_[0];
-    if (l.busy) {
-      (void)hipEventSynchronize(l.done);
-      complete(l);
-    }
     const int64_t ob = out_bytes(r.op);
-    if ((size_t)fb > fr_in_cap_ || (size_t)ob > fr_out_cap_ || !fr_small_) {
-      (void)hipFree(fr_in_), (void)hipFree(fr_out_), (void)hipFree(fr_small_);
-      fr_in_ = fr_out_ = fr_small_ = nullptr;
-      fr_in_cap_ = fr_out_cap_ = 0;
-      if (hipMalloc(&fr_in_, fb) != hipSuccess || hipMalloc(&fr_out_, ob) != hipSuccess || hipMalloc(&fr_small_, 16) != hipSuccess)
+    if ((size_t)fb > l.fr_in_cap || (size_t)ob > l.fr_out_cap || !l.fr_small) {
+      (void)hipFree(l.fr_in), (void)hipFree(l.fr_out), (void)hipFree(l.fr_small);
+      l.fr_in = l.fr_out = l.fr_small = nullptr;
+      l.fr_in_cap = l.fr_out_cap = 0;
+      if (hipMalloc(&l.fr_in, fb) != hipSuccess || hipMalloc(&l.fr_out, ob) != hipSuccess || hipMalloc(&l.fr_small, 16) != hipSuccess)
         return SDSJ_ENOMEM;
-      fr_in_cap_ = (size_t)fb;
-      fr_out_cap_ = (size_t)ob;
+      l.fr_in_cap = (size_t)fb;
+      l.fr_out_cap = (size_t)ob;
     }
-    // fr_small_: [0, 4) the frame's status, [4] its flip flag
+    // fr_small: [0, 4) the frame's status, [4] its flip flag
     uint8_t small[8] = {0, 0, 0, 0, (uint8_t)(r.flip ? 1 : 0), 0, 0, 0};
-    if (hipMemcpyAsync(fr_in_, c.base, fb, hipMemcpyHostToDevice, l.s) != hipSuccess ||
-        hipMemcpyAsync(fr_small_, small, sizeof(small), hipMemcpyHostToDevice, l.s) != hipSuccess ||
+    if (hipMemcpyAsync(l.fr_in, c.base, fb, hipMemcpyHostToDevice, l.s) != hipSuccess ||
+        hipMemcpyAsync(l.fr_small, small, sizeof(small), hipMemcpyHostToDevice, l.s) != hipSuccess ||
         hipStreamSynchronize(l.s) != hipSuccess)
       return SDSJ_EHIP;
-    int st = sdsj_resize_frames_device(l.e, 1, fr_in_, r.width, r.height, fb, &r.op, fr_small_ + 4, fr_out_,
-                                       reinterpret_cast<int32_t*>(fr_small_), l.s);
+    int st = sdsj_resize_frames_device(l.e, 1, l.fr_in, r.width, r.height, fb, &r.op, l.fr_small + 4, l.fr_out,
+                                       reinterpret_cast<int32_t*>(l.fr_small), l.s);
     if (st != SDSJ_OK) return st;
-    if (hipMemcpyAsync(small, fr_small_, sizeof(small), hipMemcpyDeviceToHost, l.s) != hipSuccess ||
-        hipMemcpyAsync(c.base + r.out_off, fr_out_, ob, hipMemcpyDeviceToHost, l.s) != hipSuccess ||
+    if (hipMemcpyAsync(small, l.fr_small, sizeof(small), hipMemcpyDeviceToHost, l.s) != hipSuccess ||
+        hipMemcpyAsync(c.base + r.out_off, l.fr_out, ob, hipMemcpyDeviceToHost, l.s) != hipSuccess ||
         hipStreamSynchronize(l.s) != hipSuccess)
       return SDSJ_EHIP;
     int32_t fst;
@@ -371,12 +401,15 @@ class Service {
 
   sdsj_service_cfg cfg_;
   int max_batch_ = 64;
+  bool trace_ = false;
   int ep_ = -1;
   std::vector<Lane> lanes_;
-  std::map<int, std::shared_ptr<Client>> clients_;
+  std::vector<std::thread> threads_;
+  std::map<int, std::shared_ptr<Client>> clients_;  // (the epoll thread's)
+  std::mutex qmu_;
+  std::condition_variable qcv_;
   std::deque<Req> pending_;
-  uint8_t *fr_in_ = nullptr, *fr_out_ = nullptr, *fr_small_ = nullptr;  // frame path buffers (grow only)
-  size_t fr_in_cap_ = 0, fr_out_cap_ = 0;
+  bool stopping_ = false;
 };
 
 }  // namespace

@@ -241,7 +241,7 @@ def test_simd_idct_semantics_on_extreme_coefficients_vs_oracle(engine):
         np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res, flip=flips[k]), err_msg=f"image {k}")
 
 
-def test_fill_stuffed_streams_rerun_on_pil_through_the_transform():
+def test_fill_stuffed_streams_rerun_on_pil_through_the_transform(engine):
     """FF FF .. 00 inside a baseline scan: the GPU reports CORRUPT, the per-sample transform reruns the
     sample on PIL, so the output equals the reference's PIL decode + resize."""
     import io
