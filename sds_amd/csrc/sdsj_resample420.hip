@@ -124,6 +124,9 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
 // per CU, and 5 waves per SIMD fit their registers without spills (95 VGPRs): k_rs420<5> 9.95 -> 9.23 ms
 // per 16,384 images (profiles/r03b_rs420_occupancy_ab.txt).  The 9- and 11-tap kernels and 4:4:4 (whose
 // full-width chroma rows take 34 KB) keep 4.
+#ifndef SDSJ_RS_GLDS
+#define SDSJ_RS_GLDS 1
+#endif
 #ifndef SDSJ_RS_WAVES
 #define SDSJ_RS_WAVES 5
 #endif
@@ -246,6 +249,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
     // conversion, written to LDS after its H/V work), so their latency hides behind a whole step.
     // Wave wv holds staged rows wv, wv + 4, wv + 8 (<= 12 rows), 64 dwords per load.
     constexpr int kPR = (G::kRows + 3) / 4, kPC = (kMaxSpan / 4 + 2 + 63) / 64;
+    constexpr bool kGlds = SDSJ_RS_GLDS && LAY != kRsGray;
     uint32_t pre[kPR][kPC];
     auto row_src = [&](const Step& p, int row, const uint8_t*& g, int& nd, int& o) {
       if (row < p.nr) {
@@ -277,9 +281,29 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
         }
       }
     };
-    auto commit = [&](const Step& p) {
+    // SDSJ_RS_GLDS (colour layouts): the next step's rows go straight to LDS (global_load_lds, no
+    // register staging), issued after this step's conversion has read the staged rows; the step-end
+    // barrier retires them.
+    auto issue_lds = [&](const Step& p) {
 #pragma unroll
       for (int i = 0; i < kPR; i++) {
+        const int row = wv + 4 * i;
+        if (row < p.nr + 2 * p.nrc) {
+          const uint8_t* g;
+          int nd, o;
+          row_src(p, row, g, nd, o);
+          const uint32_t* g4 = reinterpret_cast<const uint32_t*>(g);
+#pragma unroll
+          for (int h = 0; h < kPC; h++)
+            if (64 * h + lane < nd)
+              __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g4 + 64 * h + lane),
+                                               (__attribute__((address_space(3))) void*)(&L.st[o + 64 * h]), 4, 0, 0);
+        }
+      }
+    };
+    auto commit = [&](const Step& p) {
+#pragma unroll
+      for (int i = 0; i < (kGlds ? 0 : kPR); i++) {
         const int row = wv + 4 * i;
         if (row < p.nr + 2 * p.nrc) {
           const uint8_t* g;
@@ -308,7 +332,8 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
       }
     };
     Step cur = plan_step(r_lo);
-    issue(cur);
+    if (kGlds) issue_lds(cur);
+    else issue(cur);
     commit(cur);
     __syncthreads();
     // the next output row's window (uniform, carried in scalars): first row, and one past its last
@@ -322,7 +347,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
       const int nr = cur.nr;
       const bool more = ra + kFRows < r_hi;
       const Step nxt = more ? plan_step(ra + kFRows) : cur;
-      if (more) issue(nxt);
+      if (more && !kGlds) issue(nxt);
       if (LAY != kRsGray) {
         // B. fancy upsampling + ycc->rgb on 8 pixels per item
         for (int it = t; it < nr * ng; it += kFThreads) {
@@ -469,6 +494,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
           o[kFRgbW / 2 + 1] = wb[1];
         }
         __syncthreads();
+        if (kGlds && more) issue_lds(nxt);
       }
       if (active) {
 #pragma unroll

@@ -60,6 +60,9 @@ class _Handle:
         env = dict(os.environ)
         repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         env["PYTHONPATH"] = repo + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        # one stream per engine, and one hardware queue per stream (HIP's default is 4 per process)
+        if engines > int(env.get("GPU_MAX_HW_QUEUES", "4") or 4):
+            env["GPU_MAX_HW_QUEUES"] = str(min(engines, 16))
         self.proc = subprocess.Popen(cmd, stdin=subprocess.DEVNULL, close_fds=True, env=env)
         atexit.register(self.stop)
 
@@ -78,10 +81,12 @@ _handles: dict[tuple[int, int], _Handle] = {}
 _handles_lock = threading.Lock()
 
 
-def ensure_service(device: int = 0, engines: int = 4, max_batch: int = 64) -> str:
+def ensure_service(device: int = 0, engines: int | None = None, max_batch: int = 64) -> str:
     """Starts (once per process and device) the decode service for HIP device ``device``; returns its
     address (an abstract AF_UNIX name).  Call it before DataLoader workers fork -- the pipeline factory
     does.  The process starting it needs no GPU; the service initialises HIP in its own process."""
+    if engines is None:
+        engines = int(os.environ.get("SDS_AMD_SERVICE_ENGINES", "4"))
     key = (os.getpid(), int(device))
     with _handles_lock:
         h = _handles.get(key)

@@ -1,6 +1,7 @@
 """Rate of the per-sample drop-in (create_standard_image_pipeline(..., device="cuda")) in the reference's
 loader shapes: the transform list applied sample by sample (sds/dataset.py:535-561) in the main
-process, and inside DataLoader workers (examples/iter_image_dataset.py:72-80: batch 4 here, fork,
+process, and inside DataLoader workers (examples/iter_image_dataset.py:72-80: batch 4 here unless
+PERSAMPLE_BATCH says otherwise, fork,
 pin_memory=True) -- through the node-local decode service (the default, host outputs), or with an engine
 per worker (service=None, device outputs with pin_memory=False).
 Inputs: a folder of synthetic 640x480 q90 JPEGs (configs[0] shape) -> 256x256 uint8.
@@ -35,7 +36,33 @@ MODES = {
     # the workers decode on the GPU but hand back only a tiny host tensor: the rate without the
     # device-tensor IPC (CUDA IPC handles opened by the parent per batch)
     "dataloader_fork_workers8_decode_only": (8, False, None, "discard", None),
+    # comparators in the same loader shape (no sds_amd): a transform that only reads the file and returns
+    # a constant 3x256x256 uint8 tensor (the loader's own ceiling), and plain Pillow decode + centre crop +
+    # bilinear resize on the worker's CPU (the reference's per-sample library, not its exact transform)
+    "null_fork_workers8_pinned": (8, True, None, None, "null"),
+    "null_fork_workers16_pinned": (16, True, None, None, "null"),
+    "pil_fork_workers8_pinned": (8, True, None, None, "pil"),
+    "pil_fork_workers16_pinned": (16, True, None, None, "pil"),
 }
+BATCH = int(os.environ.get("PERSAMPLE_BATCH", "4"))
+
+
+def _null_transform(s):
+    with open(s["jpg"], "rb") as f:
+        f.read()
+    s["image"] = torch.zeros(3, 256, 256, dtype=torch.uint8)
+    return s
+
+
+def _pil_transform(s):
+    import numpy as np
+    from PIL import Image
+    im = Image.open(s["jpg"]).convert("RGB")
+    w, h = im.size
+    c = min(w, h)
+    im = im.crop(((w - c) // 2, (h - c) // 2, (w - c) // 2 + c, (h - c) // 2 + c)).resize((256, 256), Image.BILINEAR)
+    s["image"] = torch.from_numpy(np.asarray(im).copy()).permute(2, 0, 1)
+    return s
 
 
 class _Discard(torch.utils.data.IterableDataset):
@@ -62,14 +89,19 @@ def run_mode(mode, n_files, seconds):
             f.write(jpgs[i % len(jpgs)])
         paths.append(p)
     discard = odev == "discard"
-    ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device=None if discard else odev,
-                                        service=service)
+    if service == "null":
+        ts = [_null_transform]
+    elif service == "pil":
+        ts = [_pil_transform]
+    else:
+        ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device=None if discard else odev,
+                                            service=service)
     ds = FolderDataset(paths, ts)
     if discard:
         ds = _Discard(ds)
     if nw:
         # persistent workers: forked once, before the parent receives its first device tensor
-        src = DataLoader(ds, batch_size=4, num_workers=nw, pin_memory=pin, multiprocessing_context=ctx,
+        src = DataLoader(ds, batch_size=BATCH, num_workers=nw, pin_memory=pin, multiprocessing_context=ctx,
                          persistent_workers=True, prefetch_factor=4)
     else:
         src = ds
@@ -89,8 +121,8 @@ def run_mode(mode, n_files, seconds):
     dt = time.perf_counter() - t0
     print(json.dumps({"mode": mode, "images_per_s": round(n / dt, 1), "images": n, "seconds": round(dt, 2),
                       "num_workers": nw, "pin_memory": pin, "context": ctx or "fork",
-                      "output_device": "cpu" if service else (odev or "cuda"), "service": bool(service),
-                      "first_batch": first}), flush=True)
+                      "output_device": "cpu" if service else (odev or "cuda"), "service": service,
+                      "batch_size": BATCH if nw else None, "first_batch": first}), flush=True)
 
 
 def main():
