@@ -48,7 +48,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-PMC_JSON = os.path.join(REPO, "profiles", "pmc_latest.json")  # tools/pmc.sh + tools/pmc_summary.py output
+# tools/pmc.sh + tools/pmc_summary.py output per workload (the counters of the batch that workload runs)
+PMC_JSONS = {"vga256": os.path.join(REPO, "profiles", "pmc_latest.json"),
+             "mixed512": os.path.join(REPO, "profiles", "pmc_latest_mixed512.json")}
+PMC_JSON = PMC_JSONS["vga256"]
 # engine stage -> kernels launched in it (rocprofv3 kernel names contain these)
 STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_us_", "k_scanmap"],
                  "prog": ["k_prog"], "entspec": ["k_enttab", "k_entspec"], "entsync": ["k_entsync"],
@@ -57,11 +60,11 @@ STAGE_KERNELS = {"parse": ["k_parse"], "plan": ["k_plan"], "unstuff": ["k_us_", 
                  "resample": ["k_resample", "k_rs420", "k_finish"]}
 
 
-def pmc_traffic(stage: str, batch: int, lanes: int):
+def pmc_traffic(stage: str, batch: int, lanes: int, path: str = PMC_JSON):
     """HBM bytes per launch of `stage` from the committed PMC summary (FETCH_SIZE + WRITE_SIZE, KB as
     rocprofv3 reports them, summed over the stage's kernels), if collected at this batch and lane count."""
     try:
-        with open(PMC_JSON) as f:
+        with open(path) as f:
             pmc = json.load(f)
     except (OSError, ValueError):
         return None
@@ -72,17 +75,17 @@ def pmc_traffic(stage: str, batch: int, lanes: int):
         if any(k in name for k in STAGE_KERNELS.get(stage, [])) and "FETCH_SIZE" in ctr and "WRITE_SIZE" in ctr:
             tot += (ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024.0
             hit = True
-    return {"bytes_per_launch": round(tot), "source": os.path.relpath(PMC_JSON, REPO), "head": pmc.get("head"),
+    return {"bytes_per_launch": round(tot), "source": os.path.relpath(path, REPO), "head": pmc.get("head"),
             "note": "FETCH_SIZE + WRITE_SIZE as reported, separate --pmc passes (MI355X_MICROARCH.md: FETCH_SIZE "
                     "counts 1/2 of 16-B/lane streaming reads; these kernels read <= 4 B/lane, uncalibrated)"} \
         if hit else None
 
 
-def pmc_counters(stage: str, batch: int, lanes: int) -> Optional[dict]:
+def pmc_counters(stage: str, batch: int, lanes: int, path: str = PMC_JSON) -> Optional[dict]:
     """Per-launch PMC counters of `stage` (summed over its kernels) from the committed summary, if it
     was collected at this batch and lane count."""
     try:
-        with open(PMC_JSON) as f:
+        with open(path) as f:
             pmc = json.load(f)
     except (OSError, ValueError):
         return None
@@ -96,13 +99,13 @@ def pmc_counters(stage: str, batch: int, lanes: int) -> Optional[dict]:
     return tot or None
 
 
-def measured_limiter(stage: str, batch: int, launch_ms: float, traffic: Optional[dict]) -> dict:
+def measured_limiter(stage: str, batch: int, launch_ms: float, traffic: Optional[dict], path: str = PMC_JSON) -> dict:
     """Which roof the dominant kernel is nearest, from its measured counters: HBM (implementation bytes
     per launch / launch time / peak) or VALU issue (wave-level VALU instructions x 2 cycles -- a wave64
     VALU op holds its SIMD 2 cycles when two or more waves share it -- / (1,024 SIMDs x 2.4 GHz x launch
     time)).  Neither near 1 = latency-bound (dependent LDS lookups / VALU chains)."""
-    ctr = pmc_counters(stage, batch, 1)
-    out = {"source": os.path.relpath(PMC_JSON, REPO) if ctr else None}
+    ctr = pmc_counters(stage, batch, 1, path)
+    out = {"source": os.path.relpath(path, REPO) if ctr else None}
     if not ctr or launch_ms <= 0:
         out["verdict"] = "unmeasured (no PMC summary at this batch)"
         return out
@@ -582,7 +585,8 @@ def main():
     launch_ms = stages[dom] / args.roofline_steps
     launch_bytes = B * alg_bytes_per_img
     achieved = launch_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
-    traffic = pmc_traffic(dom, B, 1)
+    pmc_path = PMC_JSONS["mixed512" if mixed else "vga256"]
+    traffic = pmc_traffic(dom, B, 1, pmc_path)
     if args.profile_steps and rank == 0:
         print(json.dumps({"stage_ms_per_step_single_lane": {k: v / args.roofline_steps for k, v in stages.items()}}),
               file=sys.stderr)
@@ -655,7 +659,7 @@ def main():
                          "algorithmic_bytes_per_image": round(alg_bytes_per_img, 1),
                          "launch_ms": round(launch_ms, 4), "images_per_launch": B, "lanes": 1,
                          "timing": "HIP events on the launch stream, single-lane pass after the timed region",
-                         "limiter": measured_limiter(dom, B, launch_ms, traffic),
+                         "limiter": measured_limiter(dom, B, launch_ms, traffic, pmc_path),
                          "pipeline_achieved": round(value / world * alg_bytes_per_img / 1e9, 2)},
             "stage_ms_per_step_single_lane": {k: round(v / args.roofline_steps, 4) for k, v in stages.items()},
             "pixel_check": pixel_check,

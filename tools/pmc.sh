@@ -18,4 +18,4 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   rm -rf gpurun_out/pmc_$i
   timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_$i -o p -- $B > gpurun_out/pmc_$i.log 2>&1
 done
-python3 tools/pmc_summary.py gpurun_out "$BATCH" "$SDSJ_LANES" > gpurun_out/pmc.json
+python3 tools/pmc_summary.py gpurun_out "$BATCH" "$SDSJ_LANES" > gpurun_out/${PMC_OUT:-pmc.json}
