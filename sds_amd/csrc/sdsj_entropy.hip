@@ -335,6 +335,21 @@ constexpr int kRefillSpec = SDSJ_REFILL_SLACK ? 32 * (kSpecGroup + 1) : 27 * (kS
 // (fewer scattered 8-byte stores; profiles/r03d_ab.txt).
 constexpr int kRecStore = SDSJ_REC_STORE;
 static_assert(kRecStore <= kRec, "records fit their scratch");
+// Record k of subsequence j: at [j][k] (SDSJ_REC_T 0) or at [k][j] (1: the records of neighbouring
+// subsequences -- neighbouring lanes -- share cache lines, so their scattered 8-byte stores merge in L2
+// instead of each dirtying a line of its own).
+#ifndef SDSJ_REC_T
+#define SDSJ_REC_T 0
+#endif
+struct RecView {
+  SyncRec* base;
+  int64_t stride;  // elements between records k and k + 1
+  __device__ __forceinline__ const SyncRec& operator[](int k) const { return base[k * stride]; }
+  __device__ __forceinline__ void put(int k, uint2 v) const { reinterpret_cast<uint2*>(base)[k * stride] = v; }
+};
+__device__ __forceinline__ RecView rec_view(SyncRec* recs, int j, int nsub_cap) {
+  return SDSJ_REC_T ? RecView{recs + j, nsub_cap} : RecView{recs + (int64_t)j * kRec, 1};
+}
 constexpr int kRefillWrite = SDSJ_REFILL_SLACK ? 32 * (kWriteGroup + 1) : 27 * (kWriteGroup - 1) + 32;
 
 template <int Q>
@@ -611,7 +626,7 @@ using LdsSync = LdsSyncT<kEntThreads>;
 // block boundary at or after end_bit, recording every block boundary.  A segment's first
 // subsequence starts exactly at its (known) state.
 template <int LB, class TT>
-__device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
+__device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const RecView rec,
                          uint32_t seg_start, uint32_t warm) {
   constexpr bool kMulti = std::is_same_v<TT, SpecTables>;  // LB = 11: the multi-symbol table
   // (bits at or beyond S.lim_bit read as zeros)
@@ -686,8 +701,7 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           const bool done = next_z(z, s, r);
           if (done && nrec < kRecStore)  // one 8-byte store (SyncRec: p, dc, blk, pad)
-            reinterpret_cast<uint2*>(rec)[nrec] =
-                make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
+            rec.put(nrec, make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16)));
           // block end without branches: the sums, counters and the next block's context by selects
           add_dc(c, done ? dcd : 0, d0, d1, d2);
           nrec += done ? 1 : 0;
@@ -727,7 +741,7 @@ constexpr uint32_t kMergeBits = 768;
 constexpr int kSyncQ = kQ;  // (a deeper queue measured slower: the pull shifts it)
 
 template <int LB, class TT>
-__device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const SyncRec* rec) {
+__device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const RecView rec) {
   const uint32_t end = S.end_bit;
   const int nrec = S.nrec;
   BitsQ<kSyncQ> b;
@@ -877,7 +891,7 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   // this workgroup's share of the subsequences (every group computes the same layout above)
   const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
   for (int j = j0 + t; j < j1; j += kEntThreads) {
-    const int k = spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, (uint32_t)sv.lo[sub[j].seg] * 8u,
+    const int k = spec_pass<LB>(L.T, K, src, sub[j], rec_view(recs, j, d->nsub_cap), (uint32_t)sv.lo[sub[j].seg] * 8u,
                                 (uint32_t)d->warm_bits);
     if (kStats) {
       nsym_spec += k;
@@ -961,7 +975,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       }
       for (int i = t; i < ntask; i += NT) {
         const int j = L.u.task[0][i];
-        const int k = sync_full<kSyncLB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec);
+        const int k = sync_full<kSyncLB>(L.T, K, src, sub[j], rec_view(recs, j, d->nsub_cap));
         if (kStats) nsym_sync += k;
       }
       __syncthreads();
