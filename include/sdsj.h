@@ -224,7 +224,7 @@ typedef struct sdsj_svc_rep {
 typedef struct sdsj_service_cfg {
     int32_t abi_version; /* SDSJ_ABI_VERSION */
     int32_t device;      /* HIP device */
-    int32_t engines;     /* batches in flight at once (0 = 4) */
+    int32_t engines;     /* batches in flight at once (0 = 8) */
     int32_t max_batch;   /* requests per batch (0 = 64) */
     int32_t listen_fd;   /* a bound, listening AF_UNIX SOCK_SEQPACKET socket */
     int32_t parent_pid;  /* the service returns when this process is gone (0 = never) */

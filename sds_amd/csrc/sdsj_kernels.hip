@@ -1019,9 +1019,6 @@ constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides
 // Work unit = a group: 8 horizontally adjacent blocks of one component, one per thread, so each of
 // a block's 8 row stores joins the group's other 7 in 64 contiguous bytes of a plane row.  The
 // block stays in registers through both passes (64 values), so there is no LDS transpose.
-#ifndef SDSJ_IDCT_PK
-#define SDSJ_IDCT_PK 0  // 1: the packed 16-bit / dot2 form (sdsj_idct.h islow_1d_pk)
-#endif
 #ifndef SDSJ_IDCT_WAVES
 #define SDSJ_IDCT_WAVES 4  // waves per SIMD the register budget targets (124 VGPRs at 4)
 #endif
@@ -1034,7 +1031,6 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
   __shared__ alignas(16) int32_t qt[kMaxComp][64];
-  __shared__ alignas(16) uint16_t qt16[kMaxComp][64];  // (the packed path's copy)
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
   __shared__ int32_t gstart[kMaxComp + 1], ngx[kMaxComp], cbw[kMaxComp], ch_[kMaxComp], cv_[kMaxComp], cpitch[kMaxComp];
   __shared__ int32_t cgx0[kMaxComp], cby0[kMaxComp];  // first 8-block group column / block row needed
@@ -1043,11 +1039,7 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   const int t = threadIdx.x;
   const int ncomp = d->ncomp, bpm = d->bpm, mcux = d->mcux;
   // quantisation tables in zigzag order (the coefficient blocks' order)
-  for (int i = t; i < ncomp * 64; i += kIdctThreads) {
-    const uint16_t q = tables[img].qt[d->comp[i / 64].tq][natural_order(i % 64)];
-    qt[i / 64][i % 64] = q;
-    qt16[i / 64][i % 64] = q;
-  }
+  for (int i = t; i < ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][natural_order(i % 64)];
   if (t < bpm) binv[d->blk_comp[t]][d->blk_dy[t] * 4 + d->blk_dx[t]] = t;
   if (t == 0) {
     // only the blocks whose pixels the colour/resample passes read: the source rectangle
@@ -1137,64 +1129,6 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
                   raw[3].x | (raw[3].y & 0xFFFFu) | (raw[3].z & 0xFFFF0000u) | raw[3].w;
 #pragma unroll
     for (int i = 2; i < 8; i++) ac |= i == 3 ? 0u : (raw[i].x | raw[i].y | raw[i].z | raw[i].w);
-#if SDSJ_IDCT_PK
-    // DEQUANTIZE (vpmullw): the coefficient pairs times the quantiser pairs, low 16 bits, zigzag order
-    uint32_t dq[32];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const uint4 q = *reinterpret_cast<const uint4*>(&qt16[c][i * 8]);
-      dq[4 * i] = as_u32(as_u16x2(raw[i].x) * as_u16x2(q.x));
-      dq[4 * i + 1] = as_u32(as_u16x2(raw[i].y) * as_u16x2(q.y));
-      dq[4 * i + 2] = as_u32(as_u16x2(raw[i].z) * as_u16x2(q.z));
-      dq[4 * i + 3] = as_u32(as_u16x2(raw[i].w) * as_u16x2(q.w));
-    }
-    // the dequantised values at natural positions pa (low half) and pb (high half): one v_perm_b32
-    auto pair = [&](int pa, int pb) {
-      const int za = zigzag_of(pa), zb = zigzag_of(pb);
-      const uint32_t sel = ((za & 1) ? 0x0302u : 0x0100u) | ((zb & 1) ? 0x07060000u : 0x05040000u);
-      return as_u16x2(__builtin_amdgcn_perm(dq[zb >> 1], dq[za >> 1], sel));
-    };
-    // pass 1, columns in the pairs pass 2 takes: (2, 6), (7, 1), (5, 3), (0, 4).  Row 0 sits in the low
-    // half of column k's (x0, x4) pair; the SIMD shortcut (rows 1..7 zero, see below) is wrap16(4 x) / 4
-    // on it (x4 is then zero).  Outputs: (sum + 2^10) >> 11 packed with 16-bit saturation (vpackssdw).
-    u16x2 r26[8], r71[8], r53[8], r04[8];  // pass-2 input pairs of each row
-    auto column = [&](int k, uint32_t o[8]) {
-      u16x2 p04 = pair(k, 32 + k);
-      if (!ac) p04 = as_u16x2(as_u32(__builtin_bit_cast(u16x2, (__builtin_bit_cast(s16x2, p04) << 2) >> 2)));
-      islow_1d_pk(pair(16 + k, 48 + k), pair(56 + k, 8 + k), pair(40 + k, 24 + k), p04, 1u << 10, o);
-    };
-    constexpr int kColPair[4][2] = {{2, 6}, {7, 1}, {5, 3}, {0, 4}};
-#pragma unroll
-    for (int cp = 0; cp < 4; cp++) {
-      uint32_t oa[8], ob[8];
-      column(kColPair[cp][0], oa);
-      column(kColPair[cp][1], ob);
-#pragma unroll
-      for (int r = 0; r < 8; r++) {
-        const u16x2 v = __builtin_bit_cast(u16x2, __builtin_amdgcn_cvt_pk_i16((int)oa[r] >> 11, (int)ob[r] >> 11));
-        if (cp == 0) r26[r] = v;
-        else if (cp == 1) r71[r] = v;
-        else if (cp == 2) r53[r] = v;
-        else r04[r] = v;
-      }
-    }
-    // pass 2: rows -> (sum + 2^17) >> 18, saturated to 8 bits, + 128 (vpacksswb, vpaddb) -> 8 bytes
-    uint8_t* dst = planes + cplane[c] + (int64_t)(by * 8) * cpitch[c] + bx * 8;
-#pragma unroll
-    for (int r = 0; r < 8; r++) {
-      uint32_t o[8];
-      islow_1d_pk(r26[r], r71[r], r53[r], r04[r], 1u << 17, o);
-      uint32_t b[4];
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        s16x2 v = __builtin_amdgcn_cvt_pk_i16((int)o[2 * k] >> 18, (int)o[2 * k + 1] >> 18);
-        v = __builtin_elementwise_min(__builtin_elementwise_max(v, (s16x2){-128, -128}), (s16x2){127, 127});
-        b[k] = as_u32(__builtin_bit_cast(u16x2, v) + (u16x2){128, 128});
-      }
-      const uint32_t lo = __builtin_amdgcn_perm(b[1], b[0], 0x06040200u), hi = __builtin_amdgcn_perm(b[3], b[2], 0x06040200u);
-      *reinterpret_cast<uint2*>(dst + (int64_t)r * cpitch[c]) = make_uint2(lo, hi);
-    }
-#else
     // DEQUANTIZE as vpmullw: the low 16 bits of coef * quantval, zigzag position k into row-major
     // natural_order(k)
     int x[64];
@@ -1237,7 +1171,6 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
       for (int k = 0; k < 4; k++) hi |= descale_p2(o[k + 4]) << (8 * k);
       *reinterpret_cast<uint2*>(dst + (int64_t)r * cpitch[c]) = make_uint2(lo, hi);
     }
-#endif
   }
 }
 

@@ -115,7 +115,7 @@ class Service {
     const char* path = getenv("SDSJ_SERVICE_PATH");
     submit_path_ = path && strcmp(path, "submit") == 0;
     if (hipSetDevice(cfg_.device) != hipSuccess) return fail("hipSetDevice", SDSJ_EHIP);
-    const int nl = cfg_.engines > 0 ? cfg_.engines : 4;
+    const int nl = cfg_.engines > 0 ? cfg_.engines : 8;
     max_batch_ = cfg_.max_batch > 0 ? cfg_.max_batch : 64;
     lanes_.resize(nl);
     for (auto& l : lanes_) {

@@ -86,7 +86,7 @@ def ensure_service(device: int = 0, engines: int | None = None, max_batch: int =
     address (an abstract AF_UNIX name).  Call it before DataLoader workers fork -- the pipeline factory
     does.  The process starting it needs no GPU; the service initialises HIP in its own process."""
     if engines is None:
-        engines = int(os.environ.get("SDS_AMD_SERVICE_ENGINES", "4"))
+        engines = int(os.environ.get("SDS_AMD_SERVICE_ENGINES", "8"))
     key = (os.getpid(), int(device))
     with _handles_lock:
         h = _handles.get(key)
@@ -219,7 +219,7 @@ def serve_main(argv=None) -> int:
     ap.add_argument("--address", required=True)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--parent", type=int, default=0)
-    ap.add_argument("--engines", type=int, default=4)
+    ap.add_argument("--engines", type=int, default=8)
     ap.add_argument("--max-batch", type=int, default=64)
     a = ap.parse_args(argv)
     sock = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
