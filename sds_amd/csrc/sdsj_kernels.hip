@@ -1019,6 +1019,9 @@ constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides
 // Work unit = a group: 8 horizontally adjacent blocks of one component, one per thread, so each of
 // a block's 8 row stores joins the group's other 7 in 64 contiguous bytes of a plane row.  The
 // block stays in registers through both passes (64 values), so there is no LDS transpose.
+#ifndef SDSJ_IDCT_COAL
+#define SDSJ_IDCT_COAL 0  // 1: coalesced coefficient loads exchanged through LDS (see k_idct)
+#endif
 #ifndef SDSJ_IDCT_WAVES
 #define SDSJ_IDCT_WAVES 4  // waves per SIMD the register budget targets (124 VGPRs at 4)
 #endif
@@ -1036,6 +1039,9 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   __shared__ int32_t cgx0[kMaxComp], cby0[kMaxComp];  // first 8-block group column / block row needed
   __shared__ float rngx[kMaxComp], rch[kMaxComp], rcv[kMaxComp];  // reciprocals for the exact quotients below
   __shared__ int64_t cplane[kMaxComp];
+#if SDSJ_IDCT_COAL
+  __shared__ uint4 xch[kIdctThreads / 8][8 * 9];  // per group: [block][chunk], rows padded to 9 chunks
+#endif
   const int t = threadIdx.x;
   const int ncomp = d->ncomp, bpm = d->bpm, mcux = d->mcux;
   // quantisation tables in zigzag order (the coefficient blocks' order)
@@ -1116,6 +1122,24 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   for (int grp = blockIdx.x * (kIdctThreads / 8) + (t >> 3); grp < ngroups; grp += gridDim.x * (kIdctThreads / 8)) {
     int c, by, bx, g;
     locate(grp, c, by, bx, g);
+#if SDSJ_IDCT_COAL
+    // The group's 8 blocks are read cooperatively -- lane lb takes 16-byte chunk lb of each, so one
+    // load instruction covers whole 128-byte blocks -- and handed to their lanes through LDS.
+    // key: the block's decode index; -2 = a block the entropy decoder left zero; -1 = none.
+    const int key = g < 0 ? -1 : (zero_block(g) ? -2 : g);
+    uint4* X = xch[t >> 3];
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const int kb = __shfl(key, ((t & 63) & ~7) + b);
+      X[b * 9 + lb] = kb >= 0 ? reinterpret_cast<const uint4*>(coef + (int64_t)kb * 64)[lb] : make_uint4(0, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint4 raw[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) raw[i] = X[lb * 9 + i];
+    __builtin_amdgcn_wave_barrier();
+    if (g < 0) continue;
+#else
     if (g < 0) continue;
     // the block (zigzag order, k_entwrite / k_prog), or zeros where the entropy decoder left it zero
     const uint4* src = reinterpret_cast<const uint4*>(coef + (int64_t)g * 64);
@@ -1123,6 +1147,7 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
     uint4 raw[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) raw[i] = zb ? make_uint4(0, 0, 0, 0) : src[i];
+#endif
     // `ac`: any raw coefficient outside row 0 (the SIMD pass 1's zero test); row 0 is zigzag positions
     // 0, 1, 5, 6, 14, 15, 27 and 28
     uint32_t ac = raw[0].y | (raw[0].z & 0xFFFFu) | (raw[0].w & 0xFFFF0000u) | raw[1].x | raw[1].y | raw[1].z |
