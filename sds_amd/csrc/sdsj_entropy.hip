@@ -393,15 +393,32 @@ __device__ __forceinline__ void bits_init(BitsQ<Q>& b, const uint32_t* src, uint
 #ifndef SDSJ_PARTIAL_REFILL
 #define SDSJ_PARTIAL_REFILL 0
 #endif
+// SDSJ_FILL_X4: the kQ words as 16-byte loads (dword-aligned global_load_dwordx4: a quarter of the
+// load instructions, and of the per-lane cache-line requests, of one dword load per word)
+#ifndef SDSJ_FILL_X4
+#define SDSJ_FILL_X4 0
+#endif
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 template <int Q>
 __device__ __forceinline__ void bits_fill(BitsQ<Q>& b) {
   if ((b.wi + Q) * 32u <= b.lim) {  // the common case: all kQ words lie before the limit
+    if constexpr (SDSJ_FILL_X4 && Q % 4 == 0 && !SDSJ_PARTIAL_REFILL) {
 #pragma unroll
-    for (int k = 0; k < Q; k++) {
-      if (SDSJ_PARTIAL_REFILL) {  // only the words not queued yet (q[0 .. nq) hold words wi .. wi + nq)
-        if (k >= b.nq) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
-      } else {
-        b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+      for (int k = 0; k < Q; k += 4) {
+        const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(b.src + b.wi + k);
+        b.q[k] = __builtin_bswap32(v.x);
+        b.q[k + 1] = __builtin_bswap32(v.y);
+        b.q[k + 2] = __builtin_bswap32(v.z);
+        b.q[k + 3] = __builtin_bswap32(v.w);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < Q; k++) {
+        if (SDSJ_PARTIAL_REFILL) {  // only the words not queued yet (q[0 .. nq) hold words wi .. wi + nq)
+          if (k >= b.nq) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+        } else {
+          b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
+        }
       }
     }
   } else {
