@@ -396,7 +396,7 @@ __device__ __forceinline__ void bits_init(BitsQ<Q>& b, const uint32_t* src, uint
 // SDSJ_FILL_X4: the kQ words as 16-byte loads (dword-aligned global_load_dwordx4: a quarter of the
 // load instructions, and of the per-lane cache-line requests, of one dword load per word)
 #ifndef SDSJ_FILL_X4
-#define SDSJ_FILL_X4 0
+#define SDSJ_FILL_X4 1
 #endif
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 template <int Q>
