@@ -1019,9 +1019,6 @@ constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides
 // Work unit = a group: 8 horizontally adjacent blocks of one component, one per thread, so each of
 // a block's 8 row stores joins the group's other 7 in 64 contiguous bytes of a plane row.  The
 // block stays in registers through both passes (64 values), so there is no LDS transpose.
-#ifndef SDSJ_IDCT_MCU
-#define SDSJ_IDCT_MCU 0  // 1: one thread per block of the needed MCU rectangle, in decode order (see k_idct)
-#endif
 #ifndef SDSJ_IDCT_WAVES
 #define SDSJ_IDCT_WAVES 4  // waves per SIMD the register budget targets (124 VGPRs at 4)
 #endif
@@ -1039,7 +1036,6 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   __shared__ int32_t cgx0[kMaxComp], cby0[kMaxComp];  // first 8-block group column / block row needed
   __shared__ float rngx[kMaxComp], rch[kMaxComp], rcv[kMaxComp];  // reciprocals for the exact quotients below
   __shared__ int64_t cplane[kMaxComp];
-  __shared__ int32_t mrect[4];  // needed MCU columns [0] .. [1] and rows [2] .. [3] (SDSJ_IDCT_MCU)
   const int t = threadIdx.x;
   const int ncomp = d->ncomp, bpm = d->bpm, mcux = d->mcux;
   // quantisation tables in zigzag order (the coefficient blocks' order)
@@ -1072,15 +1068,8 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
       rch[c] = 1.0f / (float)ch_[c];
       rcv[c] = 1.0f / (float)cv_[c];
       acc += x1 > x0 && y1 > y0 ? ngx[c] * ((cy1 >> 3) - cby0[c] + 1) : 0;
-      // (the MCUs holding those blocks, over all components)
-      const int m0 = (cx0 >> 3) / ch_[c], m1 = (cx1 >> 3) / ch_[c], n0 = (cy0 >> 3) / cv_[c], n1 = (cy1 >> 3) / cv_[c];
-      mrect[0] = c == 0 || m0 < mrect[0] ? m0 : mrect[0];
-      mrect[1] = c == 0 || m1 > mrect[1] ? m1 : mrect[1];
-      mrect[2] = c == 0 || n0 < mrect[2] ? n0 : mrect[2];
-      mrect[3] = c == 0 || n1 > mrect[3] ? n1 : mrect[3];
     }
     gstart[ncomp] = acc;
-    if (!(x1 > x0 && y1 > y0)) mrect[1] = mrect[0] - 1;  // nothing to transform
   }
   __syncthreads();
   const int lb = t & 7;  // this lane's block within its group
@@ -1124,25 +1113,10 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   // One block per lane, held in registers: dequantise, columns (pass 1), rows (pass 2), each row's 8
   // bytes stored straight to the plane -- no LDS transposes.  The 8 lanes of a group write 64
   // contiguous bytes of a plane row per store.
-#if SDSJ_IDCT_MCU
-  // One thread per block of the needed MCU rectangle in decode order: a wave's 64 coefficient blocks
-  // are consecutive in memory (8 KB read as one stream); its plane rows are written in 8-byte pieces
-  // that neighbouring lanes extend (16 bytes per MCU and luma row pair, merged in L2).
-  const int mw = mrect[1] - mrect[0] + 1, mh = mrect[3] - mrect[2] + 1;
-  const uint32_t nitems = mw > 0 && mh > 0 ? (uint32_t)(mw * mh * bpm) : 0u;
-  for (uint32_t it = blockIdx.x * kIdctThreads + t; it < nitems; it += gridDim.x * kIdctThreads) {
-    const uint32_t mcu = it / (uint32_t)bpm, mr = mcu / (uint32_t)mw;
-    const int b = (int)(it - mcu * (uint32_t)bpm);
-    const int mx = mrect[0] + (int)(mcu - mr * (uint32_t)mw), my = mrect[2] + (int)mr;
-    const int g = (my * mcux + mx) * bpm + b;
-    const int c = d->blk_comp[b];
-    const int bx = mx * ch_[c] + d->blk_dx[b], by = my * cv_[c] + d->blk_dy[b];
-#else
   for (int grp = blockIdx.x * (kIdctThreads / 8) + (t >> 3); grp < ngroups; grp += gridDim.x * (kIdctThreads / 8)) {
     int c, by, bx, g;
     locate(grp, c, by, bx, g);
     if (g < 0) continue;
-#endif
     // the block (zigzag order, k_entwrite / k_prog), or zeros where the entropy decoder left it zero
     const uint4* src = reinterpret_cast<const uint4*>(coef + (int64_t)g * 64);
     const bool zb = zero_block(g);
