@@ -3,7 +3,8 @@
 // horizontal and a vertical Pillow pass of KT taps (odd, 3..11).  Same arithmetic and the same
 // streaming structure as k_resample (sdsj_resample.hip, whose header describes the phases and the
 // reference lines), with the per-image geometry fixed at compile time where it matters:
-//   * the plane rows of the next step travel through registers (loads issued a whole step ahead);
+//   * the plane rows of the next step go straight to LDS (global_load_lds, issued once this step's
+//     conversion has read the staged rows; grayscale: through registers, its H pass reads them);
 //   * conversion is one flattened loop over (step row, 8-pixel group); each item reads its luma and
 //     chroma as aligned dwords from the staged rows and writes each channel's 8 pixels as 2 dwords
 //     (grayscale has no conversion: the horizontal taps read the staged luma rows, and one channel
@@ -245,9 +246,10 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
       }
       return p;
     };
-    // The next step's rows travel through registers (global loads issued before this step's
-    // conversion, written to LDS after its H/V work), so their latency hides behind a whole step.
-    // Wave wv holds staged rows wv, wv + 4, wv + 8 (<= 12 rows), 64 dwords per load.
+    // Grayscale: the next step's rows travel through registers (global loads issued before this
+    // step's H pass, written to LDS after it), so their latency hides behind a whole step.  Wave wv
+    // holds staged rows wv, wv + 4, wv + 8 (<= 12 rows), 64 dwords per load.  Colour layouts
+    // (kGlds): the same rows and lanes, loaded straight into LDS by issue_lds below.
     constexpr int kPR = (G::kRows + 3) / 4, kPC = (kMaxSpan / 4 + 2 + 63) / 64;
     constexpr bool kGlds = SDSJ_RS_GLDS && LAY != kRsGray;
     uint32_t pre[kPR][kPC];
