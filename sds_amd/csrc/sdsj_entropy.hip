@@ -335,21 +335,6 @@ constexpr int kRefillSpec = SDSJ_REFILL_SLACK ? 32 * (kSpecGroup + 1) : 27 * (kS
 // (fewer scattered 8-byte stores; profiles/r03d_ab.txt).
 constexpr int kRecStore = SDSJ_REC_STORE;
 static_assert(kRecStore <= kRec, "records fit their scratch");
-// Record k of subsequence j: at [j][k] (SDSJ_REC_T 0) or at [k][j] (1: the records of neighbouring
-// subsequences -- neighbouring lanes -- share cache lines, so their scattered 8-byte stores merge in L2
-// instead of each dirtying a line of its own).
-#ifndef SDSJ_REC_T
-#define SDSJ_REC_T 0
-#endif
-struct RecView {
-  SyncRec* base;
-  int64_t stride;  // elements between records k and k + 1
-  __device__ __forceinline__ const SyncRec& operator[](int k) const { return base[k * stride]; }
-  __device__ __forceinline__ void put(int k, uint2 v) const { reinterpret_cast<uint2*>(base)[k * stride] = v; }
-};
-__device__ __forceinline__ RecView rec_view(SyncRec* recs, int j, int nsub_cap) {
-  return SDSJ_REC_T ? RecView{recs + j, nsub_cap} : RecView{recs + (int64_t)j * kRec, 1};
-}
 constexpr int kRefillWrite = SDSJ_REFILL_SLACK ? 32 * (kWriteGroup + 1) : 27 * (kWriteGroup - 1) + 32;
 
 template <int Q>
@@ -643,20 +628,22 @@ using LdsSync = LdsSyncT<kEntThreads>;
 // block boundary at or after end_bit, recording every block boundary.  A segment's first
 // subsequence starts exactly at its (known) state.
 template <int LB, class TT>
-__device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const RecView rec,
-                         uint32_t seg_start, uint32_t warm) {
+// at: the subsequence is entered exactly at (at_p, MCU block at_blk) -- the speculative exit of its
+// predecessor, decoded by the same lane just before (paired subsequences) -- with no warm-up.
+__device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
+                         uint32_t seg_start, uint32_t warm, bool at = false, uint32_t at_p = 0, int at_blk = 0) {
   constexpr bool kMulti = std::is_same_v<TT, SpecTables>;  // LB = 11: the multi-symbol table
   // (bits at or beyond S.lim_bit read as zeros)
   const uint32_t start = S.start_bit, end = S.end_bit;
-  const uint32_t ws = S.first ? start : (start - seg_start > warm ? start - warm : seg_start);
+  const uint32_t ws = at ? at_p : (S.first ? start : (start - seg_start > warm ? start - warm : seg_start));
   Bits b;
   bits_init(b, src, ws, S.lim_bit);
-  int blk = 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
+  int blk = at ? at_blk : 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
   int d0 = 0, d1 = 0, d2 = 0;
-  int c = ctx_c(K, 0), sdc = ctx_dc(K, 0), sac = ctx_ac(K, 0);
-  uint32_t entry = start;
-  int entry_blk = 0;
-  bool warmup = b.pos < start;
+  int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
+  uint32_t entry = at ? at_p : start;
+  int entry_blk = blk;
+  bool warmup = !at && b.pos < start;
   // warm-up: only the MCU position matters (no values, no records): code length + size per symbol
   while (__builtin_amdgcn_ballot_w64(warmup)) {
     if (warmup) bits_fill(b);
@@ -718,7 +705,8 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           const bool done = next_z(z, s, r);
           if (done && nrec < kRecStore)  // one 8-byte store (SyncRec: p, dc, blk, pad)
-            rec.put(nrec, make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16)));
+            reinterpret_cast<uint2*>(rec)[nrec] =
+                make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
           // block end without branches: the sums, counters and the next block's context by selects
           add_dc(c, done ? dcd : 0, d0, d1, d2);
           nrec += done ? 1 : 0;
@@ -758,7 +746,7 @@ constexpr uint32_t kMergeBits = 768;
 constexpr int kSyncQ = kQ;  // (a deeper queue measured slower: the pull shifts it)
 
 template <int LB, class TT>
-__device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const RecView rec) {
+__device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, const SyncRec* rec) {
   const uint32_t end = S.end_bit;
   const int nrec = S.nrec;
   BitsQ<kSyncQ> b;
@@ -833,21 +821,25 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
 
 // The speculative pass's LDS: tables, the layout scan's scratch, statistics -- not the sync kernel's
 // task / scan arrays (5 KB that cost it two workgroups per CU)
-template <int LB>
+template <int LB, int NT>
 struct LdsSpec {
   std::conditional_t<LB == 11, SpecTables, LutTables> T;
-  int32_t tmp[kEntThreads];
+  int32_t tmp[NT];
   int32_t nsub;
   unsigned long long sym[1], it[1], t0, t1;
-  int32_t wmax[kEntThreads / 64];
+  int32_t wmax[NT / 64];
 };
 
-template <int LB>
+// NT threads per image: each lane takes kEntThreads / NT consecutive subsequences of the image's
+// kEntThreads-lane layout, the first after its warm-up, the next ones entered exactly at the
+// previous one's speculative exit (spec_pass `at`), so a pair shares one warm-up.
+template <int LB, int NT = kEntThreads>
 __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables,
                               uint8_t* __restrict__ scratch) {
+  constexpr int F = kEntThreads / NT;
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK) return;
-  __shared__ LdsSpec<LB> L;
+  __shared__ LdsSpec<LB, NT> L;
   const int t = threadIdx.x;
   int ns;
   if constexpr (LB == 11) ns = load_tables(L.T, &tables[img]);
@@ -868,7 +860,7 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   // --- subsequence layout: restart interval s (bytes [lo[s], hi[s])) -> max(1, ceil(bits / SB)) ---
   {
     int carry = 0;
-    for (int base = 0; base < nseg; base += kEntThreads) {
+    for (int base = 0; base < nseg; base += NT) {
       const int s = base + t;
       int cnt = 0;
       uint32_t b0 = 0, b1 = 0;
@@ -879,7 +871,7 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
         cnt = b1 > b0 ? (int)((b1 - b0 + SB - 1) / SB) : 1;
       }
       int total;
-      const int off = carry + block_excl_scan(cnt, L.tmp, &total);
+      const int off = carry + block_excl_scan<NT>(cnt, L.tmp, &total);
       if (s < nseg) {
         for (int k = 0; k < cnt; k++) {
           const int j = off + k;
@@ -907,9 +899,19 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   __syncthreads();
   // this workgroup's share of the subsequences (every group computes the same layout above)
   const int G = d->ent_groups, per = (nsub + G - 1) / G, j0 = grp * per, j1 = j0 + per < nsub ? j0 + per : nsub;
-  for (int j = j0 + t; j < j1; j += kEntThreads) {
-    const int k = spec_pass<LB>(L.T, K, src, sub[j], rec_view(recs, j, d->nsub_cap), (uint32_t)sv.lo[sub[j].seg] * 8u,
-                                (uint32_t)d->warm_bits);
+  for (int jb = j0 + F * t; jb < j1; jb += F * NT) {
+    int k = 0;
+#pragma unroll
+    for (int q = 0; q < F; q++) {
+      const int j = jb + q;
+      if (j >= j1) break;
+      // a later subsequence of the lane's run starts where the previous one stopped (same segment)
+      const bool at = q > 0 && !sub[j].first;
+      const uint32_t at_p = at ? sub[j - 1].spec_exit_p : 0u;
+      const int at_blk = at ? sub[j - 1].spec_exit_bz >> 8 : 0;
+      k += spec_pass<LB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec, (uint32_t)sv.lo[sub[j].seg] * 8u,
+                         (uint32_t)d->warm_bits, at, at_p, at_blk);
+    }
     if (kStats) {
       nsym_spec += k;
       atomicMax(&L.wmax[t >> 6], k);
@@ -918,7 +920,7 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   __syncthreads();
   if (kStats && t == 0) {
     L.t1 = __builtin_amdgcn_s_memtime();
-    for (int w = 0; w < kEntThreads / 64; w++) L.it[0] += 64ull * L.wmax[w];
+    for (int w = 0; w < NT / 64; w++) L.it[0] += 64ull * L.wmax[w];
   }
   if (kStats) atomicAdd(&L.sym[0], nsym_spec);
   __syncthreads();
@@ -992,7 +994,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       }
       for (int i = t; i < ntask; i += NT) {
         const int j = L.u.task[0][i];
-        const int k = sync_full<kSyncLB>(L.T, K, src, sub[j], rec_view(recs, j, d->nsub_cap));
+        const int k = sync_full<kSyncLB>(L.T, K, src, sub[j], recs + (int64_t)j * kRec);
         if (kStats) nsym_sync += k;
       }
       __syncthreads();
@@ -1305,9 +1307,9 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   }
 }
 
-template <int LB, int PHASE, int NTS = kSyncThreads>
+template <int LB, int PHASE, int NTS = kSyncThreads, int NSPEC = kEntThreads>
 __device__ __forceinline__ void ent_phase(int img, int grp, ImgDesc* descs, const EntTables* tables, uint8_t* scratch) {
-  if (PHASE == 0) entspec_image<LB>(img, grp, descs, tables, scratch);
+  if (PHASE == 0) entspec_image<LB, NSPEC>(img, grp, descs, tables, scratch);
   else if (PHASE == 1) entsync_image<LB, NTS>(img, descs, tables, scratch);
   else entwrite_image<LB>(img, grp, descs, tables, scratch);
 }
@@ -1317,7 +1319,7 @@ __device__ __forceinline__ void ent_phase(int img, int grp, ImgDesc* descs, cons
 // MODE 1: a small grid strides over the list and runs each image's groups in turn (LB = 10).  MODE 3:
 // (image, group) tasks of the LB = 11 images with ent_groups > 1, a grid of at most kTaskGrid
 // workgroups striding over them.  The sync pass is per image (MODE 0 for them too).
-template <int LB, int PHASE, int RT, int MODE, int NTS = kSyncThreads>
+template <int LB, int PHASE, int RT, int MODE, int NTS = kSyncThreads, int NSPEC = kEntThreads>
 __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables, uint8_t* scratch, int32_t* routes,
                                          int cap) {
   if (MODE == 3) {  // (image, group) tasks (k_plan's group_tasks list); a capped grid strides over them
@@ -1325,7 +1327,7 @@ __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables
     const int32_t* tasks = group_tasks(routes, cap);
     for (int k = blockIdx.x; k < nt; k += gridDim.x) {
       const int task = tasks[k];
-      ent_phase<LB, PHASE, NTS>(task >> kGroupShift, task & ((1 << kGroupShift) - 1), descs, tables, scratch);
+      ent_phase<LB, PHASE, NTS, NSPEC>(task >> kGroupShift, task & ((1 << kGroupShift) - 1), descs, tables, scratch);
       __syncthreads();  // LDS reuse by the next task
     }
     return;
@@ -1334,17 +1336,17 @@ __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables
   const int32_t* list = route_list(routes, cap, RT);
   if (MODE == 0) {
     if ((int)blockIdx.x >= cnt) return;
-    ent_phase<LB, PHASE, NTS>(list[blockIdx.x], 0, descs, tables, scratch);
+    ent_phase<LB, PHASE, NTS, NSPEC>(list[blockIdx.x], 0, descs, tables, scratch);
     return;
   }
   for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
     const int img = list[li];
     const int G = PHASE == 1 ? 1 : descs[img].ent_groups;
     if (MODE == 2) {
-      if ((int)blockIdx.y < G) ent_phase<LB, PHASE, NTS>(img, blockIdx.y, descs, tables, scratch);
+      if ((int)blockIdx.y < G) ent_phase<LB, PHASE, NTS, NSPEC>(img, blockIdx.y, descs, tables, scratch);
     } else {
       for (int grp = 0; grp < G; grp++) {
-        ent_phase<LB, PHASE, NTS>(img, grp, descs, tables, scratch);
+        ent_phase<LB, PHASE, NTS, NSPEC>(img, grp, descs, tables, scratch);
         __syncthreads();  // LDS reuse by the next group
       }
     }
@@ -1354,12 +1356,19 @@ __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables
 
 // k_entspec: subsequence layout + speculative pass (warm-up, records); k_entsync: sync rounds +
 // segmented scan, decode tables built only when some entry disagrees with its predecessor's exit.
-template <int LB, int RT, int MODE>
-__global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(LB == 11 ? SDSJ_SPEC_WAVES : 5)))
+template <int LB, int RT, int MODE, int NSPEC = kEntThreads>
+__global__ void __launch_bounds__(NSPEC) __attribute__((amdgpu_waves_per_eu(LB == 11 ? SDSJ_SPEC_WAVES : 5)))
 k_entspec(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, uint8_t* __restrict__ scratch,
           int32_t* __restrict__ routes, int cap) {
-  ent_feed<LB, 0, RT, MODE>(descs, tables, scratch, routes, cap);
+  ent_feed<LB, 0, RT, MODE, kSyncThreads, NSPEC>(descs, tables, scratch, routes, cap);
 }
+
+// Threads per image of the main route's speculative pass: kEntThreads / 2 = two subsequences per lane
+// and one warm-up per pair (SDSJ_SPEC_PAIR 1), or one each.
+#ifndef SDSJ_SPEC_PAIR
+#define SDSJ_SPEC_PAIR 0
+#endif
+constexpr int kSpecThreads = SDSJ_SPEC_PAIR ? kEntThreads / 2 : kEntThreads;
 
 // (multi-group images have several times the sync tasks: a 4-wave workgroup runs them)
 template <int LB, int RT, int MODE, int NTS>
@@ -1388,7 +1397,8 @@ hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* e
   if (route_on(rm, kRtEnt11) || route_on(rm, kRtEnt11M) || route_on(rm, kRtEnt10))
     hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
   if (route_on(rm, kRtEnt11))
-    hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+    hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0, kSpecThreads>), dim3(g), dim3(kSpecThreads), 0, s, descs, tables, scratch,
+                       routes, cap);
   if (route_on(rm, kRtEnt11M))
     hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3>), dim3(task_grid(n)), dim3(kEntThreads), 0, s, descs, tables,
                        scratch, routes, cap);
