@@ -1363,12 +1363,16 @@ k_entspec(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, uin
   ent_feed<LB, 0, RT, MODE, kSyncThreads, NSPEC>(descs, tables, scratch, routes, cap);
 }
 
-// Threads per image of the main route's speculative pass: kEntThreads / 2 = two subsequences per lane
-// and one warm-up per pair (SDSJ_SPEC_PAIR 1), or one each.
-#ifndef SDSJ_SPEC_PAIR
-#define SDSJ_SPEC_PAIR 0
+// Subsequences per lane of the speculative pass (one warm-up for the lane's run of them): the main
+// route (one workgroup per image, kEntThreads / SDSJ_SPEC_SUBS threads) and the multi-group route.
+#ifndef SDSJ_SPEC_SUBS
+#define SDSJ_SPEC_SUBS 2
 #endif
-constexpr int kSpecThreads = SDSJ_SPEC_PAIR ? kEntThreads / 2 : kEntThreads;
+#ifndef SDSJ_SPEC_SUBS_G
+#define SDSJ_SPEC_SUBS_G 1
+#endif
+constexpr int kSpecThreads = kEntThreads / SDSJ_SPEC_SUBS;
+constexpr int kSpecThreadsG = kEntThreads / SDSJ_SPEC_SUBS_G;
 
 // (multi-group images have several times the sync tasks: a 4-wave workgroup runs them)
 template <int LB, int RT, int MODE, int NTS>
@@ -1400,8 +1404,8 @@ hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* e
     hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0, kSpecThreads>), dim3(g), dim3(kSpecThreads), 0, s, descs, tables, scratch,
                        routes, cap);
   if (route_on(rm, kRtEnt11M))
-    hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3>), dim3(task_grid(n)), dim3(kEntThreads), 0, s, descs, tables,
-                       scratch, routes, cap);
+    hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3, kSpecThreadsG>), dim3(task_grid(n)), dim3(kSpecThreadsG), 0, s, descs,
+                       tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
     hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
