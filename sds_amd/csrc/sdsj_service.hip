@@ -10,9 +10,12 @@
 // previous ones ran), and copies each output into its worker's region before replying.
 //
 // Threads: the caller's thread reads requests (epoll over the listening socket and the clients) into
-// one queue; one thread per engine takes a batch from it, submits it, waits for it (hipEventSynchronize)
-// and answers its requests.  (A single thread polling every engine's event measured no overlap between
-// the engines' batches: 2 clients got the rate of 1.)
+// one queue; one thread per engine takes a batch from it, runs it on the engine's one stream (host
+// planning and H2D, kernels, status, then the D2H of the outputs) and answers its requests.  One stream
+// per engine matters: with the pipelined host path's second (copy) stream per engine, 8 streams shared
+// HIP's 4 hardware queues and the engines' batches ran one after another (16 clients: 3.8k images/s,
+// 10.0k with one stream each; profiles/r04_service.txt).  A single thread polling every engine's event
+// measured no overlap either.
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
