@@ -49,6 +49,17 @@ constexpr int kSmallBatch = 32;
 #endif
 constexpr int kLatSubBits = SDSJ_LAT_SUB;
 constexpr int kLatWarm = SDSJ_LAT_WARM;
+// Latency mode, multi-hypothesis (SDSJ_MH): every subsequence is decoded under each MCU phase
+// (bpm lanes) from a short warm-up (kMhWarm bits) instead of one lane from kLatWarm bits; the phase
+// whose entry matches its predecessor's exit is chosen afterwards (k_mh_select).
+#ifndef SDSJ_MH
+#define SDSJ_MH 0
+#endif
+#ifndef SDSJ_MH_WARM
+#define SDSJ_MH_WARM 512
+#endif
+constexpr int kMhWarm = SDSJ_MH_WARM;
+constexpr int kMhMaxPhases = 10;  // bpm <= 10 (D_MAX_BLOCKS_IN_MCU)
 // large images: ent_groups = ceil(bits / (kDecodeThreads x kGroupBits)) workgroups (<= kMaxEntGroups)
 // share the subsequences, so one lane's serial decode stays near kGroupBits
 #ifndef SDSJ_GROUP_BITS
@@ -199,7 +210,8 @@ struct ImgDesc {
   // last scan ran out of data in row sm_good: jdcoefct.c last_good_iMCU_row)
   int32_t smooth, sm_good;
   int8_t sm_bits[2][kMaxComp][10];
-  int8_t sm_pad[4];
+  int8_t mh;  // latency mode: the multi-hypothesis speculative pass (k_entspec_mh) takes the image
+  int8_t sm_pad[3];
 };
 
 // One tile of k_unstuff's first pass: bytes it emits and split markers (RSTn, codes below SOF0) it

@@ -209,7 +209,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, bool small, const uint8_t* d
   // (after mark 3: the next lane may start while this lane's progressive images decode)
   SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s, rm));
   mark(4);
-  SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s, rm, small));
   mark(5);
   SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
   mark(6);

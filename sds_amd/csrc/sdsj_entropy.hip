@@ -630,15 +630,18 @@ using LdsSync = LdsSyncT<kEntThreads>;
 template <int LB, class TT>
 // at: the subsequence is entered exactly at (at_p, MCU block at_blk) -- the speculative exit of its
 // predecessor, decoded by the same lane just before (paired subsequences) -- with no warm-up.
+// init_blk: the MCU block the warm-up assumes at its first bit (k_entspec_mh's phase hypotheses; 0
+// otherwise); keep_rec: store block-boundary records.
 __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubState& S, SyncRec* rec,
-                         uint32_t seg_start, uint32_t warm, bool at = false, uint32_t at_p = 0, int at_blk = 0) {
+                         uint32_t seg_start, uint32_t warm, bool at = false, uint32_t at_p = 0, int at_blk = 0,
+                         int init_blk = 0, bool keep_rec = true) {
   constexpr bool kMulti = std::is_same_v<TT, SpecTables>;  // LB = 11: the multi-symbol table
   // (bits at or beyond S.lim_bit read as zeros)
   const uint32_t start = S.start_bit, end = S.end_bit;
   const uint32_t ws = at ? at_p : (S.first ? start : (start - seg_start > warm ? start - warm : seg_start));
   Bits b;
   bits_init(b, src, ws, S.lim_bit);
-  int blk = at ? at_blk : 0, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
+  int blk = at ? at_blk : init_blk, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
   int d0 = 0, d1 = 0, d2 = 0;
   int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
   uint32_t entry = at ? at_p : start;
@@ -704,7 +707,7 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
           const bool done = next_z(z, s, r);
-          if (done && nrec < kRecStore)  // one 8-byte store (SyncRec: p, dc, blk, pad)
+          if (keep_rec && done && nrec < kRecStore)  // one 8-byte store (SyncRec: p, dc, blk, pad)
             reinterpret_cast<uint2*>(rec)[nrec] =
                 make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
           // block end without branches: the sums, counters and the next block's context by selects
@@ -838,7 +841,7 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
                               uint8_t* __restrict__ scratch) {
   constexpr int F = kEntThreads / NT;
   ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK) return;
+  if (d->status != SDSJ_OK || d->mh) return;  // (mh: k_entspec_mh + k_mh_select)
   __shared__ LdsSpec<LB, NT> L;
   const int t = threadIdx.x;
   int ns;
@@ -1388,13 +1391,168 @@ __global__ void __launch_bounds__(kEntThreads) k_entwrite(ImgDesc* __restrict__ 
   ent_feed<LB, 2, RT, MODE>(descs, tables, scratch, routes, cap);
 }
 
+// ------------------------------------------------------------------------------------------
+// Latency mode, multi-hypothesis speculative pass (ImgDesc::mh: one image per call, no restart
+// intervals).  A lane's speculative decode locks on to the true MCU phase only after ~1k bits (its
+// Huffman codes self-synchronise within ~100 bits, the block phase much later), hence kLatWarm bits
+// of warm-up per subsequence -- 80 % of a lane's serial chain.  Here each subsequence j is decoded by
+// bpm lanes, lane h assuming MCU block h at its warm-up's first bit, from only kMhWarm bits before the
+// subsequence: the lane whose assumption was right has re-aligned its codes and its coefficient index
+// by the subsequence's start (at the first end of block), so its entry is the true one.  k_mh_select
+// then picks per subsequence the phase whose entry equals the chosen predecessor's exit (a scan of
+// phase maps), and k_entsync re-decodes the rare subsequences where none did.
+// ------------------------------------------------------------------------------------------
+struct MhRes {  // one (subsequence, phase) lane's speculative result (scratch at off_rec, unused by mh images)
+  uint32_t entry_p, exit_p;
+  uint16_t entry_bz, exit_bz;
+  int32_t nblk;
+  int32_t dc[kMaxComp];
+  int32_t pad;
+};
+static_assert(sizeof(MhRes) * kMhMaxPhases <= sizeof(SyncRec) * kRec, "MhRes fit a subsequence's record scratch");
+
+// The mh image's subsequences (one segment): [b0 + j SB, min(b0 + (j + 1) SB, b1)).
+struct MhLayout {
+  uint32_t b0, b1, sb;
+  int nsub;
+};
+__device__ __forceinline__ MhLayout mh_layout(const ImgDesc* d, const SegView& sv) {
+  MhLayout m;
+  m.b0 = (uint32_t)sv.lo[0] * 8u;
+  m.b1 = (uint32_t)sv.hi[0] * 8u;
+  if (m.b1 < m.b0) m.b1 = m.b0;
+  m.sb = (uint32_t)d->sub_bits;
+  const int cnt = m.b1 > m.b0 ? (int)((m.b1 - m.b0 + m.sb - 1) / m.sb) : 1;
+  m.nsub = cnt < d->nsub_cap ? cnt : d->nsub_cap;
+  return m;
+}
+
+template <int RT>
+__global__ void __launch_bounds__(kEntThreads) __attribute__((amdgpu_waves_per_eu(SDSJ_SPEC_WAVES)))
+k_entspec_mh(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, uint8_t* __restrict__ scratch,
+             int32_t* __restrict__ routes, int cap) {
+  if ((int)blockIdx.x >= routes[RT]) return;
+  const int img = route_list(routes, cap, RT)[blockIdx.x];
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || !d->mh) return;
+  __shared__ LdsSpec<11, kEntThreads> L;
+  if (!variant_owns<11>(load_tables(L.T, &tables[img]))) return;
+  const BlkCtx K = make_ctx(L.T, d->bpm);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+  MhRes* res = reinterpret_cast<MhRes*>(scratch + d->off_rec);
+  const MhLayout m = mh_layout(d, sv);
+  const int H = d->bpm;
+  for (int i = blockIdx.y * kEntThreads + threadIdx.x; i < m.nsub * H; i += gridDim.y * kEntThreads) {
+    const int j = i / H, h = i - j * H;
+    MhRes r{};
+    if (j > 0 || h == 0) {  // (the first subsequence starts exactly: block 0)
+      SubState S;
+      S.start_bit = m.b0 + (uint32_t)j * m.sb;
+      const uint32_t e = S.start_bit + m.sb;
+      S.end_bit = e < m.b1 ? e : m.b1;
+      S.first = j == 0;
+      S.seg = 0;
+      S.lim_bit = m.b1;
+      spec_pass<11>(L.T, K, src, S, nullptr, m.b0, (uint32_t)kMhWarm, false, 0u, 0, h, false);
+      r.entry_p = S.entry_p;
+      r.entry_bz = S.entry_bz;
+      r.exit_p = S.spec_exit_p;
+      r.exit_bz = S.spec_exit_bz;
+      r.nblk = S.spec_nblk;
+      for (int c = 0; c < kMaxComp; c++) r.dc[c] = S.spec_dc[c];
+    }
+    res[i] = r;
+  }
+}
+
+// Per image (one workgroup): f_j(x) = the phase of subsequence j whose entry equals the exit of phase x
+// of subsequence j - 1 (0 when none does: k_entsync re-decodes it); F_j = f_j o ... o f_1 from phase 0
+// of subsequence 0 (an inclusive scan of maps: 4 bits per phase), j's phase = F_j(0).  Writes the
+// chosen results into the SubStates as the speculative pass would (no records).
+constexpr int kMhChunk = 2048;  // subsequences per scan chunk (LDS)
+__device__ __forceinline__ uint64_t mh_compose(uint64_t later, uint64_t earlier, int H) {
+  uint64_t r = 0;
+  for (int x = 0; x < H; x++) r |= ((later >> (4 * ((earlier >> (4 * x)) & 15))) & 15) << (4 * x);
+  return r;
+}
+
+template <int RT>
+__global__ void __launch_bounds__(kEntThreads) k_mh_select(ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
+                                                           int32_t* __restrict__ routes, int cap) {
+  if ((int)blockIdx.x >= routes[RT]) return;
+  const int img = route_list(routes, cap, RT)[blockIdx.x];
+  ImgDesc* d = &descs[img];
+  if (d->status != SDSJ_OK || !d->mh) return;
+  __shared__ uint64_t F[kMhChunk];
+  __shared__ uint64_t carry;
+  const int t = threadIdx.x;
+  const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
+  const MhRes* res = reinterpret_cast<const MhRes*>(scratch + d->off_rec);
+  SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
+  const MhLayout m = mh_layout(d, sv);
+  const int H = d->bpm;
+  if (t == 0) carry = 0;  // F_{-1}: every phase -> 0 (subsequence 0 is entered exactly)
+  __syncthreads();
+  for (int c0 = 0; c0 < m.nsub; c0 += kMhChunk) {
+    const int nc = m.nsub - c0 < kMhChunk ? m.nsub - c0 : kMhChunk;
+    for (int k = t; k < nc; k += kEntThreads) {
+      const int j = c0 + k;
+      uint64_t f = 0;
+      if (j > 0)
+        for (int x = 0; x < H; x++) {
+          const MhRes& p = res[(j - 1) * H + x];
+          int pick = 0;
+          for (int h = H - 1; h >= 0; h--) {
+            const MhRes& q = res[j * H + h];
+            pick = (q.entry_p == p.exit_p && q.entry_bz == p.exit_bz) ? h : pick;
+          }
+          f |= (uint64_t)pick << (4 * x);
+        }
+      F[k] = f;
+    }
+    __syncthreads();
+    for (int off = 1; off < nc; off <<= 1) {  // inclusive scan: F[k] = F[k] o F[k - off]
+      uint64_t v[kMhChunk / kEntThreads];
+      for (int k = t, n = 0; k < nc; k += kEntThreads, n++) v[n] = k >= off ? mh_compose(F[k], F[k - off], H) : F[k];
+      __syncthreads();
+      for (int k = t, n = 0; k < nc; k += kEntThreads, n++) F[k] = v[n];
+      __syncthreads();
+    }
+    const uint64_t cin = carry;
+    for (int k = t; k < nc; k += kEntThreads) {
+      const int j = c0 + k;
+      const int h = j == 0 ? 0 : (int)((mh_compose(F[k], cin, H) >> 0) & 15);  // F_j(0)
+      const MhRes& r = res[j * H + h];
+      SubState& S = sub[j];
+      S.start_bit = m.b0 + (uint32_t)j * m.sb;
+      const uint32_t e = S.start_bit + m.sb;
+      S.end_bit = e < m.b1 ? e : m.b1;
+      S.first = j == 0;
+      S.seg = 0;
+      S.lim_bit = m.b1;
+      S.entry_p = r.entry_p;
+      S.entry_bz = r.entry_bz;
+      S.spec_exit_p = S.cur_exit_p = r.exit_p;
+      S.spec_exit_bz = S.cur_exit_bz = r.exit_bz;
+      S.spec_nblk = S.cur_nblk = r.nblk;
+      for (int c = 0; c < kMaxComp; c++) S.spec_dc[c] = S.cur_dc[c] = r.dc[c];
+      S.nrec = 0;
+    }
+    __syncthreads();
+    if (t == 0) carry = mh_compose(F[nc - 1], cin, H);
+    __syncthreads();
+  }
+  if (t == 0) d->nsub = m.nsub;
+}
+
 size_t enttab_bytes() { return sizeof(EntTables); }
 
 constexpr int kTaskGrid = 4096;  // MODE 3 grid cap (>= the workgroups the chip holds at once)
 static int task_grid(int n) { return n * kMaxEntGroups < kTaskGrid ? n * kMaxEntGroups : kTaskGrid; }
 
 hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s, uint64_t rm) {
+                          int cap, hipStream_t s, uint64_t rm, bool small) {
   const int g = n;  // one workgroup per image on the main route
   EntTables* tables = static_cast<EntTables*>(etab);
   const int gs = g < 256 ? g : 256;
@@ -1408,6 +1566,17 @@ hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* e
                        tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
     hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+  if (SDSJ_MH && small) {  // latency-mode images (ImgDesc::mh; the kernels above skip them)
+    constexpr int kMhGridY = 64;
+    if (route_on(rm, kRtEnt11)) {
+      hipLaunchKernelGGL(k_entspec_mh<kRtEnt11>, dim3(n, kMhGridY), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+      hipLaunchKernelGGL(k_mh_select<kRtEnt11>, dim3(n), dim3(kEntThreads), 0, s, descs, scratch, routes, cap);
+    }
+    if (route_on(rm, kRtEnt11M)) {
+      hipLaunchKernelGGL(k_entspec_mh<kRtEnt11M>, dim3(n, kMhGridY), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+      hipLaunchKernelGGL(k_mh_select<kRtEnt11M>, dim3(n), dim3(kEntThreads), 0, s, descs, scratch, routes, cap);
+    }
+  }
   return hipGetLastError();
 }
 

@@ -27,8 +27,9 @@ hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* 
                        uint64_t rm = kAllRoutes);
 size_t enttab_bytes();  // per-image decode tables (k_enttab) held in HBM between the entropy kernels
 // k_enttab (decode tables) + k_entspec (subsequence layout, warm-up, speculative decode)
+// (small: a host-path latency-mode chunk, where ImgDesc::mh images take the multi-hypothesis pass)
 hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s, uint64_t rm = kAllRoutes);
+                          int cap, hipStream_t s, uint64_t rm = kAllRoutes, bool small = false);
 // k_entsync (sync rounds + segmented scan)
 hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, int32_t* routes, int cap, hipStream_t s,
                           uint64_t rm = kAllRoutes);

@@ -150,6 +150,8 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
     }
   }
   d->lat = small && !frames;
+  // multi-hypothesis speculative pass for latency-mode baseline images without restart intervals
+  d->mh = (int8_t)(SDSJ_MH && d->lat && !d->progressive && d->restart_interval == 0 && d->bpm <= kMhMaxPhases);
   {
     const int64_t bits = d->entropy_len * 8;
     const int64_t per_group = (int64_t)kDecodeThreads * (d->lat ? kLatSubBits : kGroupBits);
