@@ -1469,13 +1469,15 @@ k_entspec_mh(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, 
 // Per image (one workgroup): f_j(x) = the phase of subsequence j whose entry equals the exit of phase x
 // of subsequence j - 1 (0 when none does: k_entsync re-decodes it); F_j = f_j o ... o f_1 from phase 0
 // of subsequence 0 (an inclusive scan of maps: 4 bits per phase), j's phase = F_j(0).  Writes the
-// chosen results into the SubStates as the speculative pass would (no records).
-constexpr int kMhChunk = 2048;  // subsequences per scan chunk (LDS)
+// chosen results into the SubStates as the speculative pass would (no records).  The lanes' entries
+// and exits are staged in LDS by chunks of kMhStage (subsequence, phase) pairs.
+constexpr int kMhStage = 3072;
 __device__ __forceinline__ uint64_t mh_compose(uint64_t later, uint64_t earlier, int H) {
   uint64_t r = 0;
   for (int x = 0; x < H; x++) r |= ((later >> (4 * ((earlier >> (4 * x)) & 15))) & 15) << (4 * x);
   return r;
 }
+__device__ __forceinline__ uint64_t mh_key(uint32_t p, uint16_t bz) { return ((uint64_t)p << 16) | bz; }
 
 template <int RT>
 __global__ void __launch_bounds__(kEntThreads) k_mh_select(ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
@@ -1484,36 +1486,42 @@ __global__ void __launch_bounds__(kEntThreads) k_mh_select(ImgDesc* __restrict__
   const int img = route_list(routes, cap, RT)[blockIdx.x];
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || !d->mh) return;
-  __shared__ uint64_t F[kMhChunk];
-  __shared__ uint64_t carry;
+  __shared__ uint64_t ent[kMhStage], ext[kMhStage], F[kMhStage];
+  __shared__ uint8_t pick[kMhStage];
+  __shared__ uint64_t carry, prev_ext[kMhMaxPhases];
   const int t = threadIdx.x;
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
   const MhRes* res = reinterpret_cast<const MhRes*>(scratch + d->off_rec);
   SubState* sub = reinterpret_cast<SubState*>(scratch + d->off_sub);
   const MhLayout m = mh_layout(d, sv);
-  const int H = d->bpm;
+  const int H = d->bpm, cs = kMhStage / H;
   if (t == 0) carry = 0;  // F_{-1}: every phase -> 0 (subsequence 0 is entered exactly)
-  __syncthreads();
-  for (int c0 = 0; c0 < m.nsub; c0 += kMhChunk) {
-    const int nc = m.nsub - c0 < kMhChunk ? m.nsub - c0 : kMhChunk;
+  for (int c0 = 0; c0 < m.nsub; c0 += cs) {
+    const int nc = m.nsub - c0 < cs ? m.nsub - c0 : cs;
+    for (int i = t; i < nc * H; i += kEntThreads) {
+      const MhRes& r = res[c0 * H + i];
+      ent[i] = mh_key(r.entry_p, r.entry_bz);
+      ext[i] = mh_key(r.exit_p, r.exit_bz);
+    }
+    __syncthreads();
+    for (int i = t; i < nc * H; i += kEntThreads) {  // pair (k, x): the phase of k entered from phase x of k - 1
+      const int k = i / H, x = i - k * H, j = c0 + k;
+      int pk = 0;
+      if (j > 0) {
+        const uint64_t pe = k > 0 ? ext[(k - 1) * H + x] : prev_ext[x];
+        for (int h = H - 1; h >= 0; h--) pk = ent[k * H + h] == pe ? h : pk;
+      }
+      pick[i] = (uint8_t)pk;
+    }
+    __syncthreads();
     for (int k = t; k < nc; k += kEntThreads) {
-      const int j = c0 + k;
       uint64_t f = 0;
-      if (j > 0)
-        for (int x = 0; x < H; x++) {
-          const MhRes& p = res[(j - 1) * H + x];
-          int pick = 0;
-          for (int h = H - 1; h >= 0; h--) {
-            const MhRes& q = res[j * H + h];
-            pick = (q.entry_p == p.exit_p && q.entry_bz == p.exit_bz) ? h : pick;
-          }
-          f |= (uint64_t)pick << (4 * x);
-        }
+      for (int x = 0; x < H; x++) f |= (uint64_t)pick[k * H + x] << (4 * x);
       F[k] = f;
     }
     __syncthreads();
     for (int off = 1; off < nc; off <<= 1) {  // inclusive scan: F[k] = F[k] o F[k - off]
-      uint64_t v[kMhChunk / kEntThreads];
+      uint64_t v[kMhStage / kEntThreads];
       for (int k = t, n = 0; k < nc; k += kEntThreads, n++) v[n] = k >= off ? mh_compose(F[k], F[k - off], H) : F[k];
       __syncthreads();
       for (int k = t, n = 0; k < nc; k += kEntThreads, n++) F[k] = v[n];
@@ -1522,7 +1530,7 @@ __global__ void __launch_bounds__(kEntThreads) k_mh_select(ImgDesc* __restrict__
     const uint64_t cin = carry;
     for (int k = t; k < nc; k += kEntThreads) {
       const int j = c0 + k;
-      const int h = j == 0 ? 0 : (int)((mh_compose(F[k], cin, H) >> 0) & 15);  // F_j(0)
+      const int h = j == 0 ? 0 : (int)(mh_compose(F[k], cin, H) & 15);  // F_j(0)
       const MhRes& r = res[j * H + h];
       SubState& S = sub[j];
       S.start_bit = m.b0 + (uint32_t)j * m.sb;
@@ -1541,6 +1549,7 @@ __global__ void __launch_bounds__(kEntThreads) k_mh_select(ImgDesc* __restrict__
     }
     __syncthreads();
     if (t == 0) carry = mh_compose(F[nc - 1], cin, H);
+    if (t < H) prev_ext[t] = ext[(nc - 1) * H + t];
     __syncthreads();
   }
   if (t == 0) d->nsub = m.nsub;
