@@ -53,10 +53,10 @@ constexpr int kLatWarm = SDSJ_LAT_WARM;
 // (bpm lanes) from a short warm-up (kMhWarm bits) instead of one lane from kLatWarm bits; the phase
 // whose entry matches its predecessor's exit is chosen afterwards (k_mh_select).
 #ifndef SDSJ_MH
-#define SDSJ_MH 0
+#define SDSJ_MH 1
 #endif
 #ifndef SDSJ_MH_WARM
-#define SDSJ_MH_WARM 512
+#define SDSJ_MH_WARM 2048
 #endif
 constexpr int kMhWarm = SDSJ_MH_WARM;
 constexpr int kMhMaxPhases = 10;  // bpm <= 10 (D_MAX_BLOCKS_IN_MCU)
