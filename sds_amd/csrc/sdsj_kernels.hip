@@ -626,17 +626,47 @@ __device__ __forceinline__ int us_byte(const UsClass& c, int k) {
   for (int q = 0; q < 8; q++) dw = q == (k >> 2) ? c.u[1 + q] : dw;
   return (int)(dw >> (8 * (k & 3))) & 0xFF;
 }
-// The ten dwords holding bytes [my0 - 4, my0 + 32), all loads issued together.  A dword past the
-// input reads the last one (same page): bytes past the input are never emitted (us_classify's vmask),
-// so their values do not matter.  The 4 bytes before the entropy-coded data are header bytes.
+// Bytes past the input are never emitted (us_classify's vmask), so their values do not matter; the 4
+// bytes before the entropy-coded data are header bytes.
 struct UsRaw {
   uint32_t v[10];
 };
+// The ten dwords holding bytes [my0 - 4, my0 + 32), from four aligned 16-byte loads covering them:
+// (e + my0) & 15 is the same for every thread of the image (tiles and threads start at multiples of
+// 16), so the ten dwords sit at a wave-uniform offset into the sixteen loaded.  (Ten dword loads at a
+// 32-byte lane stride measured 1.5x slower in k_us_count, profiles/r04_ab.txt.)  Chunks past the one
+// holding the input's last byte read that one (same page); a chunk before the one holding byte -4
+// (only for my0 = 0 and (e & 15) >= 4, and then unused) reads that one, so nothing before the image's
+// headers is touched.  Loads go through the global address space as a native vector (HIP's uint4
+// struct is loaded as flat, and flat loads also count on lgkmcnt, i.e. on every LDS wait).
+typedef uint32_t us_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void us_load(const uint8_t* e, int64_t L, int64_t my0, UsRaw& r) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(((uintptr_t)(e + my0) & ~(uintptr_t)3) - 4);
-  const uint32_t* last = reinterpret_cast<const uint32_t*>(((uintptr_t)(e + L) - 1) & ~(uintptr_t)3);
+  const uintptr_t a = (uintptr_t)(e + my0) & 15;
+  const us_u32x4* A = reinterpret_cast<const us_u32x4*>((uintptr_t)(e + my0) - a - 16);
+  const us_u32x4* first = reinterpret_cast<const us_u32x4*>(((uintptr_t)e - 4) & ~(uintptr_t)15);
+  const us_u32x4* last = reinterpret_cast<const us_u32x4*>(((uintptr_t)(e + L) - 1) & ~(uintptr_t)15);
+  uint32_t D[16];
 #pragma unroll
-  for (int k = 0; k < 10; k++) r.v[k] = *(w + k < last ? w + k : last);
+  for (int i = 0; i < 4; i++) {
+    const us_u32x4* p = A + i < first ? first : A + i;
+    const us_u32x4 q = *(const __attribute__((address_space(1))) us_u32x4*)(p < last ? p : last);
+    D[4 * i] = q.x;
+    D[4 * i + 1] = q.y;
+    D[4 * i + 2] = q.z;
+    D[4 * i + 3] = q.w;
+  }
+  switch (__builtin_amdgcn_readfirstlane((int)(a >> 2))) {  // (uniform: static register indices)
+#define US_CASE(S)                                                       \
+  case S:                                                                \
+    _Pragma("unroll") for (int k = 0; k < 10; k++) r.v[k] = D[S + 3 + k]; \
+    break;
+    US_CASE(0)
+    US_CASE(1)
+    US_CASE(2)
+    default:
+    US_CASE(3)
+#undef US_CASE
+  }
 }
 __device__ __forceinline__ void us_classify(const uint8_t* e, int64_t L, int64_t my0, const UsRaw& r, UsClass& c) {
   const int sh = (int)((uintptr_t)(e + my0) & 3);
