@@ -1522,9 +1522,16 @@ hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* b
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           const int32_t* routes, int cap, hipStream_t s, uint64_t rm) {
   const int g = n < kUsLaunch ? n : kUsLaunch;
-  const int gt = n * kUsGrid < 4 * kUsLaunch ? n * kUsGrid : 4 * kUsLaunch;
+#ifndef SDSJ_US_TILE_GRID
+#define SDSJ_US_TILE_GRID 16384
+#endif
+  const int gt = n * kUsGrid < SDSJ_US_TILE_GRID ? n * kUsGrid : SDSJ_US_TILE_GRID;
+#ifndef SDSJ_US_SERIAL_GRID
+#define SDSJ_US_SERIAL_GRID 16384
+#endif
+  const int gs = n < SDSJ_US_SERIAL_GRID ? n : SDSJ_US_SERIAL_GRID;
   if (route_on(rm, kRtUsSmall))
-    hipLaunchKernelGGL(k_us_serial, dim3(g), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
+    hipLaunchKernelGGL(k_us_serial, dim3(gs), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
   if (route_on(rm, kRtUsBig)) {
     hipLaunchKernelGGL(k_us_count, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
     hipLaunchKernelGGL(k_us_scan, dim3(g), dim3(kUnstuffThreads), 0, s, descs, scratch, routes, cap);

@@ -5,7 +5,7 @@
 # usage: tools/us_ab.sh name ...
 set -e
 mkdir -p gpurun_out
-for w in vga256 mixed512; do
+for w in ${US_WORKLOADS:-vga256 mixed512}; do
   for v in product "$@"; do
     if [ "$v" = product ]; then unset SDSJ_LIBRARY; else export SDSJ_LIBRARY=sds_amd/lib/exp/libsdsj_$v.so; fi
     tools/prof_quick.sh us_${v}_$w --workload $w > gpurun_out/us_${v}_$w.txt
