@@ -1047,6 +1047,15 @@ constexpr int kIdctThreads = 256;
 #define SDSJ_IDCT_GRID 8
 #endif
 constexpr int kIdctGrid = SDSJ_IDCT_GRID;  // workgroups per image (each strides over 8-block groups)
+// SDSJ_IDCT_GPW > 0 (0: kIdctGrid per image): batch launches take kIdctGridMax workgroups per image and an image uses
+// ceil(total_blocks / 8 / SDSJ_IDCT_GPW) of them (1 .. kIdctGridMax; the rest exit at once), so a
+// workgroup's setup is amortised over about the same number of groups whatever the image size.
+#ifndef SDSJ_IDCT_GPW
+#define SDSJ_IDCT_GPW 256
+#endif
+// (odd: workgroup k of the launch runs on XCD k mod 8, so with a grid row of 16 every image's first
+// workgroups would land on the same XCDs; 17 rotates them by one XCD per image)
+constexpr int kIdctGridMax = 17;
 
 // Work unit = a group: 8 horizontally adjacent blocks of one component, one per thread, so each of
 // a block's 8 row stores joins the group's other 7 in 64 contiguous bytes of a plane row.  The
@@ -1062,6 +1071,12 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   if (img >= n) return;
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->geo == kGeoZeros) return;
+  int nwg = gridDim.x;  // this image's workgroups
+  if (SDSJ_IDCT_GPW > 0 && gridDim.x == kIdctGridMax) {
+    const int64_t want = ((int64_t)d->total_blocks / 8 + SDSJ_IDCT_GPW - 1) / SDSJ_IDCT_GPW;
+    nwg = want < 1 ? 1 : (want > kIdctGridMax ? kIdctGridMax : (int)want);
+    if ((int)blockIdx.x >= nwg) return;
+  }
   __shared__ alignas(16) int32_t qt[kMaxComp][64];
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
   __shared__ int32_t gstart[kMaxComp + 1], ngx[kMaxComp], cbw[kMaxComp], ch_[kMaxComp], cv_[kMaxComp], cpitch[kMaxComp];
@@ -1145,7 +1160,7 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   // One block per lane, held in registers: dequantise, columns (pass 1), rows (pass 2), each row's 8
   // bytes stored straight to the plane -- no LDS transposes.  The 8 lanes of a group write 64
   // contiguous bytes of a plane row per store.
-  for (int grp = blockIdx.x * (kIdctThreads / 8) + (t >> 3); grp < ngroups; grp += gridDim.x * (kIdctThreads / 8)) {
+  for (int grp = blockIdx.x * (kIdctThreads / 8) + (t >> 3); grp < ngroups; grp += nwg * (kIdctThreads / 8)) {
     int c, by, bx, g;
     locate(grp, c, by, bx, g);
     if (g < 0) continue;
@@ -1554,7 +1569,7 @@ hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, Im
 }
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s) {
   // (a few images: more workgroups per image, for latency)
-  hipLaunchKernelGGL(k_idct, dim3(n <= kSmallBatch ? 8 * kIdctGrid : kIdctGrid, n), dim3(kIdctThreads), 0, s, n, descs,
+  hipLaunchKernelGGL(k_idct, dim3(n <= kSmallBatch ? 8 * kIdctGrid : (SDSJ_IDCT_GPW > 0 ? kIdctGridMax : kIdctGrid), n), dim3(kIdctThreads), 0, s, n, descs,
                      tables, scratch);
   return hipGetLastError();
 }
