@@ -754,13 +754,15 @@ __device__ __forceinline__ int decode_progressive(ImgDesc* d, ImgTables* t, cons
 // Zeroes the coefficient arrays of the progressive images (scans accumulate into them).
 __global__ void __launch_bounds__(256) k_prog_zero(const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
                                                    const int32_t* __restrict__ routes, int cap) {
-  if ((int)blockIdx.x >= routes[kRtProg]) return;
-  const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[blockIdx.x]];
-  if (d->status != SDSJ_OK) return;
-  uint4* p = reinterpret_cast<uint4*>(scratch + d->off_coef);
-  const int64_t n16 = d->total_blocks * 8;
-  for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.y * 256)
-    p[i] = make_uint4(0, 0, 0, 0);
+  const int cnt = routes[kRtProg];
+  for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
+    const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[li]];
+    if (d->status != SDSJ_OK) continue;
+    uint4* p = reinterpret_cast<uint4*>(scratch + d->off_coef);
+    const int64_t n16 = d->total_blocks * 8;
+    for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.y * 256)
+      p[i] = make_uint4(0, 0, 0, 0);
+  }
 }
 
 // The DC plane of the progressive images to be smoothed (int16 per block, decode order) in their
@@ -768,13 +770,15 @@ __global__ void __launch_bounds__(256) k_prog_zero(const ImgDesc* __restrict__ d
 // while it rewrites blocks in place.  (Blocks stay in zigzag order: k_idct reads that order.)
 __global__ void __launch_bounds__(256) k_prog_dcs(const ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
                                                   const int32_t* __restrict__ routes, int cap) {
-  if ((int)blockIdx.x >= routes[kRtProg]) return;
-  const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[blockIdx.x]];
-  if (d->status != SDSJ_OK || !d->smooth) return;
-  const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
-  int16_t* dcs = reinterpret_cast<int16_t*>(scratch + d->off_planes);
-  const int64_t nb = d->total_blocks;
-  for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < nb; i += (int64_t)gridDim.y * 256) dcs[i] = coef[i * 64];
+  const int cnt = routes[kRtProg];
+  for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
+    const ImgDesc* d = &descs[route_list(routes, cap, kRtProg)[li]];
+    if (d->status != SDSJ_OK || !d->smooth) continue;
+    const int16_t* coef = reinterpret_cast<const int16_t*>(scratch + d->off_coef);
+    int16_t* dcs = reinterpret_cast<int16_t*>(scratch + d->off_planes);
+    const int64_t nb = d->total_blocks;
+    for (int64_t i = (int64_t)blockIdx.y * 256 + threadIdx.x; i < nb; i += (int64_t)gridDim.y * 256) dcs[i] = coef[i * 64];
+  }
 }
 
 // pred = num / (Q << 8) rounded half away from zero, clamped below 2^Al when Al > 0
@@ -793,12 +797,19 @@ __device__ __forceinline__ int smooth_pred(int64_t num, int64_t q, int al) {
 // plane area -- libjpeg likewise reads the neighbours unmodified while it smooths a copy of the block.
 // Rows: jdcoefct.c's per-iMCU-row choice (the last iMCU row's real rows only); columns clamped to the
 // component's width in blocks (tests/test_gpu_parity.py: bit-exact against the Pillow-pinned CPU restatement).
+__device__ void prog_smooth_image(int img, const ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
+                                  uint8_t* __restrict__ scratch);
 __global__ void __launch_bounds__(256) k_prog_smooth(const ImgDesc* __restrict__ descs,
                                                      const ImgTables* __restrict__ tables,
                                                      uint8_t* __restrict__ scratch, const int32_t* __restrict__ routes,
                                                      int cap) {
-  if ((int)blockIdx.x >= routes[kRtProg]) return;
-  const int img = route_list(routes, cap, kRtProg)[blockIdx.x];
+  const int cnt = routes[kRtProg];
+  for (int li = blockIdx.x; li < cnt; li += gridDim.x)
+    prog_smooth_image(route_list(routes, cap, kRtProg)[li], descs, tables, scratch);
+}
+
+__device__ void prog_smooth_image(int img, const ImgDesc* __restrict__ descs, const ImgTables* __restrict__ tables,
+                                  uint8_t* __restrict__ scratch) {
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || !d->smooth) return;
   int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
@@ -904,6 +915,7 @@ __global__ void __launch_bounds__(256) k_prog_smooth(const ImgDesc* __restrict__
 #define SDSJ_PROG_WAVES 5
 #endif
 constexpr int kProgThreads = 64;
+constexpr int kProgHelperGrid = 1024;  // workgroup columns of k_prog_zero / k_prog_dcs / k_prog_smooth
 __global__ void __launch_bounds__(kProgThreads) __attribute__((amdgpu_waves_per_eu(SDSJ_PROG_WAVES)))
 k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables, const uint8_t* __restrict__ blob,
        const int64_t* __restrict__ offsets, const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
@@ -923,11 +935,14 @@ hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* 
                        const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,
                        uint64_t rm) {
   if (!route_on(rm, kRtProg)) return hipSuccess;
-  hipLaunchKernelGGL(k_prog_zero, dim3(n, 16), dim3(256), 0, s, descs, scratch, routes, cap);
+  // (the helpers stride over the route list: a batch without progressive images launches few empty
+  // workgroups -- at one per image their grids cost 115 us per 16,384 baseline images)
+  const int gx = n < kProgHelperGrid ? n : kProgHelperGrid;
+  hipLaunchKernelGGL(k_prog_zero, dim3(gx, 16), dim3(256), 0, s, descs, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog, dim3(n), dim3(kProgThreads), 0, s, descs, tables, blob,
                      offsets, lengths, scratch, routes, cap);
-  hipLaunchKernelGGL(k_prog_dcs, dim3(n, 8), dim3(256), 0, s, descs, scratch, routes, cap);
-  hipLaunchKernelGGL(k_prog_smooth, dim3(n, 8), dim3(256), 0, s, descs, tables, scratch, routes, cap);
+  hipLaunchKernelGGL(k_prog_dcs, dim3(gx, 8), dim3(256), 0, s, descs, scratch, routes, cap);
+  hipLaunchKernelGGL(k_prog_smooth, dim3(gx, 8), dim3(256), 0, s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 
