@@ -212,6 +212,8 @@ struct ImgDesc {
   int8_t sm_bits[2][kMaxComp][10];
   int8_t mh;  // latency mode: the multi-hypothesis speculative pass (k_entspec_mh) takes the image
   int8_t sm_pad[3];
+  int32_t etab;  // k_enttab: the image whose EntTables it decodes with (itself, or image 0 of the lane when equal)
+  int32_t etab_pad;
 };
 
 // One tile of k_unstuff's first pass: bytes it emits and split markers (RSTn, codes below SOF0) it

@@ -108,14 +108,48 @@ __device__ __forceinline__ bool variant_owns(int ns) {
 // k_enttab: one workgroup per image builds its decode tables once into HBM; every entropy kernel
 // then copies the image's EntTables into LDS with 16-byte loads (one round trip) instead of
 // rebuilding them.
-__global__ void __launch_bounds__(kEntThreads) k_enttab(const ImgDesc* __restrict__ descs,
+#ifndef SDSJ_ETAB_SHARE
+#define SDSJ_ETAB_SHARE 1
+#endif
+__global__ void __launch_bounds__(kEntThreads) k_enttab(ImgDesc* __restrict__ descs,
                                                        const ImgTables* __restrict__ tables, EntTables* __restrict__ out) {
-  const ImgDesc* d = &descs[blockIdx.x];
+  ImgDesc* d = &descs[blockIdx.x];
   if (d->status != SDSJ_OK || d->progressive) return;
   const ImgTables* tb = &tables[blockIdx.x];
   __shared__ LutTables T;  // (the multi-symbol table goes straight to HBM: nothing here reads it back)
   __shared__ int32_t lim[kMaxSlots][12];
   const int t = threadIdx.x;
+  if (SDSJ_ETAB_SHARE && blockIdx.x > 0) {
+    // SDSJ_ETAB_SHARE: an image whose table inputs equal image 0's (same components' table selectors,
+    // same block -> component map, byte-equal Huffman specs of the tables it uses) decodes with image
+    // 0's EntTables (most JPEGs carry the standard tables), so only image 0 builds them.  Image 0's
+    // status is read here as its own workgroup reads it (this kernel changes no status).
+    const ImgDesc* a = &descs[0];
+    const ImgTables* ta = &tables[0];
+    __shared__ int same;
+    const bool cand = a->status == SDSJ_OK && !a->progressive && a->ncomp == d->ncomp && a->bpm == d->bpm;
+    if (t == 0) same = cand ? 1 : 0;
+    __syncthreads();
+    if (cand) {
+      bool diff = false;
+      if (t < d->ncomp) diff |= a->comp[t].td != d->comp[t].td || a->comp[t].ta != d->comp[t].ta;
+      if (t < d->bpm) diff |= a->blk_comp[t] != d->blk_comp[t];
+      // bits[0..16] and vals[0..255] of each component's DC and AC spec (273 bytes each)
+      for (int i = t; i < 2 * d->ncomp * 273; i += kEntThreads) {
+        const int c = i / (2 * 273), r = i % (2 * 273), ac = r >= 273, k = ac ? r - 273 : r;
+        const HuffSpec& ha = ac ? ta->ac_spec[d->comp[c].ta & 3] : ta->dc_spec[d->comp[c].td & 3];
+        const HuffSpec& hd = ac ? tb->ac_spec[d->comp[c].ta & 3] : tb->dc_spec[d->comp[c].td & 3];
+        diff |= k < 17 ? ha.bits[k] != hd.bits[k] : ha.vals[k - 17] != hd.vals[k - 17];
+      }
+      if (diff) same = 0;  // (benign race: every writer stores 0)
+    }
+    __syncthreads();
+    if (same) {
+      if (t == 0) d->etab = 0;
+      return;
+    }
+  }
+  if (t == 0) d->etab = blockIdx.x;
   if (t == 0) {
     int ns = 0;
     auto slot_of = [&](int key) {
@@ -845,8 +879,8 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   __shared__ LdsSpec<LB, NT> L;
   const int t = threadIdx.x;
   int ns;
-  if constexpr (LB == 11) ns = load_tables(L.T, &tables[img]);
-  else ns = load_tables<LB>(L.T, &tables[img]);
+  if constexpr (LB == 11) ns = load_tables(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]);
+  else ns = load_tables<LB>(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]);
   if (!variant_owns<LB>(ns)) return;
   if (t == 0) {
     L.sym[0] = 0;
@@ -962,7 +996,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       need_any = true;
   BlkCtx K{};
   if (__syncthreads_or(need_any)) {
-    load_sync_tables<LB>(L.T, &tables[img]);
+    load_sync_tables<LB>(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]);
     K = make_ctx(L.T, d->bpm);
     // --- 2. sync rounds until every entry equals its predecessor's exit ---
     for (;;) {
@@ -1160,8 +1194,8 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   __shared__ LdsWriteT<TT> L;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   int ns;
-  if constexpr (LB == 11) ns = load_write_tables(L.T, &tables[img], reinterpret_cast<int32_t*>(L.stage));
-  else ns = load_tables<LB>(L.T, &tables[img]);
+  if constexpr (LB == 11) ns = load_write_tables(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img], reinterpret_cast<int32_t*>(L.stage));
+  else ns = load_tables<LB>(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]);
   if (!variant_owns<LB>(ns)) return;
   {
     uint4* z4 = reinterpret_cast<uint4*>(L.stage);
@@ -1436,7 +1470,7 @@ k_entspec_mh(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, 
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || !d->mh) return;
   __shared__ LdsSpec<11, kEntThreads> L;
-  if (!variant_owns<11>(load_tables(L.T, &tables[img]))) return;
+  if (!variant_owns<11>(load_tables(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]))) return;
   const BlkCtx K = make_ctx(L.T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);
