@@ -108,9 +108,6 @@ __device__ __forceinline__ bool variant_owns(int ns) {
 // k_enttab: one workgroup per image builds its decode tables once into HBM; every entropy kernel
 // then copies the image's EntTables into LDS with 16-byte loads (one round trip) instead of
 // rebuilding them.
-#ifndef SDSJ_WRITE_RECT
-#define SDSJ_WRITE_RECT 0
-#endif
 #ifndef SDSJ_ETAB_SHARE
 #define SDSJ_ETAB_SHARE 1
 #endif
@@ -1220,42 +1217,6 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   const int nsub = d->nsub;
   const int blocks_per_seg = d->restart_interval ? d->restart_interval * K.bpm : (int)d->total_blocks;
   const int my_base = t * kStageStride, sink_base = kEntThreads * kStageStride;
-  // SDSJ_WRITE_RECT: only the MCUs k_idct reads are stored (its 8-block groups over the crop's source
-  // rectangle, widened by one sample; the same arithmetic as k_idct's setup, in MCU units over all
-  // components): decode index g is stored iff its MCU row is in [mya, myb) and its offset in that row
-  // in [wlo, whi).  A centre crop of a 4:3 image skips a quarter of the coefficient stores.
-  int mya = 0, myb = 1 << 30, wlo = 0, whi = 1 << 30, rowlen = 1 << 30;
-  float rrow = 0.f;
-  bool wall = true;
-  if (SDSJ_WRITE_RECT) {
-    const int x0 = d->src_x0, x1 = d->src_x0 + d->src_w, y0 = d->src_y0, y1 = d->src_y1;
-    int mxa = 1 << 30, mxb = 0;
-    mya = 1 << 30;
-    myb = 0;
-    for (int c = 0; c < d->ncomp; c++) {
-      const CompDesc& cd = d->comp[c];
-      const int h = d->ncomp == 1 ? 1 : cd.h, v = d->ncomp == 1 ? 1 : cd.v;
-      const int rh = d->ncomp == 1 ? 1 : d->hmax / cd.h, rv = d->ncomp == 1 ? 1 : d->vmax / cd.v;
-      int cx0 = x0 / rh - 1, cx1 = (x1 - 1) / rh + 1, cy0 = y0 / rv - 1, cy1 = (y1 - 1) / rv + 1;
-      cx0 = cx0 < 0 ? 0 : cx0;
-      cy0 = cy0 < 0 ? 0 : cy0;
-      cx1 = cx1 > cd.bw * 8 - 1 ? cd.bw * 8 - 1 : cx1;
-      cy1 = cy1 > cd.bh * 8 - 1 ? cd.bh * 8 - 1 : cy1;
-      const int bx0 = (cx0 >> 6) * 8, bx1 = ((cx1 >> 6) + 1) * 8;  // k_idct's groups (clipped to bw by it)
-      const int by0 = cy0 >> 3, by1 = (cy1 >> 3) + 1;
-      mxa = min(mxa, bx0 / h);
-      mxb = max(mxb, (bx1 + h - 1) / h);
-      mya = min(mya, by0 / v);
-      myb = max(myb, (by1 + v - 1) / v);
-    }
-    mxb = min(mxb, d->mcux);
-    wall = x1 <= x0 || y1 <= y0 ? false : (mxa <= 0 && mxb >= d->mcux && mya <= 0 && myb >= d->mcuy);
-    if (x1 <= x0 || y1 <= y0) mya = myb = 0;  // (k_idct reads nothing)
-    rowlen = K.bpm * d->mcux;
-    rrow = 1.0f / (float)rowlen;
-    wlo = mxa * K.bpm;
-    whi = mxb * K.bpm;
-  }
   int bad = 0;
   unsigned long long nsym = 0, witers = 0;
 
@@ -1353,18 +1314,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
               const uint32_t f = L.flist[wv][bi];
               uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
               const uint4 v = *sp;
-              const int gb = (int)(f & 0xFFFFFF);
-              bool keep = true;
-              if (SDSJ_WRITE_RECT && !wall) {  // MCU row of gb (exact for gb < 2^24: float estimate within 2, corrected)
-                int my = (int)((float)gb * rrow);
-                my -= my * rowlen > gb ? 1 : 0;
-                my -= my * rowlen > gb ? 1 : 0;
-                my += (my + 1) * rowlen <= gb ? 1 : 0;
-                my += (my + 1) * rowlen <= gb ? 1 : 0;
-                const int w = gb - my * rowlen;
-                keep = my >= mya && my < myb && w >= wlo && w < whi;
-              }
-              if (keep) store_coef16(reinterpret_cast<uint4*>(coef + (int64_t)gb * 64) + (lane & 7), v);
+              store_coef16(reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64) + (lane & 7), v);
               *sp = make_uint4(0, 0, 0, 0);
             }
           }
