@@ -451,23 +451,42 @@ def main():
         cursor[0] = s + B
 
     step = dev_step
-    cache_dir = None
+    cache_dir = src_dir = None
+    dl_rates = None
     if e2e:
-        # configs[4]: the rank's rows as files in a local cache directory (what sds/downloader.py leaves
-        # for LoadFromDiskTransform, presets.py:613-626) -> pinned slot -> H2D -> decode + resize -> D2H
-        # into pinned host memory.  One step submits batch k and completes batch k - 1 (its D2H on a
-        # second stream), so batch k's file reads and H2D overlap batch k - 1's decode.
+        # configs[4]: sds/downloader.py -> host cache -> H2D -> decode + resize -> D2H.  The rank's rows
+        # come from a source folder (one file per pool image, the "remote" of a local-scheme index)
+        # through the restated ParallelDownloader (sds_amd/downloader.py: a thread pool copying each row's
+        # file into the cache directory via <dst>.tmp + rename, skip_if_exists), whose completed rows --
+        # in completion order, as StreamingDataset consumes them (dataset.py:361-384) -- form the batches
+        # -> pinned slot -> H2D -> decode + resize -> D2H into pinned host memory.  One step submits
+        # batch k and completes batch k - 1 (its D2H on a second stream), so batch k's downloads, file
+        # reads and H2D overlap batch k - 1's decode; downloads run up to two batches ahead.
+        from itertools import islice
+
+        from sds_amd.downloader import ParallelDownloader
+        src_dir = tempfile.mkdtemp(prefix=f"sdsj_src_r{rank}_")
         cache_dir = tempfile.mkdtemp(prefix=f"sdsj_cache_r{rank}_")
-        fpaths = []
-        for k, p in enumerate(period):
-            fpaths.append(os.path.join(cache_dir, f"{r0 + k:08d}.jpg"))
-            with open(fpaths[-1], "wb") as f:
+        src_paths = {}
+        for p in set(period):
+            src_paths[p] = os.path.join(src_dir, f"{p:06d}.jpg")
+            with open(src_paths[p], "wb") as f:
                 f.write(pool[p])
-        row_paths = [fpaths[j % len(period)] for j in range(nrows)]
+        dl_workers = max(4, workers)
+        dl = ParallelDownloader(num_workers=dl_workers, prefetch=2 * B, num_retries=3, skip_if_exists=True)
+        dst_of = lambda key: os.path.join(cache_dir, f"{key:08d}-jpg.jpg")  # noqa: E731  (dataset.py:250)
+        sched = [0]
+
+        def schedule_ahead(upto):
+            while sched[0] < upto:
+                j = sched[0] % nrows
+                dl.schedule_task(r0 + j, [src_paths[period[j % len(period)]]], [dst_of(r0 + j)])
+                sched[0] += 1
+
         outs = [out, torch.empty_like(out)]
         hosts = [torch.empty(out.shape, dtype=out.dtype, pin_memory=True) for _ in range(2)]
         d2h = torch.cuda.Stream(dev)
-        pipe = {"k": 0, "prev": None, "bad": 0, "done": 0}
+        pipe = {"k": 0, "prev": None, "bad": 0, "done": 0, "taken": 0}
 
         def complete_prev():
             prev = pipe["prev"]
@@ -479,17 +498,40 @@ def main():
             pipe["prev"] = None
 
         def e2e_step():
-            s = cursor[0]
-            if s + B > nrows:
-                s = 0
+            schedule_ahead(pipe["taken"] + 2 * B)
+            paths = [dst_of(key) for key, _ in islice(dl.yield_completed(), B)]
+            pipe["taken"] += B
             slot = pipe["k"] % 2
             torch.cuda.current_stream(dev).wait_stream(d2h)  # slot's previous output has left for the host
-            eng.submit(slot, row_paths[s:s + B], (args.res, args.res), files=True, out=outs[slot])
+            eng.submit(slot, paths, (args.res, args.res), files=True, out=outs[slot])
             if pipe["prev"] is not None:
                 complete_prev()
             pipe["prev"], pipe["k"] = slot, pipe["k"] + 1
-            cursor[0] = s + B
 
+        def e2e_epoch_rate(nsteps):
+            barrier()
+            sync()
+            t = time.perf_counter()
+            for _ in range(nsteps):
+                e2e_step()
+            complete_prev()
+            sync()
+            return B * nsteps * world / max_over_ranks(time.perf_counter() - t,
+                                                       device=None if stub or args.backend == "gloo" else dev)
+
+        # correctness gate on the device-resident rows first (the engine's first call)
+        dev_step()
+        sync()
+        if int((status != 0).sum().item()):
+            raise SystemExit(f"rank {rank}: samples failed to decode")
+        # cold epoch: every row of the rank copied into the empty cache (nrows / B whole batches)
+        epoch_steps = max(1, nrows // B)
+        cold = e2e_epoch_rate(epoch_steps)
+        # the downloader's queue now holds the next two batches (already in the cache): the warm passes
+        # below find every destination present (skip_if_exists: one stat per row)
+        dl_rates = {"cold": round(cold, 1), "cold_rows_per_rank": epoch_steps * B, "workers": dl_workers,
+                    "prefetch": 2 * B, "restated": "sds_amd/downloader.py (downloader.py:25-131, "
+                                                   "utils/download.py:830-861)"}
         step = e2e_step
 
     # correctness gate before timing: the first batch's statuses are all OK
@@ -515,7 +557,11 @@ def main():
         complete_prev()
         sync()
         n_bad = pipe["bad"]
+        dl_rates["warm"] = round(B * args.steps * world / max_over_ranks(t1 - t0, device=None if stub or args.backend ==
+                                                                         "gloo" else dev), 1)
+        dl.shutdown()
         shutil.rmtree(cache_dir, ignore_errors=True)
+        shutil.rmtree(src_dir, ignore_errors=True)
     else:
         n_bad = int((status != 0).sum().item())  # the last timed batch decoded completely as well
     if n_bad:
@@ -623,9 +669,11 @@ def main():
         workload = (f"configs[2]: synthetic mixed VGA..4K q90 4:2:0 baseline JPEGs resident in HBM -> centre crop + "
                     f"bilinear resize {args.res}x{args.res} + hflip (p=0.5, seeded) + float32 CHW x/127.5-1"
                     if mixed else
-                    f"configs[4]: synthetic 640x480 q90 JPEG files in a local cache directory per rank -> pinned "
-                    f"slot -> H2D -> centre crop + bilinear resize {args.res}x{args.res} uint8 CHW -> D2H into "
-                    f"pinned host memory (two slots in flight)"
+                    f"configs[4]: synthetic 640x480 q90 JPEG files -> restated sds ParallelDownloader (local "
+                    f"scheme: copy to the rank's cache directory via .tmp + rename, skip_if_exists) -> pinned slot "
+                    f"-> H2D -> centre crop + bilinear resize {args.res}x{args.res} uint8 CHW -> D2H into pinned "
+                    f"host memory (two slots in flight); value = warm cache (every row present: one stat per "
+                    f"row), downloader.cold = the first epoch into an empty cache"
                     if e2e else
                     ("configs[3]: " if world > 1 else "configs[1]: ") +
                     f"{total_rows:,}-row {'parquet' if index_path else 'in-memory'} index, one compute_index_slice "
@@ -668,6 +716,7 @@ def main():
         if e2e:
             line["device_resident_value"] = round(dev_value, 1)
             line["e2e_over_device_resident"] = round(value / dev_value, 4)
+            line["downloader"] = dl_rates
             line["roofline"]["note"] = "device-resident kernels of the same rows (the PCIe legs are not kernels)"
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -612,6 +612,26 @@ SDSJ_HD inline int nearest_src(int in_size, int out_size, int xx) {
   return (xin >= 0 && xin < in_size) ? xin : -1;
 }
 
+// The blocks of component c the colour / resample passes read -- k_idct transforms exactly these and
+// k_entwrite stores only these: the source rectangle [src_x0, src_x0 + src_w) x [src_y0, src_y1) in the
+// component's sampling, widened by one sample for the fancy upsampling's neighbours, as inclusive block
+// bounds.  False when the crop is empty (nothing is read).
+SDSJ_HD inline bool comp_block_rect(const ImgDesc& d, int c, int& bx0, int& bx1, int& by0, int& by1) {
+  const int x0 = d.src_x0, x1 = d.src_x0 + d.src_w, y0 = d.src_y0, y1 = d.src_y1;
+  const CompDesc& cd = d.comp[c];
+  const int rh = d.ncomp == 1 ? 1 : d.hmax / cd.h, rv = d.ncomp == 1 ? 1 : d.vmax / cd.v;
+  int cx0 = x0 / rh - 1, cx1 = (x1 - 1) / rh + 1, cy0 = y0 / rv - 1, cy1 = (y1 - 1) / rv + 1;
+  cx0 = cx0 < 0 ? 0 : cx0;
+  cy0 = cy0 < 0 ? 0 : cy0;
+  cx1 = cx1 > cd.bw * 8 - 1 ? cd.bw * 8 - 1 : cx1;
+  cy1 = cy1 > cd.bh * 8 - 1 ? cd.bh * 8 - 1 : cy1;
+  bx0 = cx0 >> 3;
+  bx1 = cx1 >> 3;
+  by0 = cy0 >> 3;
+  by1 = cy1 >> 3;
+  return x1 > x0 && y1 > y0 && d.geo != kGeoZeros;
+}
+
 SDSJ_HD inline double filter_support(int filter) {
   switch (filter) {
     case SDSJ_FILTER_BOX: return 0.5;

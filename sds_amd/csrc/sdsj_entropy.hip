@@ -108,9 +108,6 @@ __device__ __forceinline__ bool variant_owns(int ns) {
 // k_enttab: one workgroup per image builds its decode tables once into HBM; every entropy kernel
 // then copies the image's EntTables into LDS with 16-byte loads (one round trip) instead of
 // rebuilding them.
-#ifndef SDSJ_ETAB_SHARE
-#define SDSJ_ETAB_SHARE 1
-#endif
 __global__ void __launch_bounds__(kEntThreads) k_enttab(ImgDesc* __restrict__ descs,
                                                        const ImgTables* __restrict__ tables, EntTables* __restrict__ out) {
   ImgDesc* d = &descs[blockIdx.x];
@@ -119,8 +116,8 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(ImgDesc* __restrict__ de
   __shared__ LutTables T;  // (the multi-symbol table goes straight to HBM: nothing here reads it back)
   __shared__ int32_t lim[kMaxSlots][12];
   const int t = threadIdx.x;
-  if (SDSJ_ETAB_SHARE && blockIdx.x > 0) {
-    // SDSJ_ETAB_SHARE: an image whose table inputs equal image 0's (same components' table selectors,
+  if (blockIdx.x > 0) {
+    // Shared tables: an image whose table inputs equal image 0's (same components' table selectors,
     // same block -> component map, byte-equal Huffman specs of the tables it uses) decodes with image
     // 0's EntTables (most JPEGs carry the standard tables), so only image 0 builds them.  Image 0's
     // status is read here as its own workgroup reads it (this kernel changes no status).
@@ -356,10 +353,7 @@ constexpr int kWriteGroup = SDSJ_WRITE_GROUP;  // (write pass)
 static_assert(kSpecGroup < kQ && kWriteGroup < kQ, "a fresh refill must pass the group check");
 // A symbol takes at most 27 bits (16-bit code + 11 extra bits; a bad code 17): a group of G symbols
 // has a word to pull before each of them when nb + 32 nq >= 27 (G - 1) + 32 at its start.
-#ifndef SDSJ_REFILL_SLACK
-#define SDSJ_REFILL_SLACK 0
-#endif
-constexpr int kRefillSpec = SDSJ_REFILL_SLACK ? 32 * (kSpecGroup + 1) : 27 * (kSpecGroup - 1) + 32;
+constexpr int kRefillSpec = 27 * (kSpecGroup - 1) + 32;
 #ifndef SDSJ_REC_STORE
 #define SDSJ_REC_STORE 16
 #endif
@@ -369,7 +363,7 @@ constexpr int kRefillSpec = SDSJ_REFILL_SLACK ? 32 * (kSpecGroup + 1) : 27 * (kS
 // (fewer scattered 8-byte stores; profiles/r03d_ab.txt).
 constexpr int kRecStore = SDSJ_REC_STORE;
 static_assert(kRecStore <= kRec, "records fit their scratch");
-constexpr int kRefillWrite = SDSJ_REFILL_SLACK ? 32 * (kWriteGroup + 1) : 27 * (kWriteGroup - 1) + 32;
+constexpr int kRefillWrite = 27 * (kWriteGroup - 1) + 32;
 
 template <int Q>
 struct BitsQ {
@@ -408,37 +402,21 @@ __device__ __forceinline__ void bits_init(BitsQ<Q>& b, const uint32_t* src, uint
   for (int k = 0; k < Q; k++) b.q[k] = 0;
 }
 
-// Wave-synchronous refill: re-reads kQ words from wi (the ustream carries kUPad bytes of slack).
-#ifndef SDSJ_PARTIAL_REFILL
-#define SDSJ_PARTIAL_REFILL 0
-#endif
-// SDSJ_FILL_X4: the kQ words as 16-byte loads (dword-aligned global_load_dwordx4: a quarter of the
-// load instructions, and of the per-lane cache-line requests, of one dword load per word)
-#ifndef SDSJ_FILL_X4
-#define SDSJ_FILL_X4 1
-#endif
+// Wave-synchronous refill: re-reads kQ words from wi (the ustream carries kUPad bytes of slack), as
+// dword-aligned 16-byte loads (global_load_dwordx4: a quarter of the load instructions, and of the
+// per-lane cache-line requests, of one dword load per word).
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 template <int Q>
 __device__ __forceinline__ void bits_fill(BitsQ<Q>& b) {
+  static_assert(Q % 4 == 0, "the queue refills in 16-byte loads");
   if ((b.wi + Q) * 32u <= b.lim) {  // the common case: all kQ words lie before the limit
-    if constexpr (SDSJ_FILL_X4 && Q % 4 == 0 && !SDSJ_PARTIAL_REFILL) {
 #pragma unroll
-      for (int k = 0; k < Q; k += 4) {
-        const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(b.src + b.wi + k);
-        b.q[k] = __builtin_bswap32(v.x);
-        b.q[k + 1] = __builtin_bswap32(v.y);
-        b.q[k + 2] = __builtin_bswap32(v.z);
-        b.q[k + 3] = __builtin_bswap32(v.w);
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < Q; k++) {
-        if (SDSJ_PARTIAL_REFILL) {  // only the words not queued yet (q[0 .. nq) hold words wi .. wi + nq)
-          if (k >= b.nq) b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
-        } else {
-          b.q[k] = __builtin_bswap32(b.src[b.wi + k]);
-        }
-      }
+    for (int k = 0; k < Q; k += 4) {
+      const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(b.src + b.wi + k);
+      b.q[k] = __builtin_bswap32(v.x);
+      b.q[k + 1] = __builtin_bswap32(v.y);
+      b.q[k + 2] = __builtin_bswap32(v.z);
+      b.q[k + 3] = __builtin_bswap32(v.w);
     }
   } else {
 #pragma unroll
@@ -879,8 +857,8 @@ __device__ void entspec_image(int img, int grp, ImgDesc* __restrict__ descs, con
   __shared__ LdsSpec<LB, NT> L;
   const int t = threadIdx.x;
   int ns;
-  if constexpr (LB == 11) ns = load_tables(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]);
-  else ns = load_tables<LB>(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]);
+  if constexpr (LB == 11) ns = load_tables(L.T, &tables[d->etab]);
+  else ns = load_tables<LB>(L.T, &tables[d->etab]);
   if (!variant_owns<LB>(ns)) return;
   if (t == 0) {
     L.sym[0] = 0;
@@ -996,7 +974,7 @@ __device__ void entsync_image(int img, ImgDesc* __restrict__ descs, const EntTab
       need_any = true;
   BlkCtx K{};
   if (__syncthreads_or(need_any)) {
-    load_sync_tables<LB>(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]);
+    load_sync_tables<LB>(L.T, &tables[d->etab]);
     K = make_ctx(L.T, d->bpm);
     // --- 2. sync rounds until every entry equals its predecessor's exit ---
     for (;;) {
@@ -1127,9 +1105,49 @@ struct LdsWriteT {
   TT T;
   alignas(16) int16_t stage[(kEntThreads + 1) * kStageStride];  // + one shared sink block
   uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
+  int32_t krect[kMaxBlocksPerMcu][4];     // MCU block b: stored iff MCU column in [0], [1], MCU row in [2], [3]
+  int32_t keep_all;
   int32_t bad;
   unsigned long long sym;
 };
+
+// Exact a / b for 0 <= a < 2^24, 1 <= b: float estimate (error < 2), then two corrections each way.
+__device__ __forceinline__ int div_exact24(int a, int b, float rb) {
+  int q = (int)((float)a * rb);
+  q -= q * b > a ? 1 : 0;
+  q -= q * b > a ? 1 : 0;
+  q += (q + 1) * b <= a ? 1 : 0;
+  q += (q + 1) * b <= a ? 1 : 0;
+  return q;
+}
+
+// The coefficient rectangle (comp_block_rect, the blocks k_idct reads) as per-MCU-block ranges of MCU
+// columns and rows: block b of MCU (mx, my) is component c's block (mx h + dx, my v + dy).
+__device__ void write_rect(const ImgDesc* d, int32_t (*krect)[4], int32_t* keep_all) {
+  const int t = threadIdx.x;
+  if (t < d->bpm) {
+    const int c = d->blk_comp[t];
+    const int h = d->ncomp == 1 ? 1 : d->comp[c].h, v = d->ncomp == 1 ? 1 : d->comp[c].v;
+    const int dx = d->blk_dx[t], dy = d->blk_dy[t];
+    int bx0, bx1, by0, by1;
+    if (comp_block_rect(*d, c, bx0, bx1, by0, by1)) {
+      krect[t][0] = bx0 - dx <= 0 ? 0 : (bx0 - dx + h - 1) / h;
+      krect[t][1] = bx1 - dx < 0 ? -1 : (bx1 - dx) / h;
+      krect[t][2] = by0 - dy <= 0 ? 0 : (by0 - dy + v - 1) / v;
+      krect[t][3] = by1 - dy < 0 ? -1 : (by1 - dy) / v;
+    } else {
+      krect[t][0] = krect[t][2] = 1;
+      krect[t][1] = krect[t][3] = 0;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    bool all = true;
+    for (int b = 0; b < d->bpm; b++)
+      all &= krect[b][0] <= 0 && krect[b][1] >= d->mcux - 1 && krect[b][2] <= 0 && krect[b][3] >= d->mcuy - 1;
+    *keep_all = all;
+  }
+}
 
 // The compact two-level tables from the image's LB = 11 tables (HBM).  The staging area serves as
 // the scan's scratch before it is cleared.
@@ -1194,8 +1212,8 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   __shared__ LdsWriteT<TT> L;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   int ns;
-  if constexpr (LB == 11) ns = load_write_tables(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img], reinterpret_cast<int32_t*>(L.stage));
-  else ns = load_tables<LB>(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]);
+  if constexpr (LB == 11) ns = load_write_tables(L.T, &tables[d->etab], reinterpret_cast<int32_t*>(L.stage));
+  else ns = load_tables<LB>(L.T, &tables[d->etab]);
   if (!variant_owns<LB>(ns)) return;
   {
     uint4* z4 = reinterpret_cast<uint4*>(L.stage);
@@ -1207,7 +1225,12 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     L.it = 0;
     if (kStats) L.t0 = __builtin_amdgcn_s_memtime();
   }
+  write_rect(d, L.krect, &L.keep_all);
   __syncthreads();
+  // only the blocks k_idct reads are stored (a centre crop of a 4:3 image: about 4 in 5)
+  const bool keep_all = L.keep_all != 0;
+  const int bpm_i = d->bpm, mcux_i = d->mcux;
+  const float rbpm = 1.0f / (float)bpm_i, rmcux = 1.0f / (float)mcux_i;
   const TT& T = L.T;
   const BlkCtx K = make_ctx(T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
@@ -1314,7 +1337,14 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
               const uint32_t f = L.flist[wv][bi];
               uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
               const uint4 v = *sp;
-              store_coef16(reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64) + (lane & 7), v);
+              const int gb = (int)(f & 0xFFFFFF);
+              bool keep = true;
+              if (!keep_all) {  // (uniform) MCU (mx, my) and MCU block b of decode index gb
+                const int m = div_exact24(gb, bpm_i, rbpm), b = gb - m * bpm_i;
+                const int my = div_exact24(m, mcux_i, rmcux), mx = m - my * mcux_i;
+                keep = mx >= L.krect[b][0] && mx <= L.krect[b][1] && my >= L.krect[b][2] && my <= L.krect[b][3];
+              }
+              if (keep) store_coef16(reinterpret_cast<uint4*>(coef + (int64_t)gb * 64) + (lane & 7), v);
               *sp = make_uint4(0, 0, 0, 0);
             }
           }
@@ -1470,7 +1500,7 @@ k_entspec_mh(ImgDesc* __restrict__ descs, const EntTables* __restrict__ tables, 
   ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || !d->mh) return;
   __shared__ LdsSpec<11, kEntThreads> L;
-  if (!variant_owns<11>(load_tables(L.T, &tables[SDSJ_ETAB_SHARE ? d->etab : img]))) return;
+  if (!variant_owns<11>(load_tables(L.T, &tables[d->etab]))) return;
   const BlkCtx K = make_ctx(L.T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
   const SegView sv = seg_view(scratch + d->off_seg, d->nseg);

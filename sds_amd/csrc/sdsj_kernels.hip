@@ -60,6 +60,20 @@ __device__ __host__ inline int warm_for(int sub_bits, int floor_bits) {
   return sub_bits * 3 / 2 < w ? sub_bits * 3 / 2 : w;
 }
 
+// Distinct Huffman table slots the scan uses (DC keys td, AC keys 4 | ta), counted as load_tables
+// counts them: more than 4 selects the 10-bit entropy route (kRtEnt10, image_routes).
+__device__ __host__ inline int huff_slots(const ImgDesc& d) {
+  int keys[2 * kMaxComp], ns = 0;
+  for (int c = 0; c < d.ncomp; c++)
+    for (int k = 0; k < 2; k++) {
+      const int key = k ? (4 | d.comp[c].ta) : d.comp[c].td;
+      bool seen = false;
+      for (int q = 0; q < ns; q++) seen |= keys[q] == key;
+      if (!seen) keys[ns++] = key;
+    }
+  return ns;
+}
+
 __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, bool frames = false, bool small = false) {
   // Geometry: functional.py:78-80 shortcut, :118-147 crop, Pillow ImagingResampleInner.
   const int W = d->width, H = d->height;
@@ -150,8 +164,11 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
     }
   }
   d->lat = small && !frames;
-  // multi-hypothesis speculative pass for latency-mode baseline images without restart intervals
-  d->mh = (int8_t)(SDSJ_MH && d->lat && !d->progressive && d->restart_interval == 0 && d->bpm <= kMhMaxPhases);
+  // multi-hypothesis speculative pass for latency-mode baseline images without restart intervals;
+  // only the 11-bit entropy routes launch it (k_entspec_mh), so images of more than 4 table slots
+  // (kRtEnt10) keep the ordinary speculative pass
+  d->mh = (int8_t)(SDSJ_MH && d->lat && !d->progressive && d->restart_interval == 0 && d->bpm <= kMhMaxPhases &&
+                   huff_slots(*d) <= 4);
   {
     const int64_t bits = d->entropy_len * 8;
     const int64_t per_group = (int64_t)kDecodeThreads * (d->lat ? kLatSubBits : kGroupBits);
@@ -310,14 +327,7 @@ __global__ void __launch_bounds__(64) k_parse(int n, const uint8_t* __restrict__
 // progressive images), entropy variant by the Huffman tables in use (slots as load_tables counts
 // them), resample variant as plan_image chose it (-1 for an empty crop).
 SDSJ_HD inline void image_routes(const ImgDesc& d, int* ru, int* re, int* rr) {
-  int keys[2 * kMaxComp], ns = 0;
-  for (int c = 0; c < d.ncomp; c++)
-    for (int k = 0; k < 2; k++) {
-      const int key = k ? (4 | d.comp[c].ta) : d.comp[c].td;
-      bool seen = false;
-      for (int q = 0; q < ns; q++) seen |= keys[q] == key;
-      if (!seen) keys[ns++] = key;
-    }
+  const int ns = huff_slots(d);
   *ru = d.progressive ? -1 : (d.ntiles > kUsSerialTiles || d.lat ? kRtUsBig : kRtUsSmall);
   *re = d.progressive ? kRtProg : ns > 4 ? kRtEnt10 : (d.ent_groups > 1 ? kRtEnt11M : kRtEnt11);
   *rr = d.geo == kGeoZeros ? -1
@@ -1096,7 +1106,7 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   __shared__ alignas(16) int32_t qt[kMaxComp][64];
   __shared__ int32_t binv[kMaxComp][16];  // (dy * 4 + dx) -> MCU block index b (jdcoefct order)
   __shared__ int32_t gstart[kMaxComp + 1], ngx[kMaxComp], cbw[kMaxComp], ch_[kMaxComp], cv_[kMaxComp], cpitch[kMaxComp];
-  __shared__ int32_t cgx0[kMaxComp], cby0[kMaxComp];  // first 8-block group column / block row needed
+  __shared__ int32_t cbx0[kMaxComp], cbx1[kMaxComp], cby0[kMaxComp];  // first / last block column, first block row read
   __shared__ float rngx[kMaxComp], rch[kMaxComp], rcv[kMaxComp];  // reciprocals for the exact quotients below
   __shared__ int64_t cplane[kMaxComp];
   const int t = threadIdx.x;
@@ -1105,23 +1115,19 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
   for (int i = t; i < ncomp * 64; i += kIdctThreads) qt[i / 64][i % 64] = tables[img].qt[d->comp[i / 64].tq][natural_order(i % 64)];
   if (t < bpm) binv[d->blk_comp[t]][d->blk_dy[t] * 4 + d->blk_dx[t]] = t;
   if (t == 0) {
-    // only the blocks whose pixels the colour/resample passes read: the source rectangle
-    // [src_x0, src_x0 + src_w) x [src_y0, src_y1) in each component's sampling, widened by one
-    // sample for the fancy upsampling's neighbours (the crop drops the rest of the image)
-    const int x0 = d->src_x0, x1 = d->src_x0 + d->src_w, y0 = d->src_y0, y1 = d->src_y1;
+    // only the blocks whose pixels the colour/resample passes read (comp_block_rect: the crop's source
+    // rectangle widened by one sample), in groups of 8 horizontally adjacent blocks from its first
+    // block column -- the blocks k_entwrite stored
     int acc = 0;
     for (int c = 0; c < ncomp; c++) {
       const CompDesc& cd = d->comp[c];
-      const int rh = ncomp == 1 ? 1 : d->hmax / cd.h, rv = ncomp == 1 ? 1 : d->vmax / cd.v;
-      int cx0 = x0 / rh - 1, cx1 = (x1 - 1) / rh + 1, cy0 = y0 / rv - 1, cy1 = (y1 - 1) / rv + 1;
-      cx0 = cx0 < 0 ? 0 : cx0;
-      cy0 = cy0 < 0 ? 0 : cy0;
-      cx1 = cx1 > cd.bw * 8 - 1 ? cd.bw * 8 - 1 : cx1;
-      cy1 = cy1 > cd.bh * 8 - 1 ? cd.bh * 8 - 1 : cy1;
+      int bx0, bx1, by0, by1;
+      const bool any = comp_block_rect(*d, c, bx0, bx1, by0, by1);
       gstart[c] = acc;
-      cgx0[c] = cx0 >> 6;
-      ngx[c] = (cx1 >> 6) - cgx0[c] + 1;
-      cby0[c] = cy0 >> 3;
+      cbx0[c] = bx0;
+      cbx1[c] = bx1;
+      ngx[c] = (bx1 - bx0) / 8 + 1;
+      cby0[c] = by0;
       cbw[c] = cd.bw;
       ch_[c] = ncomp == 1 ? 1 : cd.h;
       cv_[c] = ncomp == 1 ? 1 : cd.v;
@@ -1130,7 +1136,7 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
       rngx[c] = 1.0f / (float)ngx[c];
       rch[c] = 1.0f / (float)ch_[c];
       rcv[c] = 1.0f / (float)cv_[c];
-      acc += x1 > x0 && y1 > y0 ? ngx[c] * ((cy1 >> 3) - cby0[c] + 1) : 0;
+      acc += any ? ngx[c] * (by1 - by0 + 1) : 0;
     }
     gstart[ncomp] = acc;
   }
@@ -1165,9 +1171,9 @@ k_idct(int n, const ImgDesc* __restrict__ descs,
     const int local = grp - gstart[c];
     const int byl = qdiv(local, ngx[c], rngx[c]);
     by = cby0[c] + byl;
-    bx = (cgx0[c] + local - byl * ngx[c]) * 8 + lb;
+    bx = cbx0[c] + (local - byl * ngx[c]) * 8 + lb;
     g = -1;
-    if (grp < ngroups && bx < cbw[c]) {
+    if (grp < ngroups && bx <= cbx1[c] && bx < cbw[c]) {
       const int h = ch_[c], v = cv_[c];
       const int mx = qdiv(bx, h, rch[c]), my = qdiv(by, v, rcv[c]);
       g = (my * mcux + mx) * bpm + binv[c][(by - my * v) * 4 + (bx - mx * h)];
@@ -1353,12 +1359,24 @@ __device__ double filt_eval(int filter, double x) {
   }
 }
 
-__device__ void coeffs_one(int in_size, int out_size, int filter, int ksize, int xx, int32_t* bounds, int32_t* kk) {
-  if (filter == SDSJ_FILTER_NEAREST) {  // one tap of weight 1.0 (ksize 1), or none (fill value 0)
-    const int s = nearest_src(in_size, out_size, xx);
+// NEAREST: one tap of weight 1.0 (ksize 1) at the source index of Pillow's running sum, or none (fill
+// value 0).  One thread walks the whole axis (the running sum is sequential; a per-index restart
+// would cost O(out^2)).
+__device__ void nearest_axis(int in_size, int out_size, int32_t* bounds, int32_t* kk) {
+  const double a = (double)in_size / out_size;
+  double xo = 0.0 + a * 0.5;
+  for (int xx = 0; xx < out_size; xx++, xo += a) {
+    const int xin = xo < 0.0 ? -1 : (int)xo;
+    const int s = (xin >= 0 && xin < in_size) ? xin : -1;
     kk[xx] = 1 << 22;
     bounds[2 * xx] = s < 0 ? 0 : s;
     bounds[2 * xx + 1] = s < 0 ? 0 : 1;
+  }
+}
+
+__device__ void coeffs_one(int in_size, int out_size, int filter, int ksize, int xx, int32_t* bounds, int32_t* kk) {
+  if (filter == SDSJ_FILTER_NEAREST) {
+    if (xx == 0) nearest_axis(in_size, out_size, bounds, kk);
     return;
   }
   const double scale = (double)in_size / out_size;

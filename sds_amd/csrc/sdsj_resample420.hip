@@ -22,10 +22,6 @@
 #include "sdsj_kernels.h"
 #include "sdsj_pixel.h"
 
-#ifndef SDSJ_VUNROLL
-#define SDSJ_VUNROLL 1  // (0: the vertical taps as a runtime loop, for A/B runs)
-#endif
-
 namespace sdsj {
 
 constexpr int kFThreads = 256;
@@ -125,9 +121,6 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
 // per CU, and 5 waves per SIMD fit their registers without spills (95 VGPRs): k_rs420<5> 9.95 -> 9.23 ms
 // per 16,384 images (profiles/r03b_rs420_occupancy_ab.txt).  The 9- and 11-tap kernels and 4:4:4 (whose
 // full-width chroma rows take 34 KB) keep 4.
-#ifndef SDSJ_RS_GLDS
-#define SDSJ_RS_GLDS 1
-#endif
 #ifndef SDSJ_RS_WAVES
 #define SDSJ_RS_WAVES 5
 #endif
@@ -251,7 +244,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
     // holds staged rows wv, wv + 4, wv + 8 (<= 12 rows), 64 dwords per load.  Colour layouts
     // (kGlds): the same rows and lanes, loaded straight into LDS by issue_lds below.
     constexpr int kPR = (G::kRows + 3) / 4, kPC = (kMaxSpan / 4 + 2 + 63) / 64;
-    constexpr bool kGlds = SDSJ_RS_GLDS && LAY != kRsGray;
+    constexpr bool kGlds = LAY != kRsGray;
     uint32_t pre[kPR][kPC];
     auto row_src = [&](const Step& p, int row, const uint8_t*& g, int& nd, int& o) {
       if (row < p.nr) {
@@ -283,7 +276,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
         }
       }
     };
-    // SDSJ_RS_GLDS (colour layouts): the next step's rows go straight to LDS (global_load_lds, no
+    // Colour layouts: the next step's rows go straight to LDS (global_load_lds, no
     // register staging), issued after this step's conversion has read the staged rows; the step-end
     // barrier retires them.
     auto issue_lds = [&](const Step& p) {
@@ -536,7 +529,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
                   v2 += tap((int32_t)(h >> 16), w);
                 }
               };
-              if (SDSJ_VUNROLL && ksv <= KT) {
+              if (ksv <= KT) {
 #pragma unroll
                 for (int k = 0; k < KT; k++) vtap(k);
               } else {

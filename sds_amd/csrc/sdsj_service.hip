@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <poll.h>
 #include <pthread.h>
 #include <signal.h>
 #include <stdio.h>
@@ -80,7 +81,11 @@ struct Client {
       const ssize_t w = send(fd, &rep, sizeof(rep), MSG_NOSIGNAL);
       if (w == (ssize_t)sizeof(rep)) return;
       if (w < 0 && errno == EINTR) continue;
-      closed.store(true);  // the worker went away: its later requests are dropped
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {  // socket buffer full: wait until writable
+        pollfd p{fd, POLLOUT, 0};
+        if (poll(&p, 1, 1000) >= 0 && !(p.revents & (POLLERR | POLLHUP | POLLNVAL))) continue;
+      }
+      closed.store(true);  // the worker went away (EPIPE, ECONNRESET, ...): its later requests are dropped
       return;
     }
   }
@@ -115,8 +120,6 @@ class Service {
 
   int run() {
     trace_ = getenv("SDSJ_SERVICE_TRACE") != nullptr;
-    const char* path = getenv("SDSJ_SERVICE_PATH");
-    submit_path_ = path && strcmp(path, "submit") == 0;
     if (hipSetDevice(cfg_.device) != hipSuccess) return fail("hipSetDevice", SDSJ_EHIP);
     const int nl = cfg_.engines > 0 ? cfg_.engines : 8;
     max_batch_ = cfg_.max_batch > 0 ? cfg_.max_batch : 64;
@@ -350,23 +353,13 @@ class Service {
       lens[i] = (size_t)l.batch[i].r.in_len;
       flips[i] = l.batch[i].r.flip ? 1 : 0;
     }
-    double t1 = 0;
-    if (submit_path_) {  // (experiment) the pipelined host path: H2D on the engine's copy stream
-      if (rc == SDSJ_OK) rc = sdsj_submit_batch(l.e, 0, n, ptrs.data(), lens.data(), &op, flips.data(), l.d_out, l.s);
-      if (rc == SDSJ_OK && hipMemcpyAsync(l.h_out, l.d_out, need, hipMemcpyDeviceToHost, l.s) != hipSuccess) rc = SDSJ_EHIP;
-      if (rc == SDSJ_OK && hipEventRecord(l.done, l.s) != hipSuccess) rc = SDSJ_EHIP;
-      t1 = trace_ ? now_us() : 0;
-      if (rc == SDSJ_OK && hipEventSynchronize(l.done) != hipSuccess) rc = SDSJ_EHIP;
-      if (rc == SDSJ_OK && sdsj_wait_batch(l.e, 0, l.status.data()) != SDSJ_OK) rc = SDSJ_EHIP;
-    } else {
-      // everything on the lane's one stream (H2D, kernels, status), so the lanes' streams are the
-      // only ones the service queues work on: one hardware queue each
-      if (rc == SDSJ_OK)
-        rc = sdsj_decode_resize_batch(l.e, n, ptrs.data(), lens.data(), &op, flips.data(), l.d_out, l.status.data(), l.s);
-      t1 = trace_ ? now_us() : 0;
-      if (rc == SDSJ_OK && hipMemcpyAsync(l.h_out, l.d_out, need, hipMemcpyDeviceToHost, l.s) != hipSuccess) rc = SDSJ_EHIP;
-      if (rc == SDSJ_OK && hipStreamSynchronize(l.s) != hipSuccess) rc = SDSJ_EHIP;
-    }
+    // everything on the lane's one stream (H2D, kernels, status), so the lanes' streams are the only
+    // ones the service queues work on: one hardware queue each
+    if (rc == SDSJ_OK)
+      rc = sdsj_decode_resize_batch(l.e, n, ptrs.data(), lens.data(), &op, flips.data(), l.d_out, l.status.data(), l.s);
+    const double t1 = trace_ ? now_us() : 0;
+    if (rc == SDSJ_OK && hipMemcpyAsync(l.h_out, l.d_out, need, hipMemcpyDeviceToHost, l.s) != hipSuccess) rc = SDSJ_EHIP;
+    if (rc == SDSJ_OK && hipStreamSynchronize(l.s) != hipSuccess) rc = SDSJ_EHIP;
     if (rc != SDSJ_OK) {
       log_err("batch", sdsj_last_error(l.e));
       (void)hipStreamSynchronize(l.s);
@@ -418,7 +411,6 @@ class Service {
   sdsj_service_cfg cfg_;
   int max_batch_ = 64;
   bool trace_ = false;
-  bool submit_path_ = false;
   int ep_ = -1;
   std::vector<Lane> lanes_;
   std::vector<std::thread> threads_;

@@ -41,6 +41,9 @@ _REP = struct.Struct("<Qii")
 assert _REQ.size == 72 and _REP.size == 16
 OK, EINVAL = 0, -1
 CONNECT_TIMEOUT_S = float(os.environ.get("SDS_AMD_SERVICE_TIMEOUT", "300"))
+# SDS_AMD_SERVICE_PROFILE=<path>: each worker appends its cumulative per-phase times (seconds) to <path>
+# every 256 requests (copy-in, the request's round trip, copy-out) -- tools/persample_bench.py
+PROFILE_PATH = os.environ.get("SDS_AMD_SERVICE_PROFILE")
 
 
 class ServiceError(RuntimeError):
@@ -123,6 +126,18 @@ class ServiceClient:
         self.fd = -1
         self.mm: Optional[mmap.mmap] = None
         self.size = 0
+        self.prof = {"n": 0, "copy_in": 0.0, "round_trip": 0.0, "copy_out": 0.0} if PROFILE_PATH else None
+
+    def _profile(self, t0: float, t1: float, t2: float, t3: float) -> None:
+        p = self.prof
+        p["n"] += 1
+        p["copy_in"] += t1 - t0
+        p["round_trip"] += t2 - t1
+        p["copy_out"] += t3 - t2
+        if p["n"] % 256 == 0:
+            import json
+            with open(PROFILE_PATH, "a") as f:
+                f.write(json.dumps({"pid": os.getpid(), **p}) + "\n")
 
     def close(self) -> None:
         try:
@@ -179,12 +194,20 @@ class ServiceClient:
 
     def decode(self, data: bytes, op, flip: bool = False):
         """One JPEG -> (status, output array or None)."""
+        t0 = time.perf_counter() if self.prof is not None else 0.0
         n = len(data)
         off = _align(n, 256)
         ob = op.out_h * op.out_w * 3 * (4 if op.out_dtype == 1 else 1)
         self._reserve(off + ob)
         self.mm[0:n] = data
-        return self._result(self._call(KIND_DECODE, n, off, op, flip), off, op)
+        if self.prof is None:
+            return self._result(self._call(KIND_DECODE, n, off, op, flip), off, op)
+        t1 = time.perf_counter()
+        st = self._call(KIND_DECODE, n, off, op, flip)
+        t2 = time.perf_counter()
+        r = self._result(st, off, op)
+        self._profile(t0, t1, t2, time.perf_counter())
+        return r
 
     def resize_frame(self, rgb: np.ndarray, op, flip: bool = False):
         """One HWC uint8 RGB frame (a sample PIL decoded) -> (status, output array or None)."""

@@ -85,14 +85,20 @@ def _category(v: int) -> int:
     return int(abs(v)).bit_length()
 
 
-def write_jpeg(w: int, h: int, comps, blocks, qtables) -> bytes:
-    """comps: [(h_samp, v_samp, tq)], 1 or 3 components (Huffman tables 0 for the first, 1 for the
-    others); blocks: per component an int array [bh, bw, 64] of quantised coefficients in ZIGZAG order
-    (DC as absolute values: the DPCM is done here); qtables: {tq: 64 values (zigzag order)}, a table
-    with a value > 255 is written with 16-bit precision."""
-    tabs = _annex_k_tables()
-    dc = [_codes(*tabs[(0, 0)]), _codes(*tabs[(0, 1)])]
-    ac = [_codes(*tabs[(1, 0)]), _codes(*tabs[(1, 1)])]
+def write_jpeg(w: int, h: int, comps, blocks, qtables, huff=None) -> bytes:
+    """comps: [(h_samp, v_samp, tq)], 1 or 3 components; blocks: per component an int array
+    [bh, bw, 64] of quantised coefficients in ZIGZAG order (DC as absolute values: the DPCM is done
+    here); qtables: {tq: 64 values (zigzag order)}, a table with a value > 255 is written with 16-bit
+    precision.  huff: per component its (DC, AC) table ids, default 0 for the first component and 1
+    for the others; id 2 is a copy of the luma tables (Annex K ids 0) under its own id, so
+    huff=[(0, 0), (1, 1), (2, 2)] makes a scan of 6 distinct table slots."""
+    tabs = dict(_annex_k_tables())
+    tabs[(0, 2)], tabs[(1, 2)] = tabs[(0, 0)], tabs[(1, 0)]
+    if huff is None:
+        huff = [(0, 0) if ci == 0 else (1, 1) for ci in range(len(comps))]
+    dc = [_codes(*tabs[(0, t)]) for t in range(3)]
+    ac = [_codes(*tabs[(1, t)]) for t in range(3)]
+    used = {(0, d) for d, _ in huff} | {(1, a) for _, a in huff}
     hmax = max(c[0] for c in comps)
     vmax = max(c[1] for c in comps)
     mcux = -(-w // (8 * hmax))
@@ -113,19 +119,18 @@ def write_jpeg(w: int, h: int, comps, blocks, qtables) -> bytes:
         sof += bytes([ci + 1, (hs << 4) | vs, tq])
     marker(0xC0, sof)
     for (tc, th), (bits, vals) in sorted(tabs.items()):
-        if th < (1 if len(comps) == 1 else 2):
+        if (tc, th) in used:
             marker(0xC4, bytes([(tc << 4) | th] + bits + vals))
     sos = bytes([len(comps)])
     for ci in range(len(comps)):
-        t = 0 if ci == 0 else 1
-        sos += bytes([ci + 1, (t << 4) | t])
+        sos += bytes([ci + 1, (huff[ci][0] << 4) | huff[ci][1]])
     marker(0xDA, sos + bytes([0, 63, 0]))
     bw = _BitWriter()
     pred = [0] * len(comps)
     for my in range(mcuy):
         for mx in range(mcux):
             for ci, (hs, vs, _) in enumerate(comps):
-                t = 0 if ci == 0 else 1
+                td, ta = huff[ci]
                 hh, vv = (hs, vs) if len(comps) > 1 else (1, 1)
                 for dy in range(vv):
                     for dx in range(hh):
@@ -133,7 +138,7 @@ def write_jpeg(w: int, h: int, comps, blocks, qtables) -> bytes:
                         diff = int(blk[0]) - pred[ci]
                         pred[ci] = int(blk[0])
                         s = _category(diff)
-                        code, ln = dc[t][s]
+                        code, ln = dc[td][s]
                         bw.put(code, ln)
                         if s:
                             bw.put(diff if diff > 0 else diff - 1 + (1 << s), s)
@@ -145,16 +150,16 @@ def write_jpeg(w: int, h: int, comps, blocks, qtables) -> bytes:
                                 run += 1
                                 continue
                             while run > 15:
-                                code, ln = ac[t][0xF0]
+                                code, ln = ac[ta][0xF0]
                                 bw.put(code, ln)
                                 run -= 16
                             s = _category(v)
-                            code, ln = ac[t][(run << 4) | s]
+                            code, ln = ac[ta][(run << 4) | s]
                             bw.put(code, ln)
                             bw.put(v if v > 0 else v - 1 + (1 << s), s)
                             run = 0
                         if last < 63:
-                            code, ln = ac[t][0x00]
+                            code, ln = ac[ta][0x00]
                             bw.put(code, ln)
     bw.flush()
     seg.extend(bw.out)
@@ -213,4 +218,37 @@ def extreme_jpegs(seed: int, n: int) -> list[bytes]:
             else:
                 qtabs[tq] = rng.integers(1, 65536, 64)
         out.append(write_jpeg(w, h, comps, blocks, qtabs))
+    return out
+
+
+def six_slot_jpegs(seed: int, n: int, w: int = 160, h: int = 120) -> list[bytes]:
+    """Baseline 4:2:0 / 4:4:4 JPEGs whose Cb and Cr components use their own DC/AC Huffman tables
+    (ids 1 and 2: 6 distinct table slots, the kernels' 10-bit entropy route), with natural-looking
+    coefficients: a DC random walk and a few small low-frequency AC terms per block."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        comps = [(2, 2, 0), (1, 1, 1), (1, 1, 1)] if i % 2 == 0 else [(1, 1, 0), (1, 1, 1), (1, 1, 1)]
+        hmax, vmax = max(c[0] for c in comps), max(c[1] for c in comps)
+        mcux, mcuy = -(-w // (8 * hmax)), -(-h // (8 * vmax))
+        blocks = []
+        for hs, vs, _ in comps:
+            bh, bwid = mcuy * vs, mcux * hs
+            b = np.zeros((bh, bwid, 64), np.int64)
+            nz = rng.integers(0, 12, (bh, bwid))
+            for y in range(bh):
+                for x in range(bwid):
+                    k = rng.choice(np.arange(1, 40), int(nz[y, x]), replace=False)
+                    b[y, x, k] = rng.integers(-40, 41, len(k))
+            blocks.append(b)
+        for ci, (hs, vs, _) in enumerate(comps):
+            dcv = 0
+            for my in range(mcuy):
+                for mx in range(mcux):
+                    for dy in range(vs):
+                        for dx in range(hs):
+                            dcv = int(np.clip(dcv + rng.integers(-60, 61), -1000, 1000))
+                            blocks[ci][my * vs + dy, mx * hs + dx, 0] = dcv
+        q = {0: rng.integers(2, 40, 64), 1: rng.integers(2, 60, 64)}
+        out.append(write_jpeg(w, h, comps, blocks, q, huff=[(0, 0), (1, 1), (2, 2)]))
     return out

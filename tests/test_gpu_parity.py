@@ -241,6 +241,29 @@ def test_simd_idct_semantics_on_extreme_coefficients_vs_oracle(engine):
         np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res, flip=flips[k]), err_msg=f"image {k}")
 
 
+@pytest.mark.parametrize("n", [1, 3, 40])
+def test_six_table_slot_images_vs_oracle(engine, n):
+    """Baseline images whose Cb and Cr use their own DC/AC Huffman tables (6 slots, the 10-bit entropy
+    route), alone and mixed with PIL-encoded 4-slot images: batches of <= 32 host images run in latency
+    mode, whose multi-hypothesis pass only the 11-bit routes launch (such an image must keep
+    the ordinary speculative pass); 40 runs the throughput plan.  Bit-exact against the oracle."""
+    from tests.golden.coefjpeg import six_slot_jpegs
+    from tests.golden.synth import encode_jpeg, synth_rgb
+    six = six_slot_jpegs(41, 4, 320, 240)
+    rng = np.random.default_rng(5)
+    jpgs = []
+    for k in range(n):
+        jpgs.append(six[k % 4] if k % 2 == 0 else encode_jpeg(synth_rgb(rng, 320, 240), 90))
+    res = (96, 80)
+    got, st = engine.decode_resize(jpgs, res)
+    assert (st == 0).all(), st
+    for k, j in enumerate(jpgs):
+        np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res), err_msg=f"image {k}")
+    full, st = engine.decode_resize(six[:1], (240, 320), layout="hwc")
+    assert st[0] == 0
+    np.testing.assert_array_equal(full[0].cpu().numpy(), O.decode(six[0]))
+
+
 def test_fill_stuffed_streams_rerun_on_pil_through_the_transform(engine):
     """FF FF .. 00 inside a baseline scan: the GPU reports CORRUPT, the per-sample transform reruns the
     sample on PIL, so the output equals the reference's PIL decode + resize."""

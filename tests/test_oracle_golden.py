@@ -319,6 +319,19 @@ def test_oracle_simd_idct_matches_pil_on_extreme_coefficients():
         np.testing.assert_array_equal(O.decode(j), ref, err_msg=f"image {k}")
 
 
+def test_oracle_matches_pil_on_six_table_slot_jpegs():
+    """Cb and Cr coded with their own DC/AC Huffman tables (6 distinct table slots; the kernels' 10-bit
+    entropy route): the oracle equals PIL bit for bit (pins the GPU test of the same files)."""
+    import io
+
+    from PIL import Image
+
+    from tests.golden.coefjpeg import six_slot_jpegs
+    for k, j in enumerate(six_slot_jpegs(31, 6)):
+        ref = np.asarray(Image.open(io.BytesIO(j)).convert("RGB"))
+        np.testing.assert_array_equal(O.decode(j), ref, err_msg=f"image {k}")
+
+
 def test_fill_stuffing_predicate():
     from tests.golden.synth import encode_jpeg, has_fill_stuffing, synth_rgb
     j = encode_jpeg(synth_rgb(np.random.default_rng(3), 64, 48), 90)

@@ -39,8 +39,12 @@ MODES = {
     # comparators in the same loader shape (no sds_amd): a transform that only reads the file and returns
     # a constant 3x256x256 uint8 tensor (the loader's own ceiling), and plain Pillow decode + centre crop +
     # bilinear resize on the worker's CPU (the reference's per-sample library, not its exact transform)
+    "null_fork_workers2_pinned": (2, True, None, None, "null"),
+    "null_fork_workers4_pinned": (4, True, None, None, "null"),
     "null_fork_workers8_pinned": (8, True, None, None, "null"),
     "null_fork_workers16_pinned": (16, True, None, None, "null"),
+    "pil_fork_workers2_pinned": (2, True, None, None, "pil"),
+    "pil_fork_workers4_pinned": (4, True, None, None, "pil"),
     "pil_fork_workers8_pinned": (8, True, None, None, "pil"),
     "pil_fork_workers16_pinned": (16, True, None, None, "pil"),
 }
@@ -128,11 +132,15 @@ def run_mode(mode, n_files, seconds):
 def main():
     n_files = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     seconds = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
-    if len(sys.argv) > 3:
+    if len(sys.argv) > 3 and sys.argv[3] in MODES:
         run_mode(sys.argv[3], n_files, seconds)
         return
     import subprocess
-    for mode in MODES:  # each mode in a fresh process (a forked worker needs a parent that never touched HIP)
+    # optional: a comma-separated list of modes (or prefixes) to run
+    sel = sys.argv[3].split(",") if len(sys.argv) > 3 else None
+    for mode in MODES:
+        if sel and not any(mode.startswith(p) for p in sel):
+            continue  # each mode in a fresh process (a forked worker needs a parent that never touched HIP)
         subprocess.run([sys.executable, os.path.abspath(__file__), str(n_files), str(seconds), mode], check=True,
                        timeout=300)
 
