@@ -1105,49 +1105,9 @@ struct LdsWriteT {
   TT T;
   alignas(16) int16_t stage[(kEntThreads + 1) * kStageStride];  // + one shared sink block
   uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
-  int32_t krect[kMaxBlocksPerMcu][4];     // MCU block b: stored iff MCU column in [0], [1], MCU row in [2], [3]
-  int32_t keep_all;
   int32_t bad;
   unsigned long long sym;
 };
-
-// Exact a / b for 0 <= a < 2^24, 1 <= b: float estimate (error < 2), then two corrections each way.
-__device__ __forceinline__ int div_exact24(int a, int b, float rb) {
-  int q = (int)((float)a * rb);
-  q -= q * b > a ? 1 : 0;
-  q -= q * b > a ? 1 : 0;
-  q += (q + 1) * b <= a ? 1 : 0;
-  q += (q + 1) * b <= a ? 1 : 0;
-  return q;
-}
-
-// The coefficient rectangle (comp_block_rect, the blocks k_idct reads) as per-MCU-block ranges of MCU
-// columns and rows: block b of MCU (mx, my) is component c's block (mx h + dx, my v + dy).
-__device__ void write_rect(const ImgDesc* d, int32_t (*krect)[4], int32_t* keep_all) {
-  const int t = threadIdx.x;
-  if (t < d->bpm) {
-    const int c = d->blk_comp[t];
-    const int h = d->ncomp == 1 ? 1 : d->comp[c].h, v = d->ncomp == 1 ? 1 : d->comp[c].v;
-    const int dx = d->blk_dx[t], dy = d->blk_dy[t];
-    int bx0, bx1, by0, by1;
-    if (comp_block_rect(*d, c, bx0, bx1, by0, by1)) {
-      krect[t][0] = bx0 - dx <= 0 ? 0 : (bx0 - dx + h - 1) / h;
-      krect[t][1] = bx1 - dx < 0 ? -1 : (bx1 - dx) / h;
-      krect[t][2] = by0 - dy <= 0 ? 0 : (by0 - dy + v - 1) / v;
-      krect[t][3] = by1 - dy < 0 ? -1 : (by1 - dy) / v;
-    } else {
-      krect[t][0] = krect[t][2] = 1;
-      krect[t][1] = krect[t][3] = 0;
-    }
-  }
-  __syncthreads();
-  if (t == 0) {
-    bool all = true;
-    for (int b = 0; b < d->bpm; b++)
-      all &= krect[b][0] <= 0 && krect[b][1] >= d->mcux - 1 && krect[b][2] <= 0 && krect[b][3] >= d->mcuy - 1;
-    *keep_all = all;
-  }
-}
 
 // The compact two-level tables from the image's LB = 11 tables (HBM).  The staging area serves as
 // the scan's scratch before it is cleared.
@@ -1225,12 +1185,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     L.it = 0;
     if (kStats) L.t0 = __builtin_amdgcn_s_memtime();
   }
-  write_rect(d, L.krect, &L.keep_all);
   __syncthreads();
-  // only the blocks k_idct reads are stored (a centre crop of a 4:3 image: about 4 in 5)
-  const bool keep_all = L.keep_all != 0;
-  const int bpm_i = d->bpm, mcux_i = d->mcux;
-  const float rbpm = 1.0f / (float)bpm_i, rmcux = 1.0f / (float)mcux_i;
   const TT& T = L.T;
   const BlkCtx K = make_ctx(T, d->bpm);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(scratch + d->off_ustream);
@@ -1337,14 +1292,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
               const uint32_t f = L.flist[wv][bi];
               uint4* sp = reinterpret_cast<uint4*>(L.stage + (f >> 24) * kStageStride) + (lane & 7);
               const uint4 v = *sp;
-              const int gb = (int)(f & 0xFFFFFF);
-              bool keep = true;
-              if (!keep_all) {  // (uniform) MCU (mx, my) and MCU block b of decode index gb
-                const int m = div_exact24(gb, bpm_i, rbpm), b = gb - m * bpm_i;
-                const int my = div_exact24(m, mcux_i, rmcux), mx = m - my * mcux_i;
-                keep = mx >= L.krect[b][0] && mx <= L.krect[b][1] && my >= L.krect[b][2] && my <= L.krect[b][3];
-              }
-              if (keep) store_coef16(reinterpret_cast<uint4*>(coef + (int64_t)gb * 64) + (lane & 7), v);
+              store_coef16(reinterpret_cast<uint4*>(coef + (int64_t)(f & 0xFFFFFF) * 64) + (lane & 7), v);
               *sp = make_uint4(0, 0, 0, 0);
             }
           }

@@ -47,8 +47,8 @@ struct FGeo {
 
 template <int LAY, int KT>
 struct LdsF {
-  uint32_t st[FGeo<LAY>::kStageDW];                          // step's plane rows: 4 luma, then Cb, Cr
-  uint8_t rgb[FGeo<LAY>::kRgbRows > 0 ? FGeo<LAY>::kRgbRows : 1][3][kFRgbW];  // converted rows, planar
+  alignas(16) uint32_t st[FGeo<LAY>::kStageDW];              // step's plane rows: 4 luma, then Cb, Cr
+  alignas(16) uint8_t rgb[FGeo<LAY>::kRgbRows > 0 ? FGeo<LAY>::kRgbRows : 1][3][kFRgbW];  // converted rows, planar
   uint32_t ring[rs_ring_dw(KT)];                             // per column: H results of the last R rows
   int32_t vb[kMaxStrip][2];                                  // strip rows: vertical window (first, count)
   int32_t vw[kMaxStrip][rs_vtaps(KT)];                       // strip rows: vertical weights
@@ -345,15 +345,24 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
       if (more && !kGlds) issue(nxt);
       if (LAY != kRsGray) {
         // B. fancy upsampling + ycc->rgb on 8 pixels per item
-        for (int it = t; it < nr * ng; it += kFThreads) {
-          int q = 0;  // step row of the item (it / ng without a division)
-#pragma unroll
-          for (int k = 1; k < kFRows; k++) q += it >= k * ng ? 1 : 0;
-          const int gi = it - q * ng;
+        // items of one step row per wave (64 item slots per row, 128 when the tile needs more than 64
+        // groups): a wave's chroma and luma reads then never straddle two rows, whose words met
+        // bank conflicts, and its row is uniform
+        static_assert(kMaxSpan / 8 + 2 <= 128, "a row's items fit two waves");
+        const int rsh = ng > 64 ? 7 : 6;
+        for (int it = t; it < (nr << rsh); it += kFThreads) {
+          const int q = __builtin_amdgcn_readfirstlane(it >> rsh);  // step row of the item
+          const int gi = it - (q << rsh);
+          if (gi >= ng) continue;
           const int x = xb + 8 * gi, jg = x >> 1;
           const int oY = L.rinfo[q][0], oBi = L.rinfo[q][1], oRi = L.rinfo[q][3];
           const uint32_t* sw = L.st;
-          const uint32_t y0 = sw[(oY + x) >> 2], y1 = sw[(oY + x + 4) >> 2];
+          // the item's 8 luma bytes as one 8-byte read (oY + x is 8-aligned: kFYDW is even, xb and x are
+          // multiples of 8): consecutive items 8 bytes apart fill all 64 banks, where two dword reads at
+          // a 2-dword lane stride met 2-way bank conflicts
+          static_assert(kFYDW % 2 == 0, "8-byte aligned luma rows");
+          const uint2 yy = *reinterpret_cast<const uint2*>(&sw[(oY + x) >> 2]);
+          const uint32_t y0 = yy.x, y1 = yy.y;
           uint32_t wr[2] = {0, 0}, wg[2] = {0, 0}, wb[2] = {0, 0};
           if (LAY == kRs444) {
             const uint32_t cbw[2] = {sw[(oBi + x) >> 2], sw[(oBi + x + 4) >> 2]};
@@ -480,13 +489,12 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
               wb[k >> 1] |= (uint32_t)(b0 | (b1 << 8)) << sh;
             }
           }
-          uint32_t* o = reinterpret_cast<uint32_t*>(&L.rgb[q][0][x - xb]);
-          o[0] = wr[0];
-          o[1] = wr[1];
-          o[kFRgbW / 4] = wg[0];
-          o[kFRgbW / 4 + 1] = wg[1];
-          o[kFRgbW / 2] = wb[0];
-          o[kFRgbW / 2 + 1] = wb[1];
+          // one 8-byte store per channel (x - xb and kFRgbW are multiples of 8)
+          static_assert(kFRgbW % 8 == 0, "8-byte aligned RGB rows");
+          uint2* o = reinterpret_cast<uint2*>(&L.rgb[q][0][x - xb]);
+          o[0] = make_uint2(wr[0], wr[1]);
+          o[kFRgbW / 8] = make_uint2(wg[0], wg[1]);
+          o[kFRgbW / 4] = make_uint2(wb[0], wb[1]);
         }
         __syncthreads();
         if (kGlds && more) issue_lds(nxt);
