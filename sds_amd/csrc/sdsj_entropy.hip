@@ -1111,12 +1111,13 @@ struct LdsWriteT {
 
 // The compact two-level tables from the image's LB = 11 tables (HBM).  The staging area serves as
 // the scan's scratch before it is cleared.
+template <int NT = kEntThreads>
 __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tmp) {
   const int t = threadIdx.x;
   const int ns = g->nslots;
   if (!variant_owns<11>(ns)) return ns;
-  // which 9-bit prefixes lead to longer codes: 8 consecutive prefixes per thread, one block scan
-  constexpr int kPer = (4 << kW1) / kEntThreads;
+  // which 9-bit prefixes lead to longer codes: (4 << kW1) / NT consecutive prefixes per thread, one block scan
+  constexpr int kPer = (4 << kW1) / NT;
   int cnt = 0;
   uint32_t longmask = 0;
 #pragma unroll
@@ -1129,7 +1130,7 @@ __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tm
     cnt += lng ? 1 : 0;
   }
   int total;
-  int base = block_excl_scan<kEntThreads>(cnt, tmp, &total);
+  int base = block_excl_scan<NT>(cnt, tmp, &total);
 #pragma unroll
   for (int j = 0; j < kPer; j++) {
     const int i = t * kPer + j, q = i >> kW1, k = i & ((1 << kW1) - 1);
@@ -1145,13 +1146,13 @@ __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tm
     }
     W.lut[i] = (uint16_t)e;
   }
-  for (int i = t; i < 4 * 18; i += kEntThreads) {
+  for (int i = t; i < 4 * 18; i += NT) {
     W.maxcode[i / 18][i % 18] = g->maxcode[i / 18][i % 18];
     W.valoff[i / 18][i % 18] = g->valoff[i / 18][i % 18];
   }
   const uint32_t* gv = reinterpret_cast<const uint32_t*>(g->vals);
   uint32_t* wvls = reinterpret_cast<uint32_t*>(W.vals);
-  for (int i = t; i < 4 * 64; i += kEntThreads) wvls[i] = gv[i];
+  for (int i = t; i < 4 * 64; i += NT) wvls[i] = gv[i];
   if (t == 0) {
     W.pk_dc[0] = g->pk_dc[0];
     W.pk_dc[1] = g->pk_dc[1];
@@ -1321,6 +1322,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     d->t_write = (int64_t)(__builtin_amdgcn_s_memtime() - L.t0);
   }
 }
+
 
 template <int LB, int PHASE, int NTS = kSyncThreads, int NSPEC = kEntThreads>
 __device__ __forceinline__ void ent_phase(int img, int grp, ImgDesc* descs, const EntTables* tables, uint8_t* scratch) {

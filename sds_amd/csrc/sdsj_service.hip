@@ -120,6 +120,10 @@ class Service {
 
   int run() {
     trace_ = getenv("SDSJ_SERVICE_TRACE") != nullptr;
+    // SDSJ_SERVICE_SPIN=1: the engine threads spin in their stream waits (HIP's default policy) instead
+    // of sleeping on them; sleeping leaves the waited-on GPU time's CPU to the DataLoader workers
+    const char* spin = getenv("SDSJ_SERVICE_SPIN");
+    if (!(spin && spin[0] == '1')) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
     if (hipSetDevice(cfg_.device) != hipSuccess) return fail("hipSetDevice", SDSJ_EHIP);
     const int nl = cfg_.engines > 0 ? cfg_.engines : 8;
     max_batch_ = cfg_.max_batch > 0 ? cfg_.max_batch : 64;

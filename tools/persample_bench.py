@@ -83,6 +83,7 @@ def run_mode(mode, n_files, seconds):
     from sds_amd.presets import create_standard_image_pipeline
     from tests.golden.synth import synth_jpegs
     from tests.loader_cases import FolderDataset
+    t_start = time.perf_counter()
     nw, pin, ctx, odev, service = MODES[mode]
     jpgs = synth_jpegs(64, seed=2024)
     d = tempfile.mkdtemp()
@@ -123,10 +124,21 @@ def run_mode(mode, n_files, seconds):
     if torch.cuda.is_initialized():
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # CPU seconds of the decode service process over the whole run (start-up included), if one runs
+    svc_cpu = None
+    try:
+        from sds_amd import service as _svc
+        for h in _svc._handles.values():
+            with open(f"/proc/{h.proc.pid}/stat") as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            svc_cpu = round((int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK"), 2)
+    except Exception:  # noqa: BLE001  (no service, or not Linux)
+        pass
     print(json.dumps({"mode": mode, "images_per_s": round(n / dt, 1), "images": n, "seconds": round(dt, 2),
                       "num_workers": nw, "pin_memory": pin, "context": ctx or "fork",
                       "output_device": "cpu" if service else (odev or "cuda"), "service": service,
-                      "batch_size": BATCH if nw else None, "first_batch": first}), flush=True)
+                      "batch_size": BATCH if nw else None, "first_batch": first,
+                      "service_cpu_s": svc_cpu, "wall_s_incl_startup": round(time.perf_counter() - t_start, 2)}), flush=True)
 
 
 def main():
