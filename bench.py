@@ -323,7 +323,7 @@ def main():
     # batches: one engine call per step, whose lanes drain at its end (the caller's stream orders the
     # next call after it), so larger batches amortise that (configs[1]: 455k images/s at 4096, 476k
     # at 16384; configs[2]: 45.0k at 512, 59.8k at 2048 -- DESIGN.md §5)
-    defaults = {"batch": 2048, "rows": 16384, "pool": 96, "res": 512} if mixed else \
+    defaults = {"batch": 2048, "rows": 16384, "pool": 1024, "res": 512} if mixed else \
         {"batch": 1024, "rows": 16384, "pool": 256, "res": 512} if e2e else \
         {"batch": 16384, "rows": None, "pool": 1024, "res": 256}
     for k, v in defaults.items():

@@ -292,7 +292,10 @@ class Service {
         c->reply(r.seq, SDSJ_EINVAL);
       }
     }
-    if (queued) qcv_.notify_all();
+    // one request wakes one idle engine thread (waking them all cost each request a herd of wake-ups
+    // that found the queue drained); several may need several
+    if (queued == 1) qcv_.notify_one();
+    else if (queued > 1) qcv_.notify_all();
   }
 
   // Engine thread: the oldest pending request and every pending request with its op (up to max_batch)

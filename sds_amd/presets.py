@@ -451,7 +451,15 @@ def create_standard_image_pipeline(
     service="auto",
 ) -> Sequence[SampleTransform]:
     """presets.py:716-744 with the decode/resize/to-tensor/normalise chain fused on the GPU.  ``service``:
-    see GpuDecodeResizeImageTransform (the decode service for DataLoader workers)."""
+    see GpuDecodeResizeImageTransform (the decode service for DataLoader workers).
+
+    Output device: with the default ``service="auto"`` and ``output_device=None`` the process that built
+    the pipeline gets device tensors (it decodes in-process), while its forked DataLoader workers get
+    host tensors (they decode through the service: the reference's type, which ``pin_memory=True``
+    pins).  Pass ``output_device="cpu"`` for host tensors everywhere, or ``service=None`` for device
+    tensors everywhere (workers then create their own engines: spawn / forkserver workers, INTEGRATION.md
+    §1).  On a machine with a GPU, ``service="auto"`` starts the service process at construction -- it
+    sleeps without a GPU context until a worker connects, and exits with this process."""
     transforms: list = [
         LoadFromDiskTransform([image_field]),
         GpuDecodeResizeImageTransform(input_field=image_field, output_field=output_field, resolution=resolution,

@@ -89,7 +89,9 @@ def ensure_service(device: int = 0, engines: int | None = None, max_batch: int =
     address (an abstract AF_UNIX name).  Call it before DataLoader workers fork -- the pipeline factory
     does.  The process starting it needs no GPU; the service initialises HIP in its own process."""
     if engines is None:
-        engines = int(os.environ.get("SDS_AMD_SERVICE_ENGINES", "8"))
+        # 4: the loader-shape sweep (profiles/r05_persample.jsonl) put 4 engines level with 8 at 8 workers
+        # and ahead at 16, with a third less service CPU than 8
+        engines = int(os.environ.get("SDS_AMD_SERVICE_ENGINES", "4"))
     key = (os.getpid(), int(device))
     with _handles_lock:
         h = _handles.get(key)

@@ -4,7 +4,7 @@ training process decodes each collated batch on the GPU -- synchronously (GpuDec
 with one batch in flight (GpuDecodeBatch.stream: pinned double buffering, H2D + host staging of batch
 k + 1 overlapped with batch k's decode).  Inputs: a folder of synthetic 640x480 q90 JPEGs (configs[0]
 shape) -> 256x256 uint8.  Prints one JSON line per mode.
-    python tools/batched_bench.py [n_files] [seconds] [batch]"""
+    python tools/batched_bench.py [n_files] [seconds] [batch] [num_workers]"""
 import json
 import os
 import sys
@@ -22,6 +22,7 @@ def main():
     n_files = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     seconds = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
     bs = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    nw = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     from sds_amd.batched import GpuDecodeBatch, create_deferred_image_pipeline
     from tests.golden.synth import synth_jpegs
     from tests.loader_cases import FolderDataset
@@ -35,7 +36,7 @@ def main():
         paths.append(p)
     ds = FolderDataset(paths, create_deferred_image_pipeline("jpg"))
     # CPU-only workers (bytes), forked before the parent touches the GPU; persistent across epochs
-    loader = DataLoader(ds, batch_size=bs, num_workers=8, persistent_workers=True, prefetch_factor=4)
+    loader = DataLoader(ds, batch_size=bs, num_workers=nw, persistent_workers=True, prefetch_factor=4)
     dec = GpuDecodeBatch("jpg", (256, 256), device="cuda")
 
     def epochs():
@@ -60,7 +61,7 @@ def main():
         dt = time.perf_counter() - t0
         it.close() if hasattr(it, "close") else None
         print(json.dumps({"mode": f"gpu_decode_batch_{mode}", "images_per_s": round(n / dt, 1), "images": n,
-                          "seconds": round(dt, 2), "batch": bs, "num_workers": 8, "first_batch": first}), flush=True)
+                          "seconds": round(dt, 2), "batch": bs, "num_workers": nw, "first_batch": first}), flush=True)
 
 
 if __name__ == "__main__":
