@@ -447,6 +447,7 @@ struct BlkCtx {
   uint64_t pdc, pac;
   uint32_t pc;
   int bpm;
+  uint64_t p6;  // images of <= 4 table slots (LB = 11): per MCU block 6 bits, DC slot | AC slot << 2 | comp << 4
 };
 
 __device__ __forceinline__ int ctx_dc(const BlkCtx& k, int blk) { return (int)(k.pdc >> (4 * blk)) & 15; }
@@ -460,7 +461,19 @@ __device__ __forceinline__ BlkCtx make_ctx(const TT& T, int bpm) {
   k.pac = ((uint64_t)T.pk_ac[1] << 32) | T.pk_ac[0];
   k.pc = T.pk_c;
   k.bpm = bpm;
+  k.p6 = 0;
+  for (int b = 0; b < bpm; b++)
+    k.p6 |= (uint64_t)(((k.pdc >> (4 * b)) & 3) | (((k.pac >> (4 * b)) & 3) << 2) | (((k.pc >> (2 * b)) & 3) << 4)) << (6 * b);
   return k;
+}
+
+// All three of an MCU block's context values from the 6-bit packing (<= 4 table slots): one 64-bit
+// shift and three field extracts instead of three separate shifts of the 4- and 2-bit packings.
+__device__ __forceinline__ void ctx_all6(const BlkCtx& k, int blk, int& c, int& sdc, int& sac) {
+  const uint32_t x = (uint32_t)(k.p6 >> __umul24((unsigned)blk, 6u));  // (24-bit multiply: full rate)
+  sdc = (int)(x & 3);
+  sac = (int)((x >> 2) & 3);
+  c = (int)((x >> 4) & 3);
 }
 
 // jpeg_huff_decode for a code longer than LB bits (lookahead entry 0): the canonical search --
@@ -534,12 +547,12 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   // (two-level tables: a prefix without a second level -- more long prefixes than kW2Cap / 4 -- may
   // hold 10- and 11-bit codes too, so their search starts past the first level's width)
   if (l == 0) long_code<TT::kTwoLevel ? kW1 : LB>(T, slot, isdc, hi, l, s, r, bad);
-  // HUFF_EXTEND without branches: x < 2^(s-1) -> x - (2^s - 1); s = 0 -> 0
-  const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - s) & 31);
-  const uint32_t half = (1u << s) >> 1;
-  const int ext = x < half ? (int)x - (int)((1u << s) - 1u) : (int)x;
-  val = s != 0 ? ext : 0;
+  // HUFF_EXTEND without branches: the s extra bits follow the l code bits inside hi (l + s <= 27; a
+  // bad code has s = 0), x < 2^(s-1) -> x - (2^s - 1); s = 0 -> x = 0, mask 0 -> 0
   const int tot = l + s;
+  const uint32_t msk = (1u << s) - 1u;
+  const uint32_t x = (hi >> ((32 - tot) & 31)) & msk;
+  val = (x >> ((s - 1) & 31)) ? (int)x : (int)x - (int)msk;
   b.buf <<= tot;
   b.nb -= tot;
   b.pos += tot;
@@ -560,11 +573,10 @@ __device__ __forceinline__ void decode_step(const TT& T, BitsQ<Q>& b, int slot, 
   const int mb = (e >> 12) & 31, mdz = (e >> 17) & 127, eob = (e >> 24) & 1;
   const bool multi = (mb != 0) & (z + mdz <= 64);
   if (!multi && l == 0) long_code<kMW>(T, slot, isdc, hi, l, sz, rr, bad);
-  if (kVal) {  // (only DC values are used: a group is never a DC step)
-    const uint32_t x = (uint32_t)((b.buf << l) >> 32) >> ((32 - sz) & 31);
-    const uint32_t half = (1u << sz) >> 1;
-    const int ext = x < half ? (int)x - (int)((1u << sz) - 1u) : (int)x;
-    val = sz != 0 ? ext : 0;
+  if (kVal) {  // (only DC values are used: a group is never a DC step; as decode_sym's extension)
+    const uint32_t msk = (1u << sz) - 1u;
+    const uint32_t x = (hi >> ((32 - l - sz) & 31)) & msk;
+    val = (x >> ((sz - 1) & 31)) ? (int)x : (int)x - (int)msk;
   }
   const int tot = multi ? mb : l + sz;
   s = multi ? (eob ^ 1) : sz;
@@ -1208,7 +1220,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     int g = 0, gend = 0;  // decode-order block indices (total_blocks < 2^24, setup_geometry)
     uint32_t end_bit = 0, lim = 0;
     int s_int = 0;
-    bool writing = false, last_of_seg = false, run = false;
+    bool last_of_seg = false, run = false;
     uint32_t stop_pos = 0, stop_blk = 0;
     if (active) {
       const SubState& S = sub[j];
@@ -1220,13 +1232,17 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       p0 = S.dc_ex[0];
       p1 = S.dc_ex[1];
       p2 = S.dc_ex[2];
+      // entries are block boundaries (z = 0): the speculative and the sync passes stop only there
       blk = S.entry_bz >> 8;
-      z = S.entry_bz & 0xFF;
-      c = ctx_c(K, blk);
+      z = 0;
+      if constexpr (LB == 11) {
+        ctx_all6(K, blk, c, sdc, sac);
+      } else {
+        c = ctx_c(K, blk);
+        sdc = ctx_dc(K, blk);
+        sac = ctx_ac(K, blk);
+      }
       pc = c == 0 ? p0 : (c == 1 ? p1 : p2);  // the current block's component predictor
-      sdc = ctx_dc(K, blk);
-      sac = ctx_ac(K, blk);
-      writing = z == 0;
       end_bit = S.end_bit;
       s_int = s;
       lim = S.lim_bit;
@@ -1258,22 +1274,25 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           pc += isdc ? val : 0;
           // zigzag position k + r (jpeg_natural_order's guard entries send positions past 63 to 63)
           const int zp = z + r, wpos = zp < 63 ? zp : 63;
-          const bool put = writing & (isdc | (s != 0));
+          const bool put = isdc | (s != 0);
           L.stage[(put ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
           // block end by selects (no branches): the component's predictor back, the next block's out
           const bool done = next_z(z, s, r);
-          ready = done & writing;
+          ready = done;
           gdone = (uint32_t)g;
           p0 = (done & (c == 0)) ? pc : p0;
           p1 = (done & (c == 1)) ? pc : p1;
           p2 = (done & (c == 2)) ? pc : p2;
           blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
-          c = ctx_c(K, blk);
+          if constexpr (LB == 11) {
+            ctx_all6(K, blk, c, sdc, sac);
+          } else {
+            c = ctx_c(K, blk);
+            sdc = ctx_dc(K, blk);
+            sac = ctx_ac(K, blk);
+          }
           pc = done ? (c == 0 ? p0 : (c == 1 ? p1 : p2)) : pc;
-          sdc = ctx_dc(K, blk);
-          sac = ctx_ac(K, blk);
           g += done ? 1 : 0;
-          writing = writing | done;
           run = (g < gend) & !((z == 0) & ((stop_blk >> blk) & 1u) & (b.pos >= stop_pos));
         }
         // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
