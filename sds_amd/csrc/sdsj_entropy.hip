@@ -1115,7 +1115,7 @@ template <class TT>
 struct LdsWriteT {
   unsigned long long t0, it;
   TT T;
-  alignas(16) int16_t stage[(kEntThreads + 1) * kStageStride];  // + one shared sink block
+  alignas(16) int16_t stage[kEntThreads * kStageStride];
   uint32_t flist[kEntThreads / 64][64];  // (thread << 24) | block index (total_blocks < 2^24)
   int32_t bad;
   unsigned long long sym;
@@ -1190,7 +1190,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   if (!variant_owns<LB>(ns)) return;
   {
     uint4* z4 = reinterpret_cast<uint4*>(L.stage);
-    for (int i = t; i < (kEntThreads + 1) * kStageStride * 2 / 16; i += kEntThreads) z4[i] = make_uint4(0, 0, 0, 0);
+    for (int i = t; i < kEntThreads * kStageStride * 2 / 16; i += kEntThreads) z4[i] = make_uint4(0, 0, 0, 0);
   }
   if (t == 0) {
     L.bad = 0;
@@ -1207,7 +1207,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
   const int nsub = d->nsub;
   const int blocks_per_seg = d->restart_interval ? d->restart_interval * K.bpm : (int)d->total_blocks;
-  const int my_base = t * kStageStride, sink_base = kEntThreads * kStageStride;
+  const int my_base = t * kStageStride;
   int bad = 0;
   unsigned long long nsym = 0, witers = 0;
 
@@ -1272,10 +1272,11 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           bad |= sb;
           // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
           pc += isdc ? val : 0;
-          // zigzag position k + r (jpeg_natural_order's guard entries send positions past 63 to 63)
+          // zigzag position k + r (jpeg_natural_order's guard entries send positions past 63 to 63).  EOB
+          // and ZRL symbols (s = 0, val = 0) store a zero at a position of the block not written yet
+          // (positions only grow within a block, and a clamped store ends it), so every symbol stores
           const int zp = z + r, wpos = zp < 63 ? zp : 63;
-          const bool put = isdc | (s != 0);
-          L.stage[(put ? my_base : sink_base) + wpos] = (int16_t)(isdc ? pc : val);
+          L.stage[my_base + wpos] = (int16_t)(isdc ? pc : val);
           // block end by selects (no branches): the component's predictor back, the next block's out
           const bool done = next_z(z, s, r);
           ready = done;
