@@ -322,10 +322,11 @@ def main():
     e2e = args.workload == "e2e512"
     # batches: one engine call per step, whose lanes drain at its end (the caller's stream orders the
     # next call after it), so larger batches amortise that (configs[1]: 455k images/s at 4096, 476k
-    # at 16384; configs[2]: 45.0k at 512, 59.8k at 2048 -- DESIGN.md §5)
+    # at 16384; configs[2]: 45.0k at 512, 59.8k at 2048 -- DESIGN.md §5; round 5: 16,384 -> 32,768 +1.2 %,
+    # profiles/r05_batch.txt)
     defaults = {"batch": 2048, "rows": 16384, "pool": 1024, "res": 512} if mixed else \
         {"batch": 1024, "rows": 16384, "pool": 256, "res": 512} if e2e else \
-        {"batch": 16384, "rows": None, "pool": 1024, "res": 256}
+        {"batch": 32768, "rows": None, "pool": 1024, "res": 256}
     for k, v in defaults.items():
         if getattr(args, k) is None:
             setattr(args, k, v)

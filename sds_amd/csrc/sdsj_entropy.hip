@@ -667,7 +667,18 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   bits_init(b, src, ws, S.lim_bit);
   int blk = at ? at_blk : init_blk, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
   int d0 = 0, d1 = 0, d2 = 0;
-  int c = ctx_c(K, blk), sdc = ctx_dc(K, blk), sac = ctx_ac(K, blk);
+  // MCU block context: the 6-bit packing for the LB = 11 images (<= 4 table slots), else the 4-bit ones
+  auto ctx = [&](int bk, int& cc, int& dc_slot, int& ac_slot) {
+    if constexpr (kMulti) {
+      ctx_all6(K, bk, cc, dc_slot, ac_slot);
+    } else {
+      cc = ctx_c(K, bk);
+      dc_slot = ctx_dc(K, bk);
+      ac_slot = ctx_ac(K, bk);
+    }
+  };
+  int c, sdc, sac;
+  ctx(blk, c, sdc, sac);
   uint32_t entry = at ? at_p : start;
   int entry_blk = blk;
   bool warmup = !at && b.pos < start;
@@ -700,13 +711,11 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           if (kStats) nsym++;
           if (next_z(z, sz, r)) {
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
-            sdc = ctx_dc(K, blk);
-            sac = ctx_ac(K, blk);
+            ctx(blk, c, sdc, sac);
             if (b.pos >= start) {
               warmup = false;
               entry = b.pos;
               entry_blk = blk;
-              c = ctx_c(K, blk);
             }
           }
         }
@@ -739,9 +748,7 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           nrec += done ? 1 : 0;
           nblk += done ? 1 : 0;
           blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
-          c = ctx_c(K, blk);
-          sdc = ctx_dc(K, blk);
-          sac = ctx_ac(K, blk);
+          ctx(blk, c, sdc, sac);
           run = b.pos < end || z != 0;
         }
       }

@@ -1409,12 +1409,25 @@ __device__ void coeffs_one(int in_size, int out_size, int filter, int ksize, int
   bounds[2 * xx + 1] = xmax;
 }
 
-__global__ void __launch_bounds__(256) k_coeffs(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
+__global__ void __launch_bounds__(256) k_coeffs(int n, ImgDesc* __restrict__ descs, sdsj_op op,
                                                 uint8_t* __restrict__ scratch) {
   const int img = blockIdx.y;
   if (img >= n) return;
-  const ImgDesc* d = &descs[img];
+  ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->geo != kGeoResize) return;
+  // an image whose crop and passes equal the lane's first image's uses that image's tables (same
+  // inputs, same Pillow coefficients): most batches hold one source size
+  if (img > 0) {
+    const ImgDesc* a = &descs[0];
+    if (a->status == SDSJ_OK && a->geo == kGeoResize && a->cw == d->cw && a->ch == d->ch && a->need_h == d->need_h &&
+        a->need_v == d->need_v && a->ksh == d->ksh && a->ksv == d->ksv) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        d->off_kh = a->off_kh;  // (absolute scratch offsets after k_plan_apply)
+        d->off_kv = a->off_kv;
+      }
+      return;
+    }
+  }
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (d->need_h && i < op.out_w) {
     int32_t* b = reinterpret_cast<int32_t*>(scratch + d->off_kh);
@@ -1613,7 +1626,7 @@ hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int
   hipLaunchKernelGGL(k_color, dim3(64, n < 64 ? n : 64), dim3(256), 0, s, n, descs, scratch, routes, cap);
   return hipGetLastError();
 }
-hipError_t launch_coeffs(int n, const ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s) {
+hipError_t launch_coeffs(int n, ImgDesc* descs, const sdsj_op& op, uint8_t* scratch, hipStream_t s) {
   int mx = op.out_w > op.out_h ? op.out_w : op.out_h;
   hipLaunchKernelGGL(k_coeffs, dim3((mx + 255) / 256, n), dim3(256), 0, s, n, descs, op, scratch);
   return hipGetLastError();

@@ -7,8 +7,9 @@
 set -e
 export TMPDIR=/tmp
 export SDSJ_LANES=${SDSJ_LANES:-1}
-BATCH=${BATCH:-16384}  # bench.py's default configs[1] batch (the PMC summary is per dispatch of one lane)
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 --rows 20000 --batch $BATCH $*"
+BATCH=${BATCH:-32768}  # bench.py's default configs[1] batch (the PMC summary is per dispatch of one lane)
+ROWS=$(( BATCH + 4096 ))
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 --rows $ROWS --batch $BATCH $*"
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU" \
