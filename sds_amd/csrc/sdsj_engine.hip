@@ -28,7 +28,10 @@ using namespace sdsj;
 
 namespace {
 constexpr int kStages = 13;
-constexpr int kMaxLanes = 4;
+#ifndef SDSJ_MAX_LANES
+#define SDSJ_MAX_LANES 4
+#endif
+constexpr int kMaxLanes = SDSJ_MAX_LANES;
 const char* kStageNames[kStages] = {"parse", "plan",  "unstuff", "prog",  "entspec", "entsync", "entwrite",
                                     "idct",  "color", "coeffs",  "hpass", "vpass",   "resample"};
 constexpr int kMarkAfterSpec = 5;  // mark index at the end of the entspec stage
@@ -53,6 +56,13 @@ struct sdsj_engine {
   int32_t* d_routes_x = nullptr;
   hipStream_t aux[kMaxLanes - 1] = {};
   hipEvent_t ev_mid[kMaxLanes - 1] = {}, ev_join[kMaxLanes - 1] = {};
+  // route hint of the device path (sdsj_kernels.h route_grid): each call copies its lanes' route counts
+  // to pinned memory after k_plan; a later call folds a finished copy into the hint
+  uint64_t hint = kAllRoutes;
+  int32_t* h_rcounts = nullptr;  // [kMaxLanes][kNumRoutes]
+  hipEvent_t ev_rc[kMaxLanes] = {};
+  bool rc_pending = false;
+  int rc_lanes = 0;
   // frames path: host-planned descriptors and route list, staged through pinned memory
   ImgDesc* h_fdescs = nullptr;
   int32_t* h_froutes = nullptr;
@@ -181,9 +191,11 @@ struct Lane {
 
 // Runs the kernel sequence for one lane (n <= max_batch images) of device-resident inputs.
 // after_spec (optional) is recorded once the lane's speculative entropy pass is queued.
+// hint: routes expected to hold images (full grids); rc_lane >= 0: copy this lane's route counts to the
+// engine's pinned readback slot rc_lane after k_plan
 int run_lane(sdsj_engine* e, const Lane& ln, int n, bool small, const uint8_t* d_blob, int64_t blob_bytes, const int64_t* d_offsets,
              const int32_t* d_lengths, const sdsj_op& op, const uint8_t* d_flip, void* d_out, int32_t* d_status,
-             hipStream_t s, hipEvent_t after_spec, uint64_t rm) {
+             hipStream_t s, hipEvent_t after_spec, uint64_t rm, uint64_t hint = kAllRoutes, int rc_lane = -1) {
   std::vector<hipEvent_t>* evs = nullptr;
   if (e->timing) {
     if (e->ev_used == e->ev_sets.size()) {
@@ -202,18 +214,23 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, bool small, const uint8_t* d
   mark(1);
   const int cap = e->max_batch;
   SDSJ_HIP(e, launch_plan(n, ln.descs, e->capacity, ln.base, ln.total, ln.routes, cap, s));
+  if (rc_lane >= 0) {
+    SDSJ_HIP(e, hipMemcpyAsync(e->h_rcounts + rc_lane * kNumRoutes, ln.routes, sizeof(int32_t) * kNumRoutes,
+                               hipMemcpyDeviceToHost, s));
+    SDSJ_HIP(e, hipEventRecord(e->ev_rc[rc_lane], s));
+  }
   mark(2);
-  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_unstuff(n, d_blob, d_offsets, ln.descs, e->scratch, ln.routes, cap, s, rm, hint));
   SDSJ_HIP(e, launch_scanmap(n, d_blob, d_offsets, ln.descs, e->scratch, s));
   mark(3);
   // (after mark 3: the next lane may start while this lane's progressive images decode)
-  SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_prog(n, ln.descs, ln.tables, d_blob, d_offsets, d_lengths, e->scratch, ln.routes, cap, s, rm, hint));
   mark(4);
-  SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s, rm, small));
+  SDSJ_HIP(e, launch_entspec(n, ln.descs, ln.tables, ln.etab, e->scratch, ln.routes, cap, s, rm, small, hint));
   mark(5);
-  SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_entsync(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm, hint));
   mark(6);
-  SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm));
+  SDSJ_HIP(e, launch_entwrite(n, ln.descs, ln.etab, e->scratch, ln.routes, cap, s, rm, hint));
   mark(7);
   SDSJ_HIP(e, launch_idct(n, ln.descs, ln.tables, e->scratch, s));
   mark(8);
@@ -225,7 +242,7 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, bool small, const uint8_t* d
   mark(11);
   SDSJ_HIP(e, launch_vpass(n, ln.descs, op, e->scratch, d_flip, d_out, ln.routes, cap, e->d_lut, s, rm));
   mark(12);
-  SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s, rm));
+  SDSJ_HIP(e, launch_resample(n, ln.descs, op, e->scratch, d_flip, d_out, d_status, ln.routes, cap, e->d_lut, s, rm, hint));
   SDSJ_HIP(e, launch_finish(n, ln.descs, op, d_out, d_status, e->d_lut, d_lengths, e->d_counters, s));
   mark(13);
   return SDSJ_OK;
@@ -247,10 +264,36 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, int64_t blob_bytes, 
               uint64_t rm = kAllRoutes, bool small = false) {
   int nl = std::min(std::max(e->lanes, 1), kMaxLanes);
   while (nl > 1 && n < nl * kLaneMin) nl--;
+  // route hint: the host paths know their routes exactly (rm); the device path uses the routes that held
+  // images in the last batch whose counts have come back (all routes until one has), and requests a
+  // new readback when none is outstanding
+  uint64_t hint = rm;
+  bool readback = false;
+  if (rm == kAllRoutes) {
+    if (e->rc_pending) {
+      bool done = true;
+      for (int k = 0; k < e->rc_lanes; k++) done = done && hipEventQuery(e->ev_rc[k]) == hipSuccess;
+      if (done) {
+        uint64_t h = 0;
+        for (int k = 0; k < e->rc_lanes; k++)
+          for (int r = 0; r < kNumRoutes; r++)
+            if (e->h_rcounts[k * kNumRoutes + r] > 0) h |= 1ull << r;
+        if (h & (1ull << kRtEnt11M)) h |= 1ull << kRtEnt11G;
+        e->hint = h;
+        e->rc_pending = false;
+      }
+    }
+    hint = e->hint;
+    readback = !e->rc_pending;
+    if (readback) {
+      e->rc_pending = true;
+      e->rc_lanes = nl;
+    }
+  }
   const Lane first{e->descs, e->tables, e->d_etab, e->d_routes, e->d_total, nullptr};
   if (nl == 1)
     return run_lane(e, first, n, small, d_blob, blob_bytes, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr,
-                    rm);
+                    rm, hint, readback ? 0 : -1);
   for (int k = 0; k + 1 < nl; k++)
     if (!e->aux[k]) {
       SDSJ_HIP(e, hipStreamCreateWithFlags(&e->aux[k], hipStreamNonBlocking));
@@ -270,7 +313,7 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, int64_t blob_bytes, 
     if (k > 0) SDSJ_HIP(e, hipStreamWaitEvent(ls, e->ev_mid[k - 1], 0));
     int st = run_lane(e, ln, i1 - i0, small, d_blob, blob_bytes, d_offsets + i0, d_lengths + i0, op, d_flip ? d_flip + i0 : nullptr,
                       static_cast<uint8_t*>(d_out) + i0 * ob, d_status + i0, ls,
-                      k + 1 < nl ? e->ev_mid[k] : nullptr, rm);
+                      k + 1 < nl ? e->ev_mid[k] : nullptr, rm, hint, readback ? k : -1);
     if (st != SDSJ_OK) return st;
   }
   for (int k = 0; k + 1 < nl; k++) {
@@ -593,6 +636,9 @@ int sdsj_engine_create(int hip_device, const sdsj_cfg* cfg, sdsj_engine** out) {
   if (hipMalloc(&e->d_routes, sizeof(int32_t) * (size_t)route_ints(e->max_batch)) != hipSuccess)
     return cleanup(SDSJ_ENOMEM);
   if (hipMalloc(&e->d_lut, sizeof(float) * 256) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  if (hipHostMalloc(&e->h_rcounts, sizeof(int32_t) * kMaxLanes * kNumRoutes) != hipSuccess) return cleanup(SDSJ_ENOMEM);
+  for (int k = 0; k < kMaxLanes; k++)
+    if (hipEventCreateWithFlags(&e->ev_rc[k], hipEventDisableTiming) != hipSuccess) return cleanup(SDSJ_EHIP);
   if (hipMalloc(&e->d_counters, sizeof(unsigned long long) * SDSJ_NUM_COUNTERS) != hipSuccess) return cleanup(SDSJ_ENOMEM);
   if (hipMemset(e->d_counters, 0, sizeof(unsigned long long) * SDSJ_NUM_COUNTERS) != hipSuccess) return cleanup(SDSJ_EHIP);
   {
@@ -633,6 +679,9 @@ int sdsj_engine_destroy(sdsj_engine* e) {
     if (e->ev_mid[k]) (void)hipEventDestroy(e->ev_mid[k]);
     if (e->ev_join[k]) (void)hipEventDestroy(e->ev_join[k]);
   }
+  for (int k = 0; k < kMaxLanes; k++)
+    if (e->ev_rc[k]) (void)hipEventDestroy(e->ev_rc[k]);
+  (void)hipHostFree(e->h_rcounts);
   (void)hipHostFree(e->h_fdescs);
   (void)hipHostFree(e->h_froutes);
   (void)hipFree(e->d_lut);

@@ -1378,9 +1378,11 @@ __device__ __forceinline__ void ent_feed(ImgDesc* descs, const EntTables* tables
   }
   const int cnt = routes[RT];
   const int32_t* list = route_list(routes, cap, RT);
-  if (MODE == 0) {
-    if ((int)blockIdx.x >= cnt) return;
-    ent_phase<LB, PHASE, NTS, NSPEC>(list[blockIdx.x], 0, descs, tables, scratch);
+  if (MODE == 0) {  // one entry per workgroup at the full grid; a cold route's small grid strides (route_grid)
+    for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
+      ent_phase<LB, PHASE, NTS, NSPEC>(list[li], 0, descs, tables, scratch);
+      __syncthreads();  // LDS reuse by the next entry
+    }
     return;
   }
   for (int li = blockIdx.x; li < cnt; li += gridDim.x) {
@@ -1602,20 +1604,21 @@ constexpr int kTaskGrid = 4096;  // MODE 3 grid cap (>= the workgroups the chip 
 static int task_grid(int n) { return n * kMaxEntGroups < kTaskGrid ? n * kMaxEntGroups : kTaskGrid; }
 
 hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s, uint64_t rm, bool small) {
+                          int cap, hipStream_t s, uint64_t rm, bool small, uint64_t hint) {
   const int g = n;  // one workgroup per image on the main route
   EntTables* tables = static_cast<EntTables*>(etab);
   const int gs = g < 256 ? g : 256;
   if (route_on(rm, kRtEnt11) || route_on(rm, kRtEnt11M) || route_on(rm, kRtEnt10))
     hipLaunchKernelGGL(k_enttab, dim3(n), dim3(kEntThreads), 0, s, descs, specs, tables);
   if (route_on(rm, kRtEnt11))
-    hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0, kSpecThreads>), dim3(g), dim3(kSpecThreads), 0, s, descs, tables, scratch,
-                       routes, cap);
+    hipLaunchKernelGGL((k_entspec<11, kRtEnt11, 0, kSpecThreads>), dim3(route_grid(hint, kRtEnt11, g)), dim3(kSpecThreads), 0,
+                       s, descs, tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt11M))
-    hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3, kSpecThreadsG>), dim3(task_grid(n)), dim3(kSpecThreadsG), 0, s, descs,
-                       tables, scratch, routes, cap);
+    hipLaunchKernelGGL((k_entspec<11, kRtEnt11M, 3, kSpecThreadsG>), dim3(route_grid(hint, kRtEnt11M, task_grid(n))),
+                       dim3(kSpecThreadsG), 0, s, descs, tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
-    hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+    hipLaunchKernelGGL((k_entspec<10, kRtEnt10, 1>), dim3(route_grid(hint, kRtEnt10, gs)), dim3(kEntThreads), 0, s, descs,
+                       tables, scratch, routes, cap);
   if (SDSJ_MH && small) {  // latency-mode images (ImgDesc::mh; the kernels above skip them)
     constexpr int kMhGridY = 64;
     if (route_on(rm, kRtEnt11)) {
@@ -1631,34 +1634,36 @@ hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* e
 }
 
 hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, int32_t* routes, int cap, hipStream_t s,
-                          uint64_t rm) {
+                          uint64_t rm, uint64_t hint) {
   const int g = n;
   EntTables* tables = static_cast<EntTables*>(etab);
   const int gs = g < 256 ? g : 256;
   if (route_on(rm, kRtEnt11))
-    hipLaunchKernelGGL((k_entsync<11, kRtEnt11, 0, kSyncThreads>), dim3(g), dim3(kSyncThreads), 0, s, descs, tables,
-                       scratch, routes, cap);
+    hipLaunchKernelGGL((k_entsync<11, kRtEnt11, 0, kSyncThreads>), dim3(route_grid(hint, kRtEnt11, g)), dim3(kSyncThreads), 0,
+                       s, descs, tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt11M))
-    hipLaunchKernelGGL((k_entsync<11, kRtEnt11M, 0, kEntThreads>), dim3(g), dim3(kEntThreads), 0, s, descs, tables,
-                       scratch, routes, cap);
+    hipLaunchKernelGGL((k_entsync<11, kRtEnt11M, 0, kEntThreads>), dim3(route_grid(hint, kRtEnt11M, g)), dim3(kEntThreads), 0,
+                       s, descs, tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
-    hipLaunchKernelGGL((k_entsync<10, kRtEnt10, 1, kSyncThreads>), dim3(gs), dim3(kSyncThreads), 0, s, descs, tables,
-                       scratch, routes, cap);
+    hipLaunchKernelGGL((k_entsync<10, kRtEnt10, 1, kSyncThreads>), dim3(route_grid(hint, kRtEnt10, gs)), dim3(kSyncThreads), 0,
+                       s, descs, tables, scratch, routes, cap);
   return hipGetLastError();
 }
 
 hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
-                           hipStream_t s, uint64_t rm) {
+                           hipStream_t s, uint64_t rm, uint64_t hint) {
   const int g = n;  // one workgroup per image on the main route
   const EntTables* tables = static_cast<const EntTables*>(etab);
   const int gs = g < 256 ? g : 256;
   if (route_on(rm, kRtEnt11))
-    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(g), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11, 0>), dim3(route_grid(hint, kRtEnt11, g)), dim3(kEntThreads), 0, s, descs,
+                       tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt11M))
-    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(task_grid(n)), dim3(kEntThreads), 0, s, descs, tables,
-                       scratch, routes, cap);
+    hipLaunchKernelGGL((k_entwrite<11, kRtEnt11M, 3>), dim3(route_grid(hint, kRtEnt11M, task_grid(n))), dim3(kEntThreads), 0,
+                       s, descs, tables, scratch, routes, cap);
   if (route_on(rm, kRtEnt10))
-    hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(gs), dim3(kEntThreads), 0, s, descs, tables, scratch, routes, cap);
+    hipLaunchKernelGGL((k_entwrite<10, kRtEnt10, 1>), dim3(route_grid(hint, kRtEnt10, gs)), dim3(kEntThreads), 0, s, descs,
+                       tables, scratch, routes, cap);
   return hipGetLastError();
 }
 

@@ -10,6 +10,15 @@ namespace sdsj {
 // device-resident path passes kAllRoutes (its route lists exist only on the device).
 constexpr uint64_t kAllRoutes = ~0ull;
 SDSJ_HD inline bool route_on(uint64_t rm, int r) { return (rm >> r) & 1ull; }
+// Route hints (hint: bit r = route r held images in a recent batch of this engine): a launched route
+// outside the hint gets a small grid whose workgroups stride over its list -- exact for any count,
+// only slower -- instead of one workgroup per possible entry.  The device path launches every route
+// (its lists exist only on the device), and most of them are empty for a given dataset: thousands
+// of empty workgroups per launch otherwise (sdsj_engine.hip run_chunk keeps the hint).
+constexpr int kColdGrid = 64;
+inline unsigned route_grid(uint64_t hint, int r, int64_t full) {
+  return (unsigned)(route_on(hint, r) || full < kColdGrid ? full : kColdGrid);
+}
 // blob_bytes: the blob's size -- a sample whose [offset, offset + length) leaves it is reported EINVAL
 hipError_t launch_parse(int n, const uint8_t* blob, int64_t blob_bytes, const int64_t* offsets, const int32_t* lengths,
                         const sdsj_op& op, int warm_bits, bool small, ImgDesc* descs, ImgTables* tables, hipStream_t s);
@@ -18,23 +27,24 @@ hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* b
                        int cap, hipStream_t s);
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           const int32_t* routes, int cap,
-                          hipStream_t s, uint64_t rm = kAllRoutes);
+                          hipStream_t s, uint64_t rm = kAllRoutes, uint64_t hint = kAllRoutes);
 hipError_t launch_scanmap(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
                           hipStream_t s);
 // progressive images (route kRtProg): zero their coefficients, then one lane per image decodes all scans
 hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* blob, const int64_t* offsets,
                        const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,
-                       uint64_t rm = kAllRoutes);
+                       uint64_t rm = kAllRoutes, uint64_t hint = kAllRoutes);
 size_t enttab_bytes();  // per-image decode tables (k_enttab) held in HBM between the entropy kernels
 // k_enttab (decode tables) + k_entspec (subsequence layout, warm-up, speculative decode)
 // (small: a host-path latency-mode chunk, where ImgDesc::mh images take the multi-hypothesis pass)
 hipError_t launch_entspec(int n, ImgDesc* descs, const ImgTables* specs, void* etab, uint8_t* scratch, int32_t* routes,
-                          int cap, hipStream_t s, uint64_t rm = kAllRoutes, bool small = false);
+                          int cap, hipStream_t s, uint64_t rm = kAllRoutes, bool small = false,
+                          uint64_t hint = kAllRoutes);
 // k_entsync (sync rounds + segmented scan)
 hipError_t launch_entsync(int n, ImgDesc* descs, void* etab, uint8_t* scratch, int32_t* routes, int cap, hipStream_t s,
-                          uint64_t rm = kAllRoutes);
+                          uint64_t rm = kAllRoutes, uint64_t hint = kAllRoutes);
 hipError_t launch_entwrite(int n, ImgDesc* descs, const void* etab, uint8_t* scratch, int32_t* routes, int cap,
-                           hipStream_t s, uint64_t rm = kAllRoutes);
+                           hipStream_t s, uint64_t rm = kAllRoutes, uint64_t hint = kAllRoutes);
 hipError_t launch_idct(int n, const ImgDesc* descs, const ImgTables* tables, uint8_t* scratch, hipStream_t s);
 hipError_t launch_color(int n, const ImgDesc* descs, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,
                         uint64_t rm = kAllRoutes);
@@ -46,10 +56,10 @@ hipError_t launch_vpass(int n, const ImgDesc* descs, const sdsj_op& op, const ui
                         uint64_t rm = kAllRoutes);
 hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
                            void* out, int32_t* status, const int32_t* routes, int cap, const float* lut, hipStream_t s,
-                           uint64_t rm = kAllRoutes);
+                           uint64_t rm = kAllRoutes, uint64_t hint = kAllRoutes);
 hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
                               const uint8_t* flip, void* out, const int32_t* routes, int cap, const float* lut,
-                              hipStream_t s, uint64_t rm = kAllRoutes);
+                              hipStream_t s, uint64_t rm = kAllRoutes, uint64_t hint = kAllRoutes);
 // lengths: the samples' encoded sizes (null: raw frames); counters: SDSJ_CTR_* accumulators (or null)
 // (a negative length: the sample is reported as EINVAL -- an unreadable file of the host path)
 hipError_t launch_finish(int n, ImgDesc* descs, const sdsj_op& op, void* out, int32_t* status, const float* lut,

@@ -1582,7 +1582,7 @@ hipError_t launch_plan(int n, ImgDesc* descs, int64_t capacity, const int64_t* b
   return hipGetLastError();
 }
 hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, ImgDesc* descs, uint8_t* scratch,
-                          const int32_t* routes, int cap, hipStream_t s, uint64_t rm) {
+                          const int32_t* routes, int cap, hipStream_t s, uint64_t rm, uint64_t hint) {
   const int g = n < kUsLaunch ? n : kUsLaunch;
 #ifndef SDSJ_US_TILE_GRID
 #define SDSJ_US_TILE_GRID 16384
@@ -1593,11 +1593,15 @@ hipError_t launch_unstuff(int n, const uint8_t* blob, const int64_t* offsets, Im
 #endif
   const int gs = n < SDSJ_US_SERIAL_GRID ? n : SDSJ_US_SERIAL_GRID;
   if (route_on(rm, kRtUsSmall))
-    hipLaunchKernelGGL(k_us_serial, dim3(gs), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
-  if (route_on(rm, kRtUsBig)) {
-    hipLaunchKernelGGL(k_us_count, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
-    hipLaunchKernelGGL(k_us_scan, dim3(g), dim3(kUnstuffThreads), 0, s, descs, scratch, routes, cap);
-    hipLaunchKernelGGL(k_us_write, dim3(gt), dim3(kUnstuffThreads), 0, s, blob, offsets, descs, scratch, routes, cap);
+    hipLaunchKernelGGL(k_us_serial, dim3(route_grid(hint, kRtUsSmall, gs)), dim3(kUnstuffThreads), 0, s, blob, offsets, descs,
+                       scratch, routes, cap);
+  if (route_on(rm, kRtUsBig)) {  // (the three kernels stride over their work)
+    hipLaunchKernelGGL(k_us_count, dim3(route_grid(hint, kRtUsBig, gt)), dim3(kUnstuffThreads), 0, s, blob, offsets, descs,
+                       scratch, routes, cap);
+    hipLaunchKernelGGL(k_us_scan, dim3(route_grid(hint, kRtUsBig, g)), dim3(kUnstuffThreads), 0, s, descs, scratch, routes,
+                       cap);
+    hipLaunchKernelGGL(k_us_write, dim3(route_grid(hint, kRtUsBig, gt)), dim3(kUnstuffThreads), 0, s, blob, offsets, descs,
+                       scratch, routes, cap);
   }
   return hipGetLastError();
 }

@@ -921,25 +921,30 @@ k_prog(ImgDesc* __restrict__ descs, ImgTables* __restrict__ tables, const uint8_
        const int64_t* __restrict__ offsets, const int32_t* __restrict__ lengths, uint8_t* __restrict__ scratch,
        const int32_t* __restrict__ routes, int cap) {
   __shared__ PLds lds;
-  if ((int)blockIdx.x >= routes[kRtProg]) return;
-  const int img = route_list(routes, cap, kRtProg)[blockIdx.x];
-  ImgDesc* d = &descs[img];
-  if (d->status != SDSJ_OK) return;
-  const int st = decode_progressive(d, &tables[img], blob + offsets[img], lengths[img],
-                                    reinterpret_cast<int16_t*>(scratch + d->off_coef),
-                                    reinterpret_cast<ProgTables*>(scratch + d->off_ptab), lds, threadIdx.x);
-  if (st != SDSJ_OK && threadIdx.x == 0) d->status = st;
+  const int cnt = routes[kRtProg];
+  const int32_t* lst = route_list(routes, cap, kRtProg);
+  for (int li = blockIdx.x; li < cnt; li += gridDim.x) {  // (one entry per workgroup at the full grid)
+    const int img = lst[li];
+    ImgDesc* d = &descs[img];
+    if (d->status == SDSJ_OK) {
+      const int st = decode_progressive(d, &tables[img], blob + offsets[img], lengths[img],
+                                        reinterpret_cast<int16_t*>(scratch + d->off_coef),
+                                        reinterpret_cast<ProgTables*>(scratch + d->off_ptab), lds, threadIdx.x);
+      if (st != SDSJ_OK && threadIdx.x == 0) d->status = st;
+    }
+    __syncthreads();  // LDS reuse by the next entry
+  }
 }
 
 hipError_t launch_prog(int n, ImgDesc* descs, ImgTables* tables, const uint8_t* blob, const int64_t* offsets,
                        const int32_t* lengths, uint8_t* scratch, const int32_t* routes, int cap, hipStream_t s,
-                       uint64_t rm) {
+                       uint64_t rm, uint64_t hint) {
   if (!route_on(rm, kRtProg)) return hipSuccess;
   // (the helpers stride over the route list: a batch without progressive images launches few empty
   // workgroups -- at one per image their grids cost 115 us per 16,384 baseline images)
-  const int gx = n < kProgHelperGrid ? n : kProgHelperGrid;
+  const int gx = (int)route_grid(hint, kRtProg, n < kProgHelperGrid ? n : kProgHelperGrid);
   hipLaunchKernelGGL(k_prog_zero, dim3(gx, 16), dim3(256), 0, s, descs, scratch, routes, cap);
-  hipLaunchKernelGGL(k_prog, dim3(n), dim3(kProgThreads), 0, s, descs, tables, blob,
+  hipLaunchKernelGGL(k_prog, dim3(route_grid(hint, kRtProg, n)), dim3(kProgThreads), 0, s, descs, tables, blob,
                      offsets, lengths, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog_dcs, dim3(gx, 8), dim3(256), 0, s, descs, scratch, routes, cap);
   hipLaunchKernelGGL(k_prog_smooth, dim3(gx, 8), dim3(256), 0, s, descs, tables, scratch, routes, cap);

@@ -319,13 +319,13 @@ __device__ __forceinline__ void resample_tile(LdsResample& L, const RsArgs& A, i
   }
 }
 
-// One image's share (output rows of strip blockIdx.y, column tiles from blockIdx.z) of the generic
+// One image's share (output rows of strip `strip`, column tiles tz0, tz0 + ntz, ...) of the generic
 // fused colour + resample (route gen_route(KT); status and zero outputs: k_finish).  One
 // instantiation per horizontal tap count keeps each kernel's registers to what that count needs.
 template <int KT>
-__device__ void resample_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
-                               const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
-                               void* __restrict__ out, const float* __restrict__ lut) {
+__device__ void resample_image(int img, int strip, int tz0, int ntz, const ImgDesc* __restrict__ descs,
+                               const sdsj_op& op, int strip_h, const uint8_t* __restrict__ scratch,
+                               const uint8_t* __restrict__ flip, void* __restrict__ out, const float* __restrict__ lut) {
   const ImgDesc* d = &descs[img];
   RsArgs A;
   A.ow = op.out_w;
@@ -337,7 +337,7 @@ __device__ void resample_image(int img, const ImgDesc* __restrict__ descs, const
   A.om.cs = op.layout == SDSJ_LAYOUT_HWC ? 1 : plane;
   A.lut = lut;
   A.out = out;
-  A.oy0 = blockIdx.y * strip_h;
+  A.oy0 = strip * strip_h;
   if (A.oy0 >= A.oh) return;
   A.oy1 = A.oy0 + strip_h < A.oh ? A.oy0 + strip_h : A.oh;
   if (d->status != SDSJ_OK) return;  // failed after planning: k_finish writes the zeros
@@ -368,7 +368,7 @@ __device__ void resample_image(int img, const ImgDesc* __restrict__ descs, const
     if (A.ncomp == 1 || (c1.rh == 1 && c1.rv == 1 && c2.rh == 1 && c2.rv == 1)) A.layout = kLayFull;
     else if (c1.rh == 2 && c1.rv == 2 && c2.rh == 2 && c2.rv == 2 && c1.dw > 2 && c2.dw == c1.dw) A.layout = kLay420;
   }
-  for (int tile = blockIdx.z; tile < A.ntiles; tile += gridDim.z) {
+  for (int tile = tz0; tile < A.ntiles; tile += ntz) {
     resample_tile<KT>(L, A, tile);
     __syncthreads();  // LDS reuse by the next tile
   }
@@ -376,36 +376,42 @@ __device__ void resample_image(int img, const ImgDesc* __restrict__ descs, const
 
 template <int KT>
 __global__ void __launch_bounds__(kRsThreads) k_resample(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
-                                                         int strip_h, const uint8_t* __restrict__ scratch,
+                                                         int strip_h, int strips, int ntz,
+                                                         const uint8_t* __restrict__ scratch,
                                                          const uint8_t* __restrict__ flip, void* __restrict__ out,
                                                          const int32_t* __restrict__ routes, int cap,
                                                          const float* __restrict__ lut) {
   constexpr int r = KT == 0 ? kRtGen0 : (KT == 1 ? kRtGen1 : kRtGen3 + (KT - 3) / 2);
   const int cnt = routes[r];
   const int32_t* lst = route_list(routes, cap, r);
-  for (int e = blockIdx.x; e < cnt; e += gridDim.x)  // a small grid strides over the route's list
-    resample_image<KT>(lst[e], descs, op, strip_h, scratch, flip, out, lut);
+  // work items (route entry, strip, tile column) over the grid, as k_rs420
+  const int per = strips * ntz;
+  const int64_t items = (int64_t)cnt * per;
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const int e = (int)(it / per), rem = (int)(it - (int64_t)e * per), strip = rem / ntz;
+    resample_image<KT>(lst[e], strip, rem - strip * ntz, ntz, descs, op, strip_h, scratch, flip, out, lut);
+  }
 }
 
 hipError_t launch_resample(int n, const ImgDesc* descs, const sdsj_op& op, const uint8_t* scratch, const uint8_t* flip,
                            void* out, int32_t* status, const int32_t* routes, int cap, const float* lut, hipStream_t s,
-                           uint64_t rm) {
+                           uint64_t rm, uint64_t hint) {
   // strips of output rows: tall for big batches (less window overlap), short for small ones
   const int strip_h = n >= 512 ? kMaxStrip : 16;
   const int tiles = (op.out_w + kRsThreads - 1) / kRsThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
-  const dim3 grid(n < kRsfEntries ? n : kRsfEntries, strips, tiles);
-  if (route_on(rm, kRtGen0)) hipLaunchKernelGGL(k_resample<0>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  if (route_on(rm, kRtGen1)) hipLaunchKernelGGL(k_resample<1>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  if (route_on(rm, kRtGen3)) hipLaunchKernelGGL(k_resample<3>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  if (route_on(rm, kRtGen5)) hipLaunchKernelGGL(k_resample<5>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  if (route_on(rm, kRtGen7)) hipLaunchKernelGGL(k_resample<7>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  if (route_on(rm, kRtGen9)) hipLaunchKernelGGL(k_resample<9>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
-  if (route_on(rm, kRtGen11)) hipLaunchKernelGGL(k_resample<11>, grid, dim3(kRsThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+  const int64_t full = (int64_t)(n < kRsfEntries ? n : kRsfEntries) * strips * tiles;
+  if (route_on(rm, kRtGen0)) hipLaunchKernelGGL(k_resample<0>, dim3(route_grid(hint, kRtGen0, full)), dim3(kRsThreads), 0, s, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen1)) hipLaunchKernelGGL(k_resample<1>, dim3(route_grid(hint, kRtGen1, full)), dim3(kRsThreads), 0, s, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen3)) hipLaunchKernelGGL(k_resample<3>, dim3(route_grid(hint, kRtGen3, full)), dim3(kRsThreads), 0, s, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen5)) hipLaunchKernelGGL(k_resample<5>, dim3(route_grid(hint, kRtGen5, full)), dim3(kRsThreads), 0, s, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen7)) hipLaunchKernelGGL(k_resample<7>, dim3(route_grid(hint, kRtGen7, full)), dim3(kRsThreads), 0, s, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen9)) hipLaunchKernelGGL(k_resample<9>, dim3(route_grid(hint, kRtGen9, full)), dim3(kRsThreads), 0, s, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut);
+  if (route_on(rm, kRtGen11)) hipLaunchKernelGGL(k_resample<11>, dim3(route_grid(hint, kRtGen11, full)), dim3(kRsThreads), 0, s, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   (void)status;  // published by k_finish after every resample variant
-  return launch_resample420(n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
+  return launch_resample420(n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm, hint);
 }
 
 }  // namespace sdsj

@@ -112,8 +112,8 @@ __device__ __forceinline__ void vtaps8_at(int p, const uint32_t* ring, int lane_
 }
 
 template <int KT, int LAY>
-__device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
-                          const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
+__device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* __restrict__ descs, const sdsj_op& op,
+                          int strip_h, const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
                           void* __restrict__ out, const float* __restrict__ lut);
 
 // Route (LAY, KT): a small grid strides over the route's list (an empty route costs one short launch).
@@ -127,26 +127,33 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
 #define SDSJ_RS_OCC __attribute__((amdgpu_waves_per_eu(KT <= 7 && LAY != kRs444 ? SDSJ_RS_WAVES : 4)))
 template <int KT, int LAY>
 __global__ void __launch_bounds__(kFThreads) SDSJ_RS_OCC k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
-                                                      int strip_h, const uint8_t* __restrict__ scratch,
+                                                      int strip_h, int strips, int ntz, const uint8_t* __restrict__ scratch,
                                                       const uint8_t* __restrict__ flip, void* __restrict__ out,
                                                       const int32_t* __restrict__ routes, int cap,
                                                       const float* __restrict__ lut) {
   const int r = rs_route(LAY, KT);
   const int cnt = routes[r];
   const int32_t* lst = route_list(routes, cap, r);
-  for (int e = blockIdx.x; e < cnt; e += gridDim.x) rsf_image<KT, LAY>(lst[e], descs, op, strip_h, scratch, flip, out, lut);
+  // work items (route entry, strip, tile column), an image's strips consecutive; the grid (one item per
+  // workgroup up to kRsfEntries entries, a cold route's small grid: route_grid) strides over them
+  const int per = strips * ntz;
+  const int64_t items = (int64_t)cnt * per;
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const int e = (int)(it / per), rem = (int)(it - (int64_t)e * per), strip = rem / ntz;
+    rsf_image<KT, LAY>(lst[e], strip, rem - strip * ntz, ntz, descs, op, strip_h, scratch, flip, out, lut);
+  }
 }
 
-// One image's share (strip blockIdx.y, column tiles from blockIdx.z) of the fused resample.
+// One image's share (output strip `strip`, column tiles tz0, tz0 + ntz, ...) of the fused resample.
 template <int KT, int LAY>
-__device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj_op& op, int strip_h,
-                          const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
+__device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* __restrict__ descs, const sdsj_op& op,
+                          int strip_h, const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
                           void* __restrict__ out, const float* __restrict__ lut) {
   using G = FGeo<LAY>;
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->rs_fast != KT || d->rs_lay != LAY) return;
   const int oh = op.out_h, ow = op.out_w;
-  const int oy0 = blockIdx.y * strip_h;
+  const int oy0 = strip * strip_h;
   if (oy0 >= oh) return;
   const int oy1 = oy0 + strip_h < oh ? oy0 + strip_h : oh;
   __shared__ LdsF<LAY, KT> L;
@@ -186,7 +193,7 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
     L.vw[b][k] = k < ksv ? kv[(int64_t)oy * ksv + k] : 0;
   }
 
-  for (int tile = blockIdx.z; tile < ntiles; tile += gridDim.z) {
+  for (int tile = tz0; tile < ntiles; tile += ntz) {
     const int ox0 = tile * tw, ox1 = ox0 + tw < ow ? ox0 + tw : ow;
     const int s_lo = bh[2 * ox0], s_hi = bh[2 * (ox1 - 1)] + bh[2 * (ox1 - 1) + 1];
     const int ax0 = cx0 + s_lo, ax1 = cx0 + s_hi;  // image columns of the tile
@@ -568,31 +575,32 @@ __device__ void rsf_image(int img, const ImgDesc* __restrict__ descs, const sdsj
 }
 
 template <int LAY>
-static void launch_lay(const dim3& grid, int n, const ImgDesc* descs, const sdsj_op& op, int strip_h,
+static void launch_lay(int64_t full, uint64_t hint, int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, int strips,
+                       int ntz,
                        const uint8_t* scratch, const uint8_t* flip, void* out, const int32_t* routes, int cap,
                        const float* lut, hipStream_t s, uint64_t rm) {
   if (route_on(rm, rs_route(LAY, 3)))
-    hipLaunchKernelGGL((k_rs420<3, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+    hipLaunchKernelGGL((k_rs420<3, LAY>), dim3(route_grid(hint, rs_route(LAY, 3), full)), dim3(kFThreads), 0, s, n, descs, op, strip_h, strips, ntz, scratch, flip, out, routes, cap, lut);
   if (route_on(rm, rs_route(LAY, 5)))
-    hipLaunchKernelGGL((k_rs420<5, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+    hipLaunchKernelGGL((k_rs420<5, LAY>), dim3(route_grid(hint, rs_route(LAY, 5), full)), dim3(kFThreads), 0, s, n, descs, op, strip_h, strips, ntz, scratch, flip, out, routes, cap, lut);
   if (route_on(rm, rs_route(LAY, 7)))
-    hipLaunchKernelGGL((k_rs420<7, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+    hipLaunchKernelGGL((k_rs420<7, LAY>), dim3(route_grid(hint, rs_route(LAY, 7), full)), dim3(kFThreads), 0, s, n, descs, op, strip_h, strips, ntz, scratch, flip, out, routes, cap, lut);
   if (route_on(rm, rs_route(LAY, 9)))
-    hipLaunchKernelGGL((k_rs420<9, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+    hipLaunchKernelGGL((k_rs420<9, LAY>), dim3(route_grid(hint, rs_route(LAY, 9), full)), dim3(kFThreads), 0, s, n, descs, op, strip_h, strips, ntz, scratch, flip, out, routes, cap, lut);
   if (route_on(rm, rs_route(LAY, 11)))
-    hipLaunchKernelGGL((k_rs420<11, LAY>), grid, dim3(kFThreads), 0, s, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut);
+    hipLaunchKernelGGL((k_rs420<11, LAY>), dim3(route_grid(hint, rs_route(LAY, 11), full)), dim3(kFThreads), 0, s, n, descs, op, strip_h, strips, ntz, scratch, flip, out, routes, cap, lut);
 }
 
 hipError_t launch_resample420(int n, const ImgDesc* descs, const sdsj_op& op, int strip_h, const uint8_t* scratch,
                               const uint8_t* flip, void* out, const int32_t* routes, int cap, const float* lut,
-                              hipStream_t s, uint64_t rm) {
+                              hipStream_t s, uint64_t rm, uint64_t hint) {
   const int tiles = (op.out_w + kFThreads - 1) / kFThreads;
   const int strips = (op.out_h + strip_h - 1) / strip_h;
-  const dim3 grid(n < kRsfEntries ? n : kRsfEntries, strips, tiles);
-  launch_lay<kRs420>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
-  launch_lay<kRs422>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
-  launch_lay<kRs444>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
-  launch_lay<kRsGray>(grid, n, descs, op, strip_h, scratch, flip, out, routes, cap, lut, s, rm);
+  const int64_t full = (int64_t)(n < kRsfEntries ? n : kRsfEntries) * strips * tiles;
+  launch_lay<kRs420>(full, hint, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut, s, rm);
+  launch_lay<kRs422>(full, hint, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut, s, rm);
+  launch_lay<kRs444>(full, hint, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut, s, rm);
+  launch_lay<kRsGray>(full, hint, n, descs, op, strip_h, strips, tiles, scratch, flip, out, routes, cap, lut, s, rm);
   return hipGetLastError();
 }
 
