@@ -448,6 +448,9 @@ struct BlkCtx {
   uint32_t pc;
   int bpm;
   uint64_t p6;  // images of <= 4 table slots (LB = 11): per MCU block 6 bits, DC slot | AC slot << 2 | comp << 4
+  uint64_t p5;  // (the write pass, LB = 11) per MCU block 5 bits: DC slot | AC slot << 2 | the next block's
+                // component differs << 4 (an MCU's blocks come component by component, so the predictors
+                // can rotate through the components in MCU order instead of being selected by index)
 };
 
 __device__ __forceinline__ int ctx_dc(const BlkCtx& k, int blk) { return (int)(k.pdc >> (4 * blk)) & 15; }
@@ -462,9 +465,21 @@ __device__ __forceinline__ BlkCtx make_ctx(const TT& T, int bpm) {
   k.pc = T.pk_c;
   k.bpm = bpm;
   k.p6 = 0;
-  for (int b = 0; b < bpm; b++)
-    k.p6 |= (uint64_t)(((k.pdc >> (4 * b)) & 3) | (((k.pac >> (4 * b)) & 3) << 2) | (((k.pc >> (2 * b)) & 3) << 4)) << (6 * b);
+  k.p5 = 0;
+  for (int b = 0; b < bpm; b++) {
+    const uint64_t c = (k.pc >> (2 * b)) & 3, cn = (k.pc >> (2 * (b + 1 == bpm ? 0 : b + 1))) & 3;
+    k.p6 |= (uint64_t)(((k.pdc >> (4 * b)) & 3) | (((k.pac >> (4 * b)) & 3) << 2) | (c << 4)) << (6 * b);
+    k.p5 |= (uint64_t)(((k.pdc >> (4 * b)) & 3) | (((k.pac >> (4 * b)) & 3) << 2) | ((uint64_t)(c != cn) << 4)) << (5 * b);
+  }
   return k;
+}
+
+// The write pass's context of MCU block blk (LB = 11): table slots and whether the component changes after it.
+__device__ __forceinline__ void ctx_w5(const BlkCtx& k, int blk, int& sdc, int& sac, bool& chg) {
+  const uint32_t x = (uint32_t)(k.p5 >> __umul24((unsigned)blk, 5u));
+  sdc = (int)(x & 3);
+  sac = (int)((x >> 2) & 3);
+  chg = (x >> 4) & 1;
 }
 
 // All three of an MCU block's context values from the 6-bit packing (<= 4 table slots): one 64-bit
@@ -1214,6 +1229,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   int16_t* coef = reinterpret_cast<int16_t*>(scratch + d->off_coef);
   const int nsub = d->nsub;
   const int blocks_per_seg = d->restart_interval ? d->restart_interval * K.bpm : (int)d->total_blocks;
+  const int ncomp = d->ncomp;
   const int my_base = t * kStageStride;
   int bad = 0;
   unsigned long long nsym = 0, witers = 0;
@@ -1224,6 +1240,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     const bool active = j < j1;
     Bits b;
     int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, pc = 0, sdc = 0, sac = 0;
+    bool chg = false;
     int g = 0, gend = 0;  // decode-order block indices (total_blocks < 2^24, setup_geometry)
     uint32_t end_bit = 0, lim = 0;
     int s_int = 0;
@@ -1242,14 +1259,28 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       // entries are block boundaries (z = 0): the speculative and the sync passes stop only there
       blk = S.entry_bz >> 8;
       z = 0;
+      c = ctx_c(K, blk);
       if constexpr (LB == 11) {
-        ctx_all6(K, blk, c, sdc, sac);
+        // predictors in component order from the entry block's component: pc = its own, p0 / p1 the
+        // next ones (cyclically); a block after which the component changes rotates them (ctx_w5)
+        // (the scan's component order, which the MCU follows, need not be the components' index order)
+        ctx_w5(K, blk, sdc, sac, chg);
+        int succ[kMaxComp] = {0, 0, 0};
+        for (int b = 0; b < K.bpm; b++) {
+          const int cb = ctx_c(K, b), cn = ctx_c(K, b + 1 == K.bpm ? 0 : b + 1);
+          if (cn != cb) succ[cb] = cn;
+        }
+        auto pred = [&](int k) { return k == 0 ? p0 : (k == 1 ? p1 : p2); };
+        const int c1 = succ[c], c2 = succ[c1];
+        const int pa = pred(c), pb = pred(c1), pd = pred(c2);
+        pc = pa;
+        p0 = pb;
+        p1 = pd;
       } else {
-        c = ctx_c(K, blk);
         sdc = ctx_dc(K, blk);
         sac = ctx_ac(K, blk);
+        pc = c == 0 ? p0 : (c == 1 ? p1 : p2);  // the current block's component predictor
       }
-      pc = c == 0 ? p0 : (c == 1 ? p1 : p2);  // the current block's component predictor
       end_bit = S.end_bit;
       s_int = s;
       lim = S.lim_bit;
@@ -1288,18 +1319,25 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           const bool done = next_z(z, s, r);
           ready = done;
           gdone = (uint32_t)g;
-          p0 = (done & (c == 0)) ? pc : p0;
-          p1 = (done & (c == 1)) ? pc : p1;
-          p2 = (done & (c == 2)) ? pc : p2;
-          blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
           if constexpr (LB == 11) {
-            ctx_all6(K, blk, c, sdc, sac);
+            // (pc, p0, p1) -> (p0, p1, pc) with 3 components in the scan, (pc, p0) -> (p0, pc) with 2
+            const bool rot = done & chg;
+            const int t0 = pc;
+            pc = rot ? p0 : pc;
+            p0 = rot ? (ncomp == 3 ? p1 : t0) : p0;
+            p1 = rot ? (ncomp == 3 ? t0 : p1) : p1;
+            blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
+            ctx_w5(K, blk, sdc, sac, chg);
           } else {
+            p0 = (done & (c == 0)) ? pc : p0;
+            p1 = (done & (c == 1)) ? pc : p1;
+            p2 = (done & (c == 2)) ? pc : p2;
+            blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
             c = ctx_c(K, blk);
             sdc = ctx_dc(K, blk);
             sac = ctx_ac(K, blk);
+            pc = done ? (c == 0 ? p0 : (c == 1 ? p1 : p2)) : pc;
           }
-          pc = done ? (c == 0 ? p0 : (c == 1 ? p1 : p2)) : pc;
           g += done ? 1 : 0;
           run = (g < gend) & !((z == 0) & ((stop_blk >> blk) & 1u) & (b.pos >= stop_pos));
         }

@@ -85,13 +85,14 @@ def _category(v: int) -> int:
     return int(abs(v)).bit_length()
 
 
-def write_jpeg(w: int, h: int, comps, blocks, qtables, huff=None) -> bytes:
+def write_jpeg(w: int, h: int, comps, blocks, qtables, huff=None, order=None) -> bytes:
     """comps: [(h_samp, v_samp, tq)], 1 or 3 components; blocks: per component an int array
     [bh, bw, 64] of quantised coefficients in ZIGZAG order (DC as absolute values: the DPCM is done
     here); qtables: {tq: 64 values (zigzag order)}, a table with a value > 255 is written with 16-bit
     precision.  huff: per component its (DC, AC) table ids, default 0 for the first component and 1
     for the others; id 2 is a copy of the luma tables (Annex K ids 0) under its own id, so
-    huff=[(0, 0), (1, 1), (2, 2)] makes a scan of 6 distinct table slots."""
+    huff=[(0, 0), (1, 1), (2, 2)] makes a scan of 6 distinct table slots.  order: the components' order
+    in the scan header (and so in each MCU), default the frame's."""
     tabs = dict(_annex_k_tables())
     tabs[(0, 2)], tabs[(1, 2)] = tabs[(0, 0)], tabs[(1, 0)]
     if huff is None:
@@ -121,15 +122,18 @@ def write_jpeg(w: int, h: int, comps, blocks, qtables, huff=None) -> bytes:
     for (tc, th), (bits, vals) in sorted(tabs.items()):
         if (tc, th) in used:
             marker(0xC4, bytes([(tc << 4) | th] + bits + vals))
+    if order is None:
+        order = list(range(len(comps)))
     sos = bytes([len(comps)])
-    for ci in range(len(comps)):
+    for ci in order:
         sos += bytes([ci + 1, (huff[ci][0] << 4) | huff[ci][1]])
     marker(0xDA, sos + bytes([0, 63, 0]))
     bw = _BitWriter()
     pred = [0] * len(comps)
     for my in range(mcuy):
         for mx in range(mcux):
-            for ci, (hs, vs, _) in enumerate(comps):
+            for ci in order:
+                hs, vs, _ = comps[ci]
                 td, ta = huff[ci]
                 hh, vv = (hs, vs) if len(comps) > 1 else (1, 1)
                 for dy in range(vv):
@@ -221,7 +225,7 @@ def extreme_jpegs(seed: int, n: int) -> list[bytes]:
     return out
 
 
-def six_slot_jpegs(seed: int, n: int, w: int = 160, h: int = 120) -> list[bytes]:
+def six_slot_jpegs(seed: int, n: int, w: int = 160, h: int = 120, order=None) -> list[bytes]:
     """Baseline 4:2:0 / 4:4:4 JPEGs whose Cb and Cr components use their own DC/AC Huffman tables
     (ids 1 and 2: 6 distinct table slots, the kernels' 10-bit entropy route), with natural-looking
     coefficients: a DC random walk and a few small low-frequency AC terms per block."""
@@ -250,5 +254,5 @@ def six_slot_jpegs(seed: int, n: int, w: int = 160, h: int = 120) -> list[bytes]
                             dcv = int(np.clip(dcv + rng.integers(-60, 61), -1000, 1000))
                             blocks[ci][my * vs + dy, mx * hs + dx, 0] = dcv
         q = {0: rng.integers(2, 40, 64), 1: rng.integers(2, 60, 64)}
-        out.append(write_jpeg(w, h, comps, blocks, q, huff=[(0, 0), (1, 1), (2, 2)]))
+        out.append(write_jpeg(w, h, comps, blocks, q, huff=[(0, 0), (1, 1), (2, 2)], order=order))
     return out

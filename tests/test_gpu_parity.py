@@ -264,6 +264,17 @@ def test_six_table_slot_images_vs_oracle(engine, n):
     np.testing.assert_array_equal(full[0].cpu().numpy(), O.decode(six[0]))
 
 
+def test_scan_components_out_of_frame_order_are_unsupported(engine):
+    """Scan component order differing from the frame's: UNSUPPORTED on the GPU, as in the oracle (PIL rejects it
+    too: test_scan_components_out_of_frame_order_are_rejected_like_pil); the write pass's predictor rotation
+    follows the MCU's component cycle, which is then always the frame order."""
+    from sds_amd import _lib
+    from tests.golden.coefjpeg import six_slot_jpegs
+    jpgs = [j for order in ([2, 1, 0], [1, 2, 0]) for j in six_slot_jpegs(5, 2, 96, 64, order=order)]
+    _, st = engine.decode_resize(jpgs, (32, 32))
+    assert all(int(v) == _lib.UNSUPPORTED for v in st), st
+
+
 def test_fill_stuffed_streams_rerun_on_pil_through_the_transform(engine):
     """FF FF .. 00 inside a baseline scan: the GPU reports CORRUPT, the per-sample transform reruns the
     sample on PIL, so the output equals the reference's PIL decode + resize."""

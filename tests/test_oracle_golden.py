@@ -332,6 +332,23 @@ def test_oracle_matches_pil_on_six_table_slot_jpegs():
         np.testing.assert_array_equal(O.decode(j), ref, err_msg=f"image {k}")
 
 
+def test_scan_components_out_of_frame_order_are_rejected_like_pil():
+    """A baseline scan listing its components in another order than the frame (its MCUs then follow the
+    scan's order) is rejected by PIL (libjpeg-turbo) and by the oracle alike."""
+    import io
+
+    import pytest
+    from PIL import Image
+
+    from tests.golden.coefjpeg import six_slot_jpegs
+    for order in ([2, 1, 0], [1, 2, 0], [0, 2, 1]):
+        for j in six_slot_jpegs(5, 2, 96, 64, order=order):
+            with pytest.raises(OSError):
+                Image.open(io.BytesIO(j)).convert("RGB")
+            with pytest.raises(O.OracleError, match="status -2"):  # UNSUPPORTED
+                O.decode(j)
+
+
 def test_fill_stuffing_predicate():
     from tests.golden.synth import encode_jpeg, has_fill_stuffing, synth_rgb
     j = encode_jpeg(synth_rgb(np.random.default_rng(3), 64, 48), 90)
