@@ -85,6 +85,31 @@ def run_service_case(case: str) -> dict:
                         key = "f32_512_sha256" if norm else "u8_512_sha256"
                         ok &= s["image"].device.type == "cpu" and G.sha(s["image"].contiguous().numpy()) == im[key]
             rec["equal_to_goldens"] = bool(ok)
+        elif case == "service_random_resize":
+            # random_resize (np global RNG, one draw per sample): requests of different target sizes in
+            # flight together; every output equals the oracle at the size the sample drew
+            from oracle import oracle as O  # checker only
+            _, jpgs = G.g2_jpegs()
+            paths = []
+            for i in range(24):
+                p = os.path.join(d, f"{i}.jpg")
+                with open(p, "wb") as f:
+                    f.write(jpgs[i % len(jpgs)])
+                paths.append(p)
+            rr = {(256, 256): 0.5, (192, 160): 0.25, (96, 128): 0.25}
+            ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", resize_kwargs={"random_resize": rr})
+            ok, shapes = True, set()
+            dl = DataLoader(FolderDataset(paths, ts), batch_size=4, num_workers=4, pin_memory=True,
+                            collate_fn=lambda b: b)
+            for b in dl:
+                for s in b:
+                    im = s["image"]
+                    ok &= im.device.type == "cpu"
+                    shapes.add(tuple(im.shape))
+                    ref = O.pipeline(jpgs[s["index"] % len(jpgs)], tuple(im.shape[1:]))
+                    ok &= bool(np.array_equal(im.contiguous().numpy(), ref))
+            rec["shapes"] = sorted(shapes)
+            rec["equal_to_oracle"] = bool(ok)
         elif case == "service_fallback_g6":
             meta = G.load_json("g6_fallback.json")
             z = np.load(os.path.join(G.GOLDEN, "g6_fallback.npz"))

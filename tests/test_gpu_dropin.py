@@ -281,6 +281,14 @@ def test_decode_service_g3_mixed_sizes_flip_normalize():
     assert "error" not in rec and rec["equal_to_goldens"], rec
 
 
+def test_decode_service_random_resize_matches_the_oracle():
+    """random_resize through the service (fork, 4 workers, pin_memory=True): samples draw three target
+    sizes, so requests of different ops are in flight together; each output equals the oracle at its size."""
+    rec = _case("service_random_resize")
+    assert "error" not in rec, rec
+    assert len(rec["shapes"]) >= 2 and rec["equal_to_oracle"], rec
+
+
 def test_decode_service_fallback_formats_match_g6():
     """PNG / WebP / GIF / BMP / TIFF / CMYK / no-EOI samples in service workers: PIL decodes them in the
     worker, the service resizes the frame (SDSJ_SVC_FRAME); outputs and OSErrors equal G6."""

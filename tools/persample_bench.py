@@ -29,6 +29,10 @@ MODES = {
     "service_fork_workers4_pinned": (4, True, None, None, "auto"),
     "service_fork_workers8_pinned": (8, True, None, None, "auto"),
     "service_fork_workers16_pinned": (16, True, None, None, "auto"),
+    # random_resize (RR below: three target sizes, np global RNG per sample) through the service: requests
+    # of different sizes form separate engine batches; the loader collates each batch as a list
+    "servicerr_fork_workers8_pinned": (8, True, None, None, "auto"),
+    "servicerr_fork_workers16_pinned": (16, True, None, None, "auto"),
     # per-worker engines (service=None)
     "dataloader_fork_workers2_device_out": (2, False, None, None, None),
     "dataloader_fork_workers8_device_out": (8, False, None, None, None),
@@ -49,6 +53,7 @@ MODES = {
     "pil_fork_workers16_pinned": (16, True, None, None, "pil"),
 }
 BATCH = int(os.environ.get("PERSAMPLE_BATCH", "4"))
+RR = {(256, 256): 0.5, (224, 224): 0.25, (192, 192): 0.25}
 
 
 def _null_transform(s):
@@ -100,14 +105,16 @@ def run_mode(mode, n_files, seconds):
         ts = [_pil_transform]
     else:
         ts = create_standard_image_pipeline("jpg", (256, 256), device="cuda", output_device=None if discard else odev,
-                                            service=service)
+                                            service=service,
+                                            resize_kwargs={"random_resize": RR} if mode.startswith("servicerr") else {})
     ds = FolderDataset(paths, ts)
     if discard:
         ds = _Discard(ds)
     if nw:
         # persistent workers: forked once, before the parent receives its first device tensor
+        collate = (lambda b: {"image": [s["image"] for s in b]}) if mode.startswith("servicerr") else None
         src = DataLoader(ds, batch_size=BATCH, num_workers=nw, pin_memory=pin, multiprocessing_context=ctx,
-                         persistent_workers=True, prefetch_factor=4)
+                         persistent_workers=True, prefetch_factor=4, collate_fn=collate)
     else:
         src = ds
     n, t0, first = 0, time.perf_counter(), None
@@ -115,10 +122,10 @@ def run_mode(mode, n_files, seconds):
         for b in src:
             x = b["image"]
             if first is None:
-                first = (str(x.device), list(x.shape))
+                first = [(str(y.device), list(y.shape)) for y in x] if isinstance(x, list) else (str(x.device), list(x.shape))
                 n, t0 = 0, time.perf_counter()  # worker start-up and HIP initialisation excluded
                 continue
-            n += x.shape[0] if x.dim() == 4 else 1
+            n += len(x) if isinstance(x, list) else (x.shape[0] if x.dim() == 4 else 1)
             if time.perf_counter() - t0 >= seconds:
                 break
     if torch.cuda.is_initialized():
