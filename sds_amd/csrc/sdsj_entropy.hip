@@ -350,7 +350,8 @@ constexpr int kQ = SDSJ_Q;
 #endif
 constexpr int kSpecGroup = SDSJ_SPEC_GROUP;    // symbols decoded between two wave-uniform refill checks (spec pass)
 constexpr int kWriteGroup = SDSJ_WRITE_GROUP;  // (write pass)
-static_assert(kSpecGroup < kQ && kWriteGroup < kQ, "a fresh refill must pass the group check");
+constexpr int kQW = kQ;                        // the write pass's queue (words)
+static_assert(kSpecGroup < kQ && kWriteGroup < kQW, "a fresh refill must pass the group check");
 // A symbol takes at most 27 bits (16-bit code + 11 extra bits; a bad code 17): a group of G symbols
 // has a word to pull before each of them when nb + 32 nq >= 27 (G - 1) + 32 at its start.
 constexpr int kRefillSpec = 27 * (kSpecGroup - 1) + 32;
@@ -534,6 +535,17 @@ struct WriteTables {
   uint32_t pad[3];
 };
 
+// A decode-table entry in the write pass's format: len | size << 4 | advance << 8, the advance being
+// what the symbol adds to the block's zigzag position k (decode_mcu's k loop): 1 for a DC symbol, r + 1
+// for an AC value or ZRL (r = 15), 64 for EOB -- so the block end is one compare (write_adv).
+__device__ __forceinline__ uint32_t write_adv(bool ac, uint32_t s, uint32_t r) {
+  return !ac ? 1u : ((s == 0 && r != 15) ? 64u : r + 1u);
+}
+__device__ __forceinline__ uint32_t write_entry(uint32_t e, bool ac) {
+  const uint32_t l = e & 15, sz = (e >> 4) & 15, r = (e >> 8) & 15;
+  return l == 0 ? 0u : (l | (sz << 4) | (write_adv(ac, sz, r) << 8));
+}
+
 template <int LB, class TT>
 __device__ __forceinline__ uint32_t lookup(const TT& T, int slot, uint32_t hi) {
   if constexpr (TT::kTwoLevel) {
@@ -564,6 +576,31 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   if (l == 0) long_code<TT::kTwoLevel ? kW1 : LB>(T, slot, isdc, hi, l, s, r, bad);
   // HUFF_EXTEND without branches: the s extra bits follow the l code bits inside hi (l + s <= 27; a
   // bad code has s = 0), x < 2^(s-1) -> x - (2^s - 1); s = 0 -> x = 0, mask 0 -> 0
+  const int tot = l + s;
+  const uint32_t msk = (1u << s) - 1u;
+  const uint32_t x = (hi >> ((32 - tot) & 31)) & msk;
+  val = (x >> ((s - 1) & 31)) ? (int)x : (int)x - (int)msk;
+  b.buf <<= tot;
+  b.nb -= tot;
+  b.pos += tot;
+}
+
+// decode_sym for the write pass's tables (write_entry format): the symbol's size and its advance of the
+// zigzag position instead of (size, run).  A bad code (JWRN_HUFF_BAD_CODE) sets `bad`.
+template <int Q>
+__device__ __forceinline__ void decode_wsym(const WriteTables& T, BitsQ<Q>& b, int slot, bool isdc, int& s, int& adv,
+                                            int& val, int& bad) {
+  bits_pull(b);
+  const uint32_t hi = (uint32_t)(b.buf >> 32);
+  const uint32_t e = lookup<11>(T, slot, hi);
+  int l = e & 15;
+  s = (e >> 4) & 15;
+  adv = (e >> 8) & 127;
+  if (l == 0) {
+    int r;
+    long_code<kW1>(T, slot, isdc, hi, l, s, r, bad);
+    adv = (int)write_adv(!isdc, (uint32_t)s, (uint32_t)r);
+  }
   const int tot = l + s;
   const uint32_t msk = (1u << s) - 1u;
   const uint32_t x = (hi >> ((32 - tot) & 31)) & msk;
@@ -1168,11 +1205,12 @@ __device__ int load_write_tables(WriteTables& W, const EntTables* g, int32_t* tm
 #pragma unroll
   for (int j = 0; j < kPer; j++) {
     const int i = t * kPer + j, q = i >> kW1, k = i & ((1 << kW1) - 1);
-    uint32_t e = q < ns ? g->lut[(q << 11) + (k << 2)] : 0u;
+    const bool ac = q < ns && (g->slot_src[q] & 4);
+    uint32_t e = q < ns ? write_entry(g->lut[(q << 11) + (k << 2)], ac) : 0u;
     if ((longmask >> j) & 1) {
       const int sub = base++;
       if (sub < kW2Cap / 4) {
-        for (int m = 0; m < 4; m++) W.l2[sub * 4 + m] = g->lut[(q << 11) + (k << 2) + m];
+        for (int m = 0; m < 4; m++) W.l2[sub * 4 + m] = (uint16_t)write_entry(g->lut[(q << 11) + (k << 2) + m], ac);
         e = (uint32_t)(sub + 1) << 4;
       } else {
         e = 0;  // no second level left: the canonical search
@@ -1238,7 +1276,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
   for (int jb = j0; jb < j1; jb += kEntThreads) {  // uniform trip count for the whole workgroup
     const int j = jb + t;
     const bool active = j < j1;
-    Bits b;
+    BitsQ<kQW> b;
     int blk = 0, z = 0, c = 0, p0 = 0, p1 = 0, p2 = 0, pc = 0, sdc = 0, sac = 0;
     bool chg = false;
     int g = 0, gend = 0;  // decode-order block indices (total_blocks < 2^24, setup_geometry)
@@ -1303,20 +1341,34 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
         bool ready = false;
         uint32_t gdone = 0;
         if (run) {
-          int s, r, val, sb = 0;
           const bool isdc = z == 0;
-          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
-          if (kStats) nsym++;
-          bad |= sb;
-          // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r]
-          pc += isdc ? val : 0;
-          // zigzag position k + r (jpeg_natural_order's guard entries send positions past 63 to 63).  EOB
-          // and ZRL symbols (s = 0, val = 0) store a zero at a position of the block not written yet
-          // (positions only grow within a block, and a clamped store ends it), so every symbol stores
-          const int zp = z + r, wpos = zp < 63 ? zp : 63;
-          L.stage[my_base + wpos] = (int16_t)(isdc ? pc : val);
-          // block end by selects (no branches): the component's predictor back, the next block's out
-          const bool done = next_z(z, s, r);
+          int val;
+          bool done;
+          if constexpr (LB == 11) {
+            int s, adv;
+            decode_wsym(T, b, isdc ? sdc : sac, isdc, s, adv, val, bad);
+            if (kStats) nsym++;
+            // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r], k + r =
+            // k + advance - 1 (jpeg_natural_order's guard entries send positions past 63 to 63).  EOB
+            // (advance 64: position 63) and ZRL symbols (s = 0, val = 0) store a zero at a position of the
+            // block not written yet (positions only grow within a block, and a clamped store ends it), so
+            // every symbol stores
+            pc += isdc ? val : 0;
+            const int zn = z + adv, wpos = zn < 64 ? zn - 1 : 63;
+            L.stage[my_base + wpos] = (int16_t)(isdc ? pc : val);
+            // block end by selects (no branches): the component's predictor back, the next block's out
+            done = zn > 63;
+            z = done ? 0 : zn;
+          } else {
+            int s, r, sb = 0;
+            decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, sb);
+            if (kStats) nsym++;
+            bad |= sb;
+            pc += isdc ? val : 0;
+            const int zp = z + r, wpos = zp < 63 ? zp : 63;
+            L.stage[my_base + wpos] = (int16_t)(isdc ? pc : val);
+            done = next_z(z, s, r);
+          }
           ready = done;
           gdone = (uint32_t)g;
           if constexpr (LB == 11) {
@@ -1339,7 +1391,8 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
             pc = done ? (c == 0 ? p0 : (c == 1 ? p1 : p2)) : pc;
           }
           g += done ? 1 : 0;
-          run = (g < gend) & !((z == 0) & ((stop_blk >> blk) & 1u) & (b.pos >= stop_pos));
+          // (after a symbol z = 0 exactly when it ended the block; stop_blk: every block, or MCU starts)
+          run = (g < gend) & !(done & ((stop_blk != 1u) | (blk == 0)) & (b.pos >= stop_pos));
         }
         // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
         const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
