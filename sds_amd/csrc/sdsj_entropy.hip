@@ -52,6 +52,13 @@ constexpr int max_tasks() { return 4 * NT; }  // sync tasks per round (more: pic
 constexpr int kSyncThreads = 64;
 constexpr int kMaxSlots = 2 * kMaxComp;  // a DC and an AC table per component at most
 
+// What a symbol adds to its block's zigzag position k (decode_mcu's k loop): 1 for a DC symbol, r + 1
+// for an AC value or ZRL (r = 15), 64 for EOB -- a block ends when k passes 63.  The speculative and the
+// write passes' tables carry it per entry, so a block end is one compare.
+__device__ __forceinline__ uint32_t write_adv(bool ac, uint32_t s, uint32_t r) {
+  return !ac ? 1u : ((s == 0 && r != 15) ? 64u : r + 1u);
+}
+
 // ------------------------------------------------------------------------------------------
 // Per-image decode tables in LDS.
 // ------------------------------------------------------------------------------------------
@@ -75,6 +82,7 @@ static_assert(sizeof(TabCommon) % 16 == 0, "tables are copied in 16-byte units")
 //              when it ends with an EOB: the group applies at block position z iff z + this <= 64,
 //              so a block can only end at a group's last symbol
 //   bit  24    the group ends with an EOB
+//   bits 25-31 the single symbol's advance of the block position (write_adv)
 // Groups skip the values, so only passes that need no AC values (warm-up, speculative) use them.
 constexpr int kMW = 10;
 constexpr int kMSlots = 4;  // LB = 11 images have at most 4 slots
@@ -231,6 +239,7 @@ __global__ void __launch_bounds__(kEntThreads) k_enttab(ImgDesc* __restrict__ de
       const int q = i >> kMW, k = i & ((1 << kMW) - 1);
       const uint32_t e1 = T.lut[(q << 11) + (k << 1)];
       uint32_t e = (e1 & 15) <= kMW ? e1 : 0u;
+      if (e & 15) e |= write_adv((T.slot_src[q] & 4) != 0, (e >> 4) & 15, (e >> 8) & 15) << 25;
       if (T.slot_src[q] & 4) {
         int used = 0, dz = 0, n = 0, eob = 0;
         while (used < kMW) {
@@ -535,12 +544,7 @@ struct WriteTables {
   uint32_t pad[3];
 };
 
-// A decode-table entry in the write pass's format: len | size << 4 | advance << 8, the advance being
-// what the symbol adds to the block's zigzag position k (decode_mcu's k loop): 1 for a DC symbol, r + 1
-// for an AC value or ZRL (r = 15), 64 for EOB -- so the block end is one compare (write_adv).
-__device__ __forceinline__ uint32_t write_adv(bool ac, uint32_t s, uint32_t r) {
-  return !ac ? 1u : ((s == 0 && r != 15) ? 64u : r + 1u);
-}
+// A decode-table entry in the write pass's format: len | size << 4 | advance << 8 (write_adv).
 __device__ __forceinline__ uint32_t write_entry(uint32_t e, bool ac) {
   const uint32_t l = e & 15, sz = (e >> 4) & 15, r = (e >> 8) & 15;
   return l == 0 ? 0u : (l | (sz << 4) | (write_adv(ac, sz, r) << 8));
@@ -615,27 +619,40 @@ __device__ __forceinline__ void decode_wsym(const WriteTables& T, BitsQ<Q>& b, i
 // or an AC symbol near the block end.  Gives the (s, r) next_z takes for the step: a group of value /
 // ZRL symbols advances like one symbol of run dz - 1, a group ending in EOB like an EOB.  The group's
 // symbols are exactly the ones single decodes would give (k_enttab walks them with the same LUT).
+// adv: the step's advance of the block position (write_adv; a group ending in EOB: 64), so the
+// block ends when z + adv passes 63.
 template <bool kVal, class TT, int Q>
-__device__ __forceinline__ void decode_step(const TT& T, BitsQ<Q>& b, int slot, bool isdc, int z, int& s, int& r,
+__device__ __forceinline__ void decode_step(const TT& T, BitsQ<Q>& b, int slot, bool isdc, int z, int& adv,
                                             int& val, int& bad) {
   bits_pull(b);
   const uint32_t hi = (uint32_t)(b.buf >> 32);
   const uint32_t e = T.mlut[(slot << kMW) + (hi >> (32 - kMW))];
-  int l = e & 15, sz = (e >> 4) & 15, rr = (e >> 8) & 15;
+  int l = e & 15, sz = (e >> 4) & 15, a = (int)(e >> 25);
   const int mb = (e >> 12) & 31, mdz = (e >> 17) & 127, eob = (e >> 24) & 1;
   const bool multi = (mb != 0) & (z + mdz <= 64);
-  if (!multi && l == 0) long_code<kMW>(T, slot, isdc, hi, l, sz, rr, bad);
+  if (!multi && l == 0) {
+    int rr;
+    long_code<kMW>(T, slot, isdc, hi, l, sz, rr, bad);
+    a = (int)write_adv(!isdc, (uint32_t)sz, (uint32_t)rr);
+  }
   if (kVal) {  // (only DC values are used: a group is never a DC step; as decode_sym's extension)
     const uint32_t msk = (1u << sz) - 1u;
     const uint32_t x = (hi >> ((32 - l - sz) & 31)) & msk;
     val = (x >> ((sz - 1) & 31)) ? (int)x : (int)x - (int)msk;
   }
   const int tot = multi ? mb : l + sz;
-  s = multi ? (eob ^ 1) : sz;
-  r = multi ? (eob ? 0 : mdz - 1) : rr;
+  adv = multi ? (eob ? 64 : mdz) : a;
   b.buf <<= tot;
   b.nb -= tot;
   b.pos += tot;
+}
+
+// The block position after a step of advance adv; true when the step ended the block.
+__device__ __forceinline__ bool adv_z(int& z, int adv) {
+  const int zn = z + adv;
+  const bool done = zn > 63;
+  z = done ? 0 : zn;
+  return done;
 }
 
 // decode_mcu's k loop: DC -> k = 1; AC value -> k += r + 1; ZRL -> k += 16; EOB -> done.
@@ -743,11 +760,13 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
         if (warmup) {
           const bool isdc = z == 0;
           const int slot = isdc ? sdc : sac;
-          int sz, r;
+          bool done;
           if constexpr (kMulti) {
-            int unused;
-            decode_step<false>(T, b, slot, isdc, z, sz, r, unused, bad);
+            int adv, unused;
+            decode_step<false>(T, b, slot, isdc, z, adv, unused, bad);
+            done = adv_z(z, adv);
           } else {
+            int sz, r;
             bits_pull(b);
             const uint32_t hi = (uint32_t)(b.buf >> 32);
             const uint32_t e = T.lut[(slot << LB) + (hi >> (32 - LB))];
@@ -759,9 +778,10 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
             b.buf <<= tot;
             b.nb -= tot;
             b.pos += tot;
+            done = next_z(z, sz, r);
           }
           if (kStats) nsym++;
-          if (next_z(z, sz, r)) {
+          if (done) {
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
             ctx(blk, c, sdc, sac);
             if (b.pos >= start) {
@@ -785,13 +805,20 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
 #pragma unroll
       for (int u = 0; u < kSpecGroup; u++) {
         if (run) {
-          int s, r, val;
+          int val;
+          bool done;
           const bool isdc = z == 0;
-          if constexpr (kMulti) decode_step<true>(T, b, isdc ? sdc : sac, isdc, z, s, r, val, bad);
-          else decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+          if constexpr (kMulti) {
+            int adv;
+            decode_step<true>(T, b, isdc ? sdc : sac, isdc, z, adv, val, bad);
+            done = adv_z(z, adv);
+          } else {
+            int s, r;
+            decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
+            done = next_z(z, s, r);
+          }
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
-          const bool done = next_z(z, s, r);
           if (keep_rec && done && nrec < kRecStore)  // one 8-byte store (SyncRec: p, dc, blk, pad)
             reinterpret_cast<uint2*>(rec)[nrec] =
                 make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
