@@ -58,6 +58,12 @@ constexpr int kMaxSlots = 2 * kMaxComp;  // a DC and an AC table per component a
 __device__ __forceinline__ uint32_t write_adv(bool ac, uint32_t s, uint32_t r) {
   return !ac ? 1u : ((s == 0 && r != 15) ? 64u : r + 1u);
 }
+// A decode-table entry (len | size << 4 | run << 8) in the write and sync passes' format:
+// len | size << 4 | advance << 8.
+__device__ __forceinline__ uint32_t write_entry(uint32_t e, bool ac) {
+  const uint32_t l = e & 15, sz = (e >> 4) & 15, r = (e >> 8) & 15;
+  return l == 0 ? 0u : (l | (sz << 4) | (write_adv(ac, sz, r) << 8));
+}
 
 // ------------------------------------------------------------------------------------------
 // Per-image decode tables in LDS.
@@ -311,14 +317,15 @@ struct SyncTables {
   uint32_t pk_dc[2], pk_ac[2], pk_c;
 };
 
-// The 9-bit lookahead from the image's LB-bit one: entry k << (LB - 9) when its code fits 9 bits.
+// The 9-bit lookahead from the image's LB-bit one: entry k << (LB - 9) when its code fits 9 bits, in
+// the write_entry format (size and advance).
 template <int LB>
 __device__ void load_sync_tables(SyncTables& T, const EntTables* g) {
   const int ns = g->nslots;
   for (int i = threadIdx.x; i < (ns << kSyncLB); i += blockDim.x) {
     const int q = i >> kSyncLB, k = i & ((1 << kSyncLB) - 1);
     const uint16_t e = g->lut[(q << LB) + (k << (LB - kSyncLB))];
-    T.lut[i] = (e & 15) <= kSyncLB ? e : (uint16_t)0;
+    T.lut[i] = (e & 15) <= kSyncLB ? (uint16_t)write_entry(e, (g->slot_src[q] & 4) != 0) : (uint16_t)0;
   }
   for (int i = threadIdx.x; i < ns * 18; i += blockDim.x) {
     T.maxcode[i / 18][i % 18] = g->maxcode[i / 18][i % 18];
@@ -544,11 +551,6 @@ struct WriteTables {
   uint32_t pad[3];
 };
 
-// A decode-table entry in the write pass's format: len | size << 4 | advance << 8 (write_adv).
-__device__ __forceinline__ uint32_t write_entry(uint32_t e, bool ac) {
-  const uint32_t l = e & 15, sz = (e >> 4) & 15, r = (e >> 8) & 15;
-  return l == 0 ? 0u : (l | (sz << 4) | (write_adv(ac, sz, r) << 8));
-}
 
 template <int LB, class TT>
 __device__ __forceinline__ uint32_t lookup(const TT& T, int slot, uint32_t hi) {
@@ -589,20 +591,20 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   b.pos += tot;
 }
 
-// decode_sym for the write pass's tables (write_entry format): the symbol's size and its advance of the
-// zigzag position instead of (size, run).  A bad code (JWRN_HUFF_BAD_CODE) sets `bad`.
-template <int Q>
-__device__ __forceinline__ void decode_wsym(const WriteTables& T, BitsQ<Q>& b, int slot, bool isdc, int& s, int& adv,
-                                            int& val, int& bad) {
+// decode_sym for tables in the write_entry format (the write and sync passes'): the symbol's size and its
+// advance of the zigzag position instead of (size, run).  A bad code (JWRN_HUFF_BAD_CODE) sets `bad`.
+template <int LB, class TT, int Q>
+__device__ __forceinline__ void decode_wsym(const TT& T, BitsQ<Q>& b, int slot, bool isdc, int& s, int& adv, int& val,
+                                            int& bad) {
   bits_pull(b);
   const uint32_t hi = (uint32_t)(b.buf >> 32);
-  const uint32_t e = lookup<11>(T, slot, hi);
+  const uint32_t e = lookup<LB>(T, slot, hi);
   int l = e & 15;
   s = (e >> 4) & 15;
   adv = (e >> 8) & 127;
   if (l == 0) {
     int r;
-    long_code<kW1>(T, slot, isdc, hi, l, s, r, bad);
+    long_code<TT::kTwoLevel ? kW1 : LB>(T, slot, isdc, hi, l, s, r, bad);
     adv = (int)write_adv(!isdc, (uint32_t)s, (uint32_t)r);
   }
   const int tot = l + s;
@@ -736,10 +738,15 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   bits_init(b, src, ws, S.lim_bit);
   int blk = at ? at_blk : init_blk, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
   int d0 = 0, d1 = 0, d2 = 0;
-  // MCU block context: the 6-bit packing for the LB = 11 images (<= 4 table slots), else the 4-bit ones
+  // MCU block context: for the LB = 11 images (<= 4 table slots) the 5-bit packing, whose third value
+  // is whether the component changes after the block (the DC sums rotate through the MCU's component
+  // cycle as the write pass's predictors do: d0 is the current block's component), else the 4-bit
+  // packings and the component
   auto ctx = [&](int bk, int& cc, int& dc_slot, int& ac_slot) {
     if constexpr (kMulti) {
-      ctx_all6(K, bk, cc, dc_slot, ac_slot);
+      bool chg;
+      ctx_w5(K, bk, dc_slot, ac_slot, chg);
+      cc = chg;
     } else {
       cc = ctx_c(K, bk);
       dc_slot = ctx_dc(K, bk);
@@ -748,6 +755,13 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   };
   int c, sdc, sac;
   ctx(blk, c, sdc, sac);
+  // the MCU's component cycle: succ[c] = the component after c's blocks; n3: three components in it
+  int succ[kMaxComp] = {0, 0, 0};
+  for (int bb = 0; bb < K.bpm; bb++) {
+    const int cb = ctx_c(K, bb), cn = ctx_c(K, bb + 1 == K.bpm ? 0 : bb + 1);
+    if (cn != cb) succ[cb] = cn;
+  }
+  const bool n3 = kMulti && succ[succ[ctx_c(K, 0)]] != ctx_c(K, 0) && succ[ctx_c(K, 0)] != ctx_c(K, 0);
   uint32_t entry = at ? at_p : start;
   int entry_blk = blk;
   bool warmup = !at && b.pos < start;
@@ -823,7 +837,18 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
             reinterpret_cast<uint2*>(rec)[nrec] =
                 make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
           // block end without branches: the sums, counters and the next block's context by selects
-          add_dc(c, done ? dcd : 0, d0, d1, d2);
+          if constexpr (kMulti) {
+            // (d0, d1, d2) -> (d1, d2, d0) after a block whose successor is of the next component (two
+            // components: (d0, d1) -> (d1, d0))
+            d0 += done ? dcd : 0;
+            const bool rot = done & (c != 0);
+            const int t0 = d0;
+            d0 = rot ? d1 : d0;
+            d1 = rot ? (n3 ? d2 : t0) : d1;
+            d2 = rot ? (n3 ? t0 : d2) : d2;
+          } else {
+            add_dc(c, done ? dcd : 0, d0, d1, d2);
+          }
           nrec += done ? 1 : 0;
           nblk += done ? 1 : 0;
           blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
@@ -836,6 +861,16 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           !__builtin_amdgcn_ballot_w64(run))
         break;
     }
+  }
+  if constexpr (kMulti) {  // the rotating sums back to component order
+    const int ce = ctx_c(K, blk), c1 = succ[ce], c2 = succ[c1];
+    int o0 = 0, o1 = 0, o2 = 0;
+    add_dc(ce, d0, o0, o1, o2);
+    if (c1 != ce) add_dc(c1, d1, o0, o1, o2);
+    if (n3) add_dc(c2, d2, o0, o1, o2);
+    d0 = o0;
+    d1 = o1;
+    d2 = o2;
   }
   S.entry_p = entry;
   S.entry_bz = (uint16_t)(entry_blk << 8);
@@ -876,12 +911,12 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
 #pragma unroll
       for (int u = 0; u < kSpecGroup; u++) {
         if (run) {
-          int sy, r, val;
+          int sy, adv, val;
           const bool isdc = z == 0;
-          decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, sy, r, val, bad);
+          decode_wsym<LB>(T, b, isdc ? sdc : sac, isdc, sy, adv, val, bad);
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;
-          if (next_z(z, sy, r)) {
+          if (adv_z(z, adv)) {
             add_dc(c, dcd, d0, d1, d2);
             nblk++;
             blk = blk + 1 == K.bpm ? 0 : blk + 1;
@@ -1373,7 +1408,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           bool done;
           if constexpr (LB == 11) {
             int s, adv;
-            decode_wsym(T, b, isdc ? sdc : sac, isdc, s, adv, val, bad);
+            decode_wsym<11>(T, b, isdc ? sdc : sac, isdc, s, adv, val, bad);
             if (kStats) nsym++;
             // DC: predictor update (jdhuff.c last_dc_val); AC value at natural_order[k + r], k + r =
             // k + advance - 1 (jpeg_natural_order's guard entries send positions past 63 to 63).  EOB
