@@ -387,7 +387,7 @@ struct BitsQ {
   const uint32_t* src;
   uint64_t buf;
   int nb;
-  int nq;        // valid words in q
+  uint32_t wend; // word index one past the queued words (wend - wi valid words in q)
   uint32_t wi;   // word index of q[0]
   uint32_t pos;  // absolute bit position of the next unconsumed bit
   uint32_t lim;  // bits at or beyond lim read as zeros (the data ran into a marker)
@@ -412,8 +412,8 @@ __device__ __forceinline__ void bits_init(BitsQ<Q>& b, const uint32_t* src, uint
   const int sh = p & 31;
   b.buf = (((uint64_t)hi << 32) | lo) << sh;
   b.nb = 64 - sh;
-  b.nq = 0;
   b.wi = w + 2;
+  b.wend = b.wi;
   b.pos = p;
 #pragma unroll
   for (int k = 0; k < Q; k++) b.q[k] = 0;
@@ -439,12 +439,17 @@ __device__ __forceinline__ void bits_fill(BitsQ<Q>& b) {
 #pragma unroll
     for (int k = 0; k < Q; k++) b.q[k] = load_word(b.src, b.wi + k, b.lim);
   }
-  b.nq = Q;
+  b.wend = b.wi + Q;
 }
+
+// Bits held (the window and the queue): a group of symbols may run without a refill check while this
+// covers them (the refill thresholds kRefillSpec / kRefillWrite).
+template <int Q>
+__device__ __forceinline__ int bits_avail(const BitsQ<Q>& b) { return b.nb + 32 * (int)(b.wend - b.wi); }
 
 // Can the next symbol (at most 32 bits) be decoded without a refill?
 template <int Q>
-__device__ __forceinline__ bool bits_can(const BitsQ<Q>& b) { return b.nb > 32 || b.nq > 0; }
+__device__ __forceinline__ bool bits_can(const BitsQ<Q>& b) { return b.nb > 32 || b.wi < b.wend; }
 
 template <int Q>
 __device__ __forceinline__ void bits_pull(BitsQ<Q>& b) {
@@ -455,7 +460,6 @@ __device__ __forceinline__ void bits_pull(BitsQ<Q>& b) {
   b.nb += need ? 32 : 0;
 #pragma unroll
   for (int k = 0; k + 1 < Q; k++) b.q[k] = need ? b.q[k + 1] : b.q[k];
-  b.nq -= need ? 1 : 0;
   b.wi += need ? 1u : 0u;
 }
 
@@ -736,7 +740,7 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   const uint32_t ws = at ? at_p : (S.first ? start : (start - seg_start > warm ? start - warm : seg_start));
   Bits b;
   bits_init(b, src, ws, S.lim_bit);
-  int blk = at ? at_blk : init_blk, z = 0, nblk = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;
+  int blk = at ? at_blk : init_blk, z = 0, nrec = 0, dcd = 0, bad = 0, nsym = 0;  // nrec: also the block count
   int d0 = 0, d1 = 0, d2 = 0;
   // MCU block context: for the LB = 11 images (<= 4 table slots) the 5-bit packing, whose third value
   // is whether the component changes after the block (the DC sums rotate through the MCU's component
@@ -806,7 +810,7 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           }
         }
       }
-      if (__builtin_amdgcn_ballot_w64(warmup && b.nb + 32 * b.nq < kRefillSpec) ||
+      if (__builtin_amdgcn_ballot_w64(warmup && bits_avail(b) < kRefillSpec) ||
           !__builtin_amdgcn_ballot_w64(warmup))
         break;
     }
@@ -850,14 +854,13 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
             add_dc(c, done ? dcd : 0, d0, d1, d2);
           }
           nrec += done ? 1 : 0;
-          nblk += done ? 1 : 0;
           blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
           ctx(blk, c, sdc, sac);
           run = b.pos < end || z != 0;
         }
       }
       // leave to refill when a running lane may not hold kSpecGroup more symbols (<= 32 bits each)
-      if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < kRefillSpec) ||
+      if (__builtin_amdgcn_ballot_w64(run && bits_avail(b) < kRefillSpec) ||
           !__builtin_amdgcn_ballot_w64(run))
         break;
     }
@@ -876,7 +879,7 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   S.entry_bz = (uint16_t)(entry_blk << 8);
   S.spec_exit_p = S.cur_exit_p = b.pos;
   S.spec_exit_bz = S.cur_exit_bz = (uint16_t)((blk << 8) | z);
-  S.spec_nblk = S.cur_nblk = nblk;
+  S.spec_nblk = S.cur_nblk = nrec;
   S.spec_dc[0] = S.cur_dc[0] = d0;
   S.spec_dc[1] = S.cur_dc[1] = d1;
   S.spec_dc[2] = S.cur_dc[2] = d2;
@@ -951,7 +954,7 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
           next_chk = lo < nrec ? b.pos + kMergeBits : 0xFFFFFFFFu;
         }
       }
-      if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < kRefillSpec) ||
+      if (__builtin_amdgcn_ballot_w64(run && bits_avail(b) < kRefillSpec) ||
           !__builtin_amdgcn_ballot_w64(run))
         break;
     }
@@ -1480,7 +1483,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           __builtin_amdgcn_wave_barrier();
         }
        }
-        if (__builtin_amdgcn_ballot_w64(run && b.nb + 32 * b.nq < kRefillWrite) ||
+        if (__builtin_amdgcn_ballot_w64(run && bits_avail(b) < kRefillWrite) ||
             !__builtin_amdgcn_ballot_w64(run))
           break;
       }
