@@ -570,6 +570,14 @@ __device__ __forceinline__ uint32_t lookup(const TT& T, int slot, uint32_t hi) {
   }
 }
 
+// HUFF_EXTEND of the s extra bits that follow the code inside hi (l + s = tot <= 27): x < 2^(s-1) ->
+// x - (2^s - 1); s = 0 -> 0 (a zero-width field extract, mask 0).  One bit-field extract for x.
+__device__ __forceinline__ int huff_extend(uint32_t hi, int tot, int s) {
+  const uint32_t x = __builtin_amdgcn_ubfe(hi, (uint32_t)(32 - tot), (uint32_t)s);
+  const uint32_t msk = (1u << s) - 1u;
+  return (x >> ((s - 1) & 31)) ? (int)x : (int)x - (int)msk;
+}
+
 // One symbol (jdhuff.c HUFF_DECODE + get_bits + HUFF_EXTEND): DC -> category s, r = 0;
 // AC -> (r, s).  val = the extended value (0 when s = 0).
 template <int LB, class TT, int Q>
@@ -587,9 +595,7 @@ __device__ __forceinline__ void decode_sym(const TT& T, BitsQ<Q>& b, int slot, b
   // HUFF_EXTEND without branches: the s extra bits follow the l code bits inside hi (l + s <= 27; a
   // bad code has s = 0), x < 2^(s-1) -> x - (2^s - 1); s = 0 -> x = 0, mask 0 -> 0
   const int tot = l + s;
-  const uint32_t msk = (1u << s) - 1u;
-  const uint32_t x = (hi >> ((32 - tot) & 31)) & msk;
-  val = (x >> ((s - 1) & 31)) ? (int)x : (int)x - (int)msk;
+  val = huff_extend(hi, tot, s);
   b.buf <<= tot;
   b.nb -= tot;
   b.pos += tot;
@@ -612,9 +618,7 @@ __device__ __forceinline__ void decode_wsym(const TT& T, BitsQ<Q>& b, int slot, 
     adv = (int)write_adv(!isdc, (uint32_t)s, (uint32_t)r);
   }
   const int tot = l + s;
-  const uint32_t msk = (1u << s) - 1u;
-  const uint32_t x = (hi >> ((32 - tot) & 31)) & msk;
-  val = (x >> ((s - 1) & 31)) ? (int)x : (int)x - (int)msk;
+  val = huff_extend(hi, tot, s);
   b.buf <<= tot;
   b.nb -= tot;
   b.pos += tot;
@@ -641,11 +645,7 @@ __device__ __forceinline__ void decode_step(const TT& T, BitsQ<Q>& b, int slot, 
     long_code<kMW>(T, slot, isdc, hi, l, sz, rr, bad);
     a = (int)write_adv(!isdc, (uint32_t)sz, (uint32_t)rr);
   }
-  if (kVal) {  // (only DC values are used: a group is never a DC step; as decode_sym's extension)
-    const uint32_t msk = (1u << sz) - 1u;
-    const uint32_t x = (hi >> ((32 - l - sz) & 31)) & msk;
-    val = (x >> ((sz - 1) & 31)) ? (int)x : (int)x - (int)msk;
-  }
+  if (kVal) val = huff_extend(hi, l + sz, sz);  // (only DC values are used: a group is never a DC step)
   const int tot = multi ? mb : l + sz;
   adv = multi ? (eob ? 64 : mdz) : a;
   b.buf <<= tot;
