@@ -364,11 +364,12 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
           const int x = xb + 8 * gi, jg = x >> 1;
           const int oY = L.rinfo[q][0], oBi = L.rinfo[q][1], oRi = L.rinfo[q][3];
           const uint32_t* sw = L.st;
+          const uint8_t* sb = reinterpret_cast<const uint8_t*>(L.st);  // (byte offsets: rinfo's are bytes)
           // the item's 8 luma bytes as one 8-byte read (oY + x is 8-aligned: kFYDW is even, xb and x are
           // multiples of 8): consecutive items 8 bytes apart fill all 64 banks, where two dword reads at
           // a 2-dword lane stride met 2-way bank conflicts
           static_assert(kFYDW % 2 == 0, "8-byte aligned luma rows");
-          const uint2 yy = *reinterpret_cast<const uint2*>(&sw[(oY + x) >> 2]);
+          const uint2 yy = *reinterpret_cast<const uint2*>(sb + oY + x);
           const uint32_t y0 = yy.x, y1 = yy.y;
           uint32_t wr[2] = {0, 0}, wg[2] = {0, 0}, wb[2] = {0, 0};
           if (LAY == kRs444) {
@@ -393,8 +394,12 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
             const int oBf = L.rinfo[q][2], oRf = L.rinfo[q][4];
             int ube[4], ubo[4], ure[4], uro[4];  // upsampled Cb / Cr of the even / odd pixel of column jg + k
             auto up = [&](int oi, int of, int* ue, int* uo) {
-              const uint32_t i0 = sw[(oi + jg - 4) >> 2], i1 = sw[(oi + jg) >> 2], i2 = sw[(oi + jg + 4) >> 2];
-              const uint32_t f0 = sw[(of + jg - 4) >> 2], f1 = sw[(of + jg) >> 2], f2 = sw[(of + jg + 4) >> 2];
+              // (oi + jg and of + jg are multiples of 4: rinfo's offsets and jalC, jb and jg are; one address
+              // per row, the neighbour dwords at immediate offsets)
+              const uint32_t* wi = reinterpret_cast<const uint32_t*>(sb + oi + jg);
+              const uint32_t* wf = reinterpret_cast<const uint32_t*>(sb + of + jg);
+              const uint32_t i0 = wi[-1], i1 = wi[0], i2 = wi[1];
+              const uint32_t f0 = wf[-1], f1 = wf[0], f2 = wf[1];
               if (jg > 0 && jg + 4 <= dwc - 1) {
                 constexpr uint32_t M = 0x00FF00FFu;
                 const uint32_t E = (i1 & M) * 3 + (f1 & M), O = ((i1 >> 8) & M) * 3 + ((f1 >> 8) & M);  // [jg, jg+2], [jg+1, jg+3]
@@ -447,7 +452,8 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
             // output pixel (3 * own + neighbour + 1 or 2) >> 2; interior items two columns per op
             int ube[4], ubo[4], ure[4], uro[4];
             auto up = [&](int oi, int* ue, int* uo) {
-              const uint32_t i0 = sw[(oi + jg - 4) >> 2], i1 = sw[(oi + jg) >> 2], i2 = sw[(oi + jg + 4) >> 2];
+              const uint32_t* wi = reinterpret_cast<const uint32_t*>(sb + oi + jg);  // (a multiple of 4, as for 4:2:0)
+              const uint32_t i0 = wi[-1], i1 = wi[0], i2 = wi[1];
               if (jg > 0 && jg + 4 <= dwc - 1) {
                 constexpr uint32_t M = 0x00FF00FFu;
                 const uint32_t E = i1 & M, O = (i1 >> 8) & M;  // columns [jg, jg+2], [jg+1, jg+3]
