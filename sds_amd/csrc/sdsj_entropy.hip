@@ -381,6 +381,8 @@ constexpr int kRefillSpec = 27 * (kSpecGroup - 1) + 32;
 constexpr int kRecStore = SDSJ_REC_STORE;
 static_assert(kRecStore <= kRec, "records fit their scratch");
 constexpr int kRefillWrite = 27 * (kWriteGroup - 1) + 32;
+constexpr int kFlushEvery = kWriteGroup;  // write pass: steps between stage flushes (every 2: 12.9 ms, 4: 12.8)
+static_assert(kWriteGroup % kFlushEvery == 0, "a group ends with a flush: nothing is pending across a refill");
 
 template <int Q>
 struct BitsQ {
@@ -1402,15 +1404,18 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       stop_pos = last_of_seg ? lim + 1 : end_bit;
       stop_blk = last_of_seg ? 1u : 0xFFFFFFFFu;
     }
+    // A completed block waits in its lane's stage for the next flush step (every kFlushEvery steps of
+    // the group), and the lane decodes nothing until then: a flush per step cost as much as the
+    // decode itself (some lane of the wave completes a block at almost every step).
+    bool pending = false;
+    uint32_t gpend = 0;
     while (__builtin_amdgcn_ballot_w64(run)) {
       if (run) bits_fill(b);
       for (;;) {
 #pragma unroll
        for (int u = 0; u < kWriteGroup; u++) {
         if (kStats) witers++;
-        bool ready = false;
-        uint32_t gdone = 0;
-        if (run) {
+        if (run && !pending) {
           const bool isdc = z == 0;
           int val;
           bool done;
@@ -1439,8 +1444,8 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
             L.stage[my_base + wpos] = (int16_t)(isdc ? pc : val);
             done = next_z(z, s, r);
           }
-          ready = done;
-          gdone = (uint32_t)g;
+          pending = done;
+          gpend = (uint32_t)g;
           if constexpr (LB == 11) {
             // (pc, p0, p1) -> (p0, p1, pc) with 3 components in the scan, (pc, p0) -> (p0, pc) with 2
             const bool rot = done & chg;
@@ -1464,13 +1469,13 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           // (after a symbol z = 0 exactly when it ended the block; stop_blk: every block, or MCU starts)
           run = (g < gend) & !(done & ((stop_blk != 1u) | (blk == 0)) & (b.pos >= stop_pos));
         }
-        // cooperative flush of the blocks completed in this step: 8 lanes x 16 B per block
-        const uint64_t m = __builtin_amdgcn_ballot_w64(ready);
+        // cooperative flush of the blocks completed since the last flush: 8 lanes x 16 B per block
+        const uint64_t m = u % kFlushEvery == kFlushEvery - 1 ? __builtin_amdgcn_ballot_w64(pending) : 0ull;
         if (m) {
           const int cnt = __popcll(m);
-          if (ready) {
+          if (pending) {
             const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            L.flist[wv][idx] = ((uint32_t)t << 24) | gdone;
+            L.flist[wv][idx] = ((uint32_t)t << 24) | gpend;
           }
           // (a wave's LDS accesses execute in issue order: the reads below see these writes, and the
           // owner's next stage writes land after the clears -- no waits beyond the data dependences)
@@ -1486,6 +1491,7 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
             }
           }
           __builtin_amdgcn_wave_barrier();
+          pending = false;
         }
        }
         if (__builtin_amdgcn_ballot_w64(run && bits_avail(b) < kRefillWrite) ||
