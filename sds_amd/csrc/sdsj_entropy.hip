@@ -1406,9 +1406,10 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
     }
     // A completed block waits in its lane's stage for the next flush step (every kFlushEvery steps of
     // the group), and the lane decodes nothing until then: a flush per step cost as much as the
-    // decode itself (some lane of the wave completes a block at almost every step).
+    // decode itself (some lane of the wave completes a block at almost every step).  The block-end
+    // bookkeeping (predictors, MCU position and context, block index, stop rule) runs there too, once
+    // per flush instead of as selects on every step.
     bool pending = false;
-    uint32_t gpend = 0;
     while (__builtin_amdgcn_ballot_w64(run)) {
       if (run) bits_fill(b);
       for (;;) {
@@ -1445,29 +1446,6 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
             done = next_z(z, s, r);
           }
           pending = done;
-          gpend = (uint32_t)g;
-          if constexpr (LB == 11) {
-            // (pc, p0, p1) -> (p0, p1, pc) with 3 components in the scan, (pc, p0) -> (p0, pc) with 2
-            const bool rot = done & chg;
-            const int t0 = pc;
-            pc = rot ? p0 : pc;
-            p0 = rot ? (ncomp == 3 ? p1 : t0) : p0;
-            p1 = rot ? (ncomp == 3 ? t0 : p1) : p1;
-            blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
-            ctx_w5(K, blk, sdc, sac, chg);
-          } else {
-            p0 = (done & (c == 0)) ? pc : p0;
-            p1 = (done & (c == 1)) ? pc : p1;
-            p2 = (done & (c == 2)) ? pc : p2;
-            blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
-            c = ctx_c(K, blk);
-            sdc = ctx_dc(K, blk);
-            sac = ctx_ac(K, blk);
-            pc = done ? (c == 0 ? p0 : (c == 1 ? p1 : p2)) : pc;
-          }
-          g += done ? 1 : 0;
-          // (after a symbol z = 0 exactly when it ended the block; stop_blk: every block, or MCU starts)
-          run = (g < gend) & !(done & ((stop_blk != 1u) | (blk == 0)) & (b.pos >= stop_pos));
         }
         // cooperative flush of the blocks completed since the last flush: 8 lanes x 16 B per block
         const uint64_t m = u % kFlushEvery == kFlushEvery - 1 ? __builtin_amdgcn_ballot_w64(pending) : 0ull;
@@ -1475,7 +1453,31 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
           const int cnt = __popcll(m);
           if (pending) {
             const int idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            L.flist[wv][idx] = ((uint32_t)t << 24) | gpend;
+            L.flist[wv][idx] = ((uint32_t)t << 24) | (uint32_t)g;
+            // the block end: the component's predictor back, the next block's out
+            if constexpr (LB == 11) {
+              // (pc, p0, p1) -> (p0, p1, pc) with 3 components in the scan, (pc, p0) -> (p0, pc) with 2
+              if (chg) {
+                const int t0 = pc;
+                pc = p0;
+                p0 = ncomp == 3 ? p1 : t0;
+                p1 = ncomp == 3 ? t0 : p1;
+              }
+              blk = blk + 1 == K.bpm ? 0 : blk + 1;
+              ctx_w5(K, blk, sdc, sac, chg);
+            } else {
+              p0 = c == 0 ? pc : p0;
+              p1 = c == 1 ? pc : p1;
+              p2 = c == 2 ? pc : p2;
+              blk = blk + 1 == K.bpm ? 0 : blk + 1;
+              c = ctx_c(K, blk);
+              sdc = ctx_dc(K, blk);
+              sac = ctx_ac(K, blk);
+              pc = c == 0 ? p0 : (c == 1 ? p1 : p2);
+            }
+            g++;
+            // the stop rule at this block boundary (stop_blk: every block, or MCU starts)
+            run = (g < gend) & !(((stop_blk != 1u) | (blk == 0)) & (b.pos >= stop_pos));
           }
           // (a wave's LDS accesses execute in issue order: the reads below see these writes, and the
           // owner's next stage writes land after the clears -- no waits beyond the data dependences)
