@@ -821,45 +821,49 @@ __device__ int spec_pass(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   while (__builtin_amdgcn_ballot_w64(run)) {
     if (run) bits_fill(b);
     for (;;) {
-      // kSpecGroup symbols per wave-uniform check: every running lane holds >= bits for them
+      // kSpecGroup symbols per wave-uniform check: every running lane holds >= bits for them.  A lane
+      // that completes a block waits for the group's end, where the block-end bookkeeping (record,
+      // DC sums, MCU position and context, the stop test) runs once instead of as selects on every step
+      bool pend = false;
 #pragma unroll
       for (int u = 0; u < kSpecGroup; u++) {
-        if (run) {
+        if (run && !pend) {
           int val;
-          bool done;
           const bool isdc = z == 0;
           if constexpr (kMulti) {
             int adv;
             decode_step<true>(T, b, isdc ? sdc : sac, isdc, z, adv, val, bad);
-            done = adv_z(z, adv);
+            pend = adv_z(z, adv);
           } else {
             int s, r;
             decode_sym<LB>(T, b, isdc ? sdc : sac, isdc, s, r, val, bad);
-            done = next_z(z, s, r);
+            pend = next_z(z, s, r);
           }
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;  // (the block's DC difference joins its component's sum at the block end)
-          if (keep_rec && done && nrec < kRecStore)  // one 8-byte store (SyncRec: p, dc, blk, pad)
-            reinterpret_cast<uint2*>(rec)[nrec] =
-                make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
-          // block end without branches: the sums, counters and the next block's context by selects
-          if constexpr (kMulti) {
-            // (d0, d1, d2) -> (d1, d2, d0) after a block whose successor is of the next component (two
-            // components: (d0, d1) -> (d1, d0))
-            d0 += done ? dcd : 0;
-            const bool rot = done & (c != 0);
-            const int t0 = d0;
-            d0 = rot ? d1 : d0;
-            d1 = rot ? (n3 ? d2 : t0) : d1;
-            d2 = rot ? (n3 ? t0 : d2) : d2;
-          } else {
-            add_dc(c, done ? dcd : 0, d0, d1, d2);
-          }
-          nrec += done ? 1 : 0;
-          blk = done ? (blk + 1 == K.bpm ? 0 : blk + 1) : blk;
-          ctx(blk, c, sdc, sac);
-          run = b.pos < end || z != 0;
         }
+      }
+      if (pend) {
+        if (keep_rec && nrec < kRecStore)  // one 8-byte store (SyncRec: p, dc, blk, pad)
+          reinterpret_cast<uint2*>(rec)[nrec] =
+              make_uint2(b.pos, ((uint32_t)dcd & 0xFFFFu) | ((uint32_t)(blk & 0xFF) << 16));
+        if constexpr (kMulti) {
+          // (d0, d1, d2) -> (d1, d2, d0) after a block whose successor is of the next component (two
+          // components: (d0, d1) -> (d1, d0))
+          d0 += dcd;
+          if (c != 0) {
+            const int t0 = d0;
+            d0 = d1;
+            d1 = n3 ? d2 : t0;
+            d2 = n3 ? t0 : d2;
+          }
+        } else {
+          add_dc(c, dcd, d0, d1, d2);
+        }
+        nrec++;
+        blk = blk + 1 == K.bpm ? 0 : blk + 1;
+        ctx(blk, c, sdc, sac);
+        run = b.pos < end;  // (at a block boundary)
       }
       // leave to refill when a running lane may not hold kSpecGroup more symbols (<= 32 bits each)
       if (__builtin_amdgcn_ballot_w64(run && bits_avail(b) < kRefillSpec) ||
