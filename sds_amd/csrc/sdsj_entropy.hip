@@ -917,24 +917,26 @@ __device__ int sync_full(const TT& T, const BlkCtx& K, const uint32_t* src, SubS
   while (__builtin_amdgcn_ballot_w64(run)) {
     if (run) bits_fill(b);
     for (;;) {
+      bool pend = false;  // (a completed block's bookkeeping waits for the group's end, as in spec_pass)
 #pragma unroll
       for (int u = 0; u < kSpecGroup; u++) {
-        if (run) {
+        if (run && !pend) {
           int sy, adv, val;
           const bool isdc = z == 0;
           decode_wsym<LB>(T, b, isdc ? sdc : sac, isdc, sy, adv, val, bad);
           if (kStats) nsym++;
           dcd = isdc ? val : dcd;
-          if (adv_z(z, adv)) {
-            add_dc(c, dcd, d0, d1, d2);
-            nblk++;
-            blk = blk + 1 == K.bpm ? 0 : blk + 1;
-            c = ctx_c(K, blk);
-            sdc = ctx_dc(K, blk);
-            sac = ctx_ac(K, blk);
-          }
-          run = b.pos < end || z != 0;
+          pend = adv_z(z, adv);
         }
+      }
+      if (pend) {
+        add_dc(c, dcd, d0, d1, d2);
+        nblk++;
+        blk = blk + 1 == K.bpm ? 0 : blk + 1;
+        c = ctx_c(K, blk);
+        sdc = ctx_dc(K, blk);
+        sac = ctx_ac(K, blk);
+        run = b.pos < end;  // (at a block boundary)
       }
       if (run && z == 0 && b.pos >= next_chk) {
         // first record at or after b.pos; a record there for the block just completed = merged
