@@ -30,7 +30,7 @@ static_assert((kDecodeThreads & (kDecodeThreads - 1)) == 0 && kDecodeThreads >= 
               "a power of two number of waves");
 constexpr int kMinSubBits = 1024;     // minimum entropy subsequence length (bits)
 #ifndef SDSJ_WARM_BITS
-#define SDSJ_WARM_BITS 3000
+#define SDSJ_WARM_BITS 2500
 #endif
 constexpr int kWarmBits = SDSJ_WARM_BITS;  // speculative warm-up before each subsequence (bits, <= 1.5 x sub_bits)
 constexpr int kWarmBitsSmall = 4000;  // ... for lanes of fewer than kWarmSmallLane images (the sync pass is

@@ -610,14 +610,36 @@ __device__ __forceinline__ void decode_wsym(const TT& T, BitsQ<Q>& b, int slot, 
                                             int& bad) {
   bits_pull(b);
   const uint32_t hi = (uint32_t)(b.buf >> 32);
-  const uint32_t e = lookup<LB>(T, slot, hi);
-  int l = e & 15;
-  s = (e >> 4) & 15;
-  adv = (e >> 8) & 127;
-  if (l == 0) {
-    int r;
-    long_code<TT::kTwoLevel ? kW1 : LB>(T, slot, isdc, hi, l, s, r, bad);
-    adv = (int)write_adv(!isdc, (uint32_t)s, (uint32_t)r);
+  int l;
+  if constexpr (TT::kTwoLevel) {
+    // one branch for both rare cases (a code longer than the first level: its second level, and codes
+    // longer than that the canonical search)
+    const uint32_t e = T.lut[(slot << kW1) + (hi >> (32 - kW1))];
+    l = e & 15;
+    s = (e >> 4) & 15;
+    adv = (e >> 8) & 127;
+    if (l == 0) {
+      const uint32_t sub = e >> 4;
+      const uint32_t e2 = sub ? T.l2[((sub - 1) << 2) + ((hi >> (32 - kW1 - 2)) & 3)] : 0u;
+      l = e2 & 15;
+      s = (e2 >> 4) & 15;
+      adv = (e2 >> 8) & 127;
+      if (l == 0) {
+        int r;
+        long_code<kW1>(T, slot, isdc, hi, l, s, r, bad);
+        adv = (int)write_adv(!isdc, (uint32_t)s, (uint32_t)r);
+      }
+    }
+  } else {
+    const uint32_t e = lookup<LB>(T, slot, hi);
+    l = e & 15;
+    s = (e >> 4) & 15;
+    adv = (e >> 8) & 127;
+    if (l == 0) {
+      int r;
+      long_code<LB>(T, slot, isdc, hi, l, s, r, bad);
+      adv = (int)write_adv(!isdc, (uint32_t)s, (uint32_t)r);
+    }
   }
   const int tot = l + s;
   val = huff_extend(hi, tot, s);
