@@ -323,10 +323,10 @@ def main():
     # batches: one engine call per step, whose lanes drain at its end (the caller's stream orders the
     # next call after it), so larger batches amortise that (configs[1]: 455k images/s at 4096, 476k
     # at 16384; configs[2]: 45.0k at 512, 59.8k at 2048 -- DESIGN.md §5; round 5: 16,384 -> 32,768 +1.2 %,
-    # profiles/r05_batch.txt)
-    defaults = {"batch": 2048, "rows": 16384, "pool": 1024, "res": 512} if mixed else \
+    # 32,768 -> 65,536 +2.3 %; configs[2] 2,048 -> 4,096 -> 8,192: 80.5k -> 85.0k -> 87.8k; profiles/r05_batch.txt)
+    defaults = {"batch": 8192, "rows": 16384, "pool": 1024, "res": 512} if mixed else \
         {"batch": 1024, "rows": 16384, "pool": 256, "res": 512} if e2e else \
-        {"batch": 32768, "rows": None, "pool": 1024, "res": 256}
+        {"batch": 65536, "rows": None, "pool": 1024, "res": 256}
     for k, v in defaults.items():
         if getattr(args, k) is None:
             setattr(args, k, v)

@@ -7,7 +7,7 @@
 set -e
 export TMPDIR=/tmp
 export SDSJ_LANES=${SDSJ_LANES:-1}
-BATCH=${BATCH:-32768}  # bench.py's default configs[1] batch (the PMC summary is per dispatch of one lane)
+BATCH=${BATCH:-65536}  # bench.py's default configs[1] batch (the PMC summary is per dispatch of one lane)
 ROWS=$(( BATCH + 4096 ))
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 --rows $ROWS --batch $BATCH $*"
 i=0

@@ -33,6 +33,6 @@ else
   export SDSJ_HEAD=${2:-}
   tools/gpu_steps.sh \
     "prof|900|tools/profile_round.sh $tag" \
-    "pmcmixed|400|BATCH=2048 PMC_OUT=pmc_mixed512.json tools/pmc.sh --workload mixed512" \
+    "pmcmixed|600|BATCH=8192 PMC_OUT=pmc_mixed512.json tools/pmc.sh --workload mixed512" \
     "ranks8|300|python bench.py --gpus 8 --backend gloo --batch 2048 --steps 3 --warmup 1 --no-cpu-baseline --roofline-steps 1 > gpurun_out/${tag}_rehearsal_8ranks_1gpu.json"
 fi
