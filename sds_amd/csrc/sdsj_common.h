@@ -85,6 +85,11 @@ constexpr int kVTapsF = SDSJ_VTAPS_F;  // vertical taps the specialised fused ke
 SDSJ_HD constexpr int rs_ring_rows(int kt) { return kt <= 7 ? 8 : kRingMaxRows; }
 SDSJ_HD constexpr int rs_vtaps(int kt) { return kt <= 7 ? 8 : kVTapsF; }
 SDSJ_HD constexpr int rs_ring_dw(int kt) { return kt <= 7 ? 8 * 256 : kRingDW; }
+// ... and narrower staged rows: 768 source columns bring the 4:2:0 / 4:2:2 / gray kernels' LDS to
+// 26.1 KB, 6 workgroups per CU instead of 5 (27.0 KB rows of 784 columns measured no faster: 5 still).
+// KT <= 7 means ceil(support) <= 3, so a 256-column tile spans at most 256 x 3 + 2 x 3 + 4 = 778
+// columns; plan_image halves the tile of the few images above 768 (bilinear scales in (2.97, 3]).
+SDSJ_HD constexpr int rs_span(int kt) { return kt <= 7 ? 768 : kMaxSpan; }
 
 // Raw DHT content (bits[1..16], huffval) -- jdmarker.c get_dht.
 struct HuffSpec {

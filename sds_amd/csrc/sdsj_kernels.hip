@@ -125,6 +125,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
   // (bound: (tw - 1) * scale + 2 * support + 2 columns, Pillow precompute_coeffs windows)
   d->fused = 0;
   d->tile_w = 0;
+  double span = 0.0;  // the tile's source-column bound
   d->ring_rows = 1;
   while (d->ring_rows < d->ksv) d->ring_rows *= 2;  // vertical window rows kept per column
   if (d->geo != kGeoZeros && d->ring_rows <= kRingMaxRows && !nearest) {
@@ -132,8 +133,10 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
     const double supp = d->need_h ? sup * (scale < 1.0 ? 1.0 : scale) : 0.0;
     int tw = op.out_w < 256 ? op.out_w : 256;
     if (tw > kRingDW / d->ring_rows) tw = kRingDW / d->ring_rows;
+    const int lim = d->ksh <= 7 ? rs_span(d->ksh) : kMaxSpan;  // (the KT <= 7 fused kernels' rows)
     for (;;) {
-      if ((double)tw * scale + 2.0 * supp + 4.0 <= (double)kMaxSpan) {
+      span = (double)tw * scale + 2.0 * supp + 4.0;
+      if (span <= (double)lim) {
         d->fused = 1;
         d->tile_w = tw;
         break;
@@ -150,7 +153,7 @@ __device__ __host__ inline int64_t plan_image(ImgDesc* d, const sdsj_op& op, boo
   d->rs_lay = kRs420;
   if (d->fused && d->need_h && d->need_v && d->ksh >= 3 && d->ksh <= 11 && (d->ksh & 1) &&
       d->ring_rows <= rs_ring_rows(d->ksh) && d->ksv <= rs_vtaps(d->ksh) && d->tile_w * d->ring_rows <= rs_ring_dw(d->ksh) &&
-      d->comp[0].rh == 1 && d->comp[0].rv == 1) {
+      span <= (double)rs_span(d->ksh) && d->comp[0].rh == 1 && d->comp[0].rv == 1) {
     const CompDesc &c1 = d->comp[1], &c2 = d->comp[2];
     const bool same = d->ncomp == 3 && c2.rh == c1.rh && c2.rv == c1.rv && c2.dw == c1.dw && c2.dh == c1.dh;
     int lay = -1;

@@ -29,26 +29,27 @@ constexpr int kFThreads = 256;
 #define SDSJ_FROWS 4
 #endif
 constexpr int kFRows = SDSJ_FROWS;       // source rows per step
-constexpr int kFYDW = kMaxSpan / 4 + 2;  // staged luma (full-width) row (dwords)
-constexpr int kFCDW = kMaxSpan / 8 + 3;  // staged half-width chroma row (dwords)
-constexpr int kFRgbW = kMaxSpan + 32;    // RGB row pitch (bytes, even)
-
-// Per layout: staged chroma row width (dwords), staged rows (luma + both chroma planes), RGB rows.
-template <int LAY>
+// Per layout and tap count: source columns per staged row (rs_span), staged luma and chroma row widths
+// (dwords), staged rows (luma + both chroma planes), RGB rows and their pitch (bytes).
+template <int LAY, int KT>
 struct FGeo {
-  static constexpr int kCDW = LAY == kRs444 ? kFYDW : (LAY == kRsGray ? 0 : kFCDW);
+  static constexpr int kSpan = rs_span(KT);
+  static constexpr int kYDW = kSpan / 4 + 2;  // staged luma (full-width) row
+  static constexpr int kCDW = LAY == kRs444 ? kYDW : (LAY == kRsGray ? 0 : kSpan / 8 + 3);
   // staged rows per chroma plane: 4:2:0 reads rows y >> 1 and their vertical neighbours, at most
   // kFRows / 2 + 2 of them for kFRows luma rows; the other layouts the luma rows' own
   static constexpr int kCRows = LAY == kRsGray ? 0 : (LAY == kRs420 ? kFRows / 2 + 2 : kFRows);
-  static constexpr int kStageDW = kFRows * kFYDW + 2 * kCRows * kCDW;
+  static constexpr int kStageDW = kFRows * kYDW + 2 * kCRows * kCDW;
   static constexpr int kRgbRows = LAY == kRsGray ? 0 : kFRows;
+  static constexpr int kRgbW = kSpan + 32;  // (even)
   static constexpr int kRows = kFRows + 2 * kCRows;  // staged rows per step at most
 };
 
 template <int LAY, int KT>
 struct LdsF {
-  alignas(16) uint32_t st[FGeo<LAY>::kStageDW];              // step's plane rows: 4 luma, then Cb, Cr
-  alignas(16) uint8_t rgb[FGeo<LAY>::kRgbRows > 0 ? FGeo<LAY>::kRgbRows : 1][3][kFRgbW];  // converted rows, planar
+  using G = FGeo<LAY, KT>;
+  alignas(16) uint32_t st[G::kStageDW];                                  // step's plane rows: 4 luma, then Cb, Cr
+  alignas(16) uint8_t rgb[G::kRgbRows > 0 ? G::kRgbRows : 1][3][G::kRgbW];  // converted rows, planar
   uint32_t ring[rs_ring_dw(KT)];                             // per column: H results of the last R rows
   int32_t vb[kMaxStrip][2];                                  // strip rows: vertical window (first, count)
   int32_t vw[kMaxStrip][rs_vtaps(KT)];                       // strip rows: vertical weights
@@ -117,14 +118,16 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
                           void* __restrict__ out, const float* __restrict__ lut);
 
 // Route (LAY, KT): a small grid strides over the route's list (an empty route costs one short launch).
-// Occupancy: the KT <= 7 kernels' LDS (30.6 KB: the smaller ring and weight table) fits 5 workgroups
-// per CU, and 5 waves per SIMD fit their registers without spills (95 VGPRs): k_rs420<5> 9.95 -> 9.23 ms
-// per 16,384 images (profiles/r03b_rs420_occupancy_ab.txt).  The 9- and 11-tap kernels and 4:4:4 (whose
-// full-width chroma rows take 34 KB) keep 4.
+// Occupancy: the KT <= 7 kernels' LDS (the smaller ring and weight table, 768-column rows: 26.1 KB)
+// fits 6 workgroups per CU, and 6 waves per SIMD fit their registers without spills (<= 85 VGPRs with
+// the staged-row loops' addressing scalar): k_rs420<5> 29.6 -> 28.0 ms per 65,536 images
+// (profiles/r05_ab.txt; 5 waves at 30.6 KB: 9.95 -> 9.23 ms per 16,384 in round 3,
+// profiles/r03b_rs420_occupancy_ab.txt).  4:4:4 at KT <= 7 (full-width chroma rows: 30 KB) takes 5;
+// the 9- and 11-tap kernels keep 4.
 #ifndef SDSJ_RS_WAVES
-#define SDSJ_RS_WAVES 5
+#define SDSJ_RS_WAVES 6
 #endif
-#define SDSJ_RS_OCC __attribute__((amdgpu_waves_per_eu(KT <= 7 && LAY != kRs444 ? SDSJ_RS_WAVES : 4)))
+#define SDSJ_RS_OCC __attribute__((amdgpu_waves_per_eu(KT <= 7 ? (LAY != kRs444 ? SDSJ_RS_WAVES : 5) : 4)))
 template <int KT, int LAY>
 __global__ void __launch_bounds__(kFThreads) SDSJ_RS_OCC k_rs420(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                       int strip_h, int strips, int ntz, const uint8_t* __restrict__ scratch,
@@ -149,7 +152,7 @@ template <int KT, int LAY>
 __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* __restrict__ descs, const sdsj_op& op,
                           int strip_h, const uint8_t* __restrict__ scratch, const uint8_t* __restrict__ flip,
                           void* __restrict__ out, const float* __restrict__ lut) {
-  using G = FGeo<LAY>;
+  using G = FGeo<LAY, KT>;
   const ImgDesc* d = &descs[img];
   if (d->status != SDSJ_OK || d->rs_fast != KT || d->rs_lay != LAY) return;
   const int oh = op.out_h, ow = op.out_w;
@@ -158,7 +161,9 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
   const int oy1 = oy0 + strip_h < oh ? oy0 + strip_h : oh;
   __shared__ LdsF<LAY, KT> L;
   constexpr int kVT = rs_vtaps(KT);
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // (the wave index through readfirstlane: the staged-row loops' row tests and plane addresses are
+  // then scalar work, off the VALU this kernel is bound by)
+  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int64_t plane = (int64_t)oh * ow;
   OutMap om;
   om.f32 = op.out_dtype == SDSJ_DTYPE_F32;
@@ -250,22 +255,22 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
     // step's H pass, written to LDS after it), so their latency hides behind a whole step.  Wave wv
     // holds staged rows wv, wv + 4, wv + 8 (<= 12 rows), 64 dwords per load.  Colour layouts
     // (kGlds): the same rows and lanes, loaded straight into LDS by issue_lds below.
-    constexpr int kPR = (G::kRows + 3) / 4, kPC = (kMaxSpan / 4 + 2 + 63) / 64;
+    constexpr int kPR = (G::kRows + 3) / 4, kPC = (G::kSpan / 4 + 2 + 63) / 64;
     constexpr bool kGlds = LAY != kRsGray;
     uint32_t pre[kPR][kPC];
     auto row_src = [&](const Step& p, int row, const uint8_t*& g, int& nd, int& o) {
       if (row < p.nr) {
         g = pY + (int64_t)(p.ya + row) * pitchY + jalY;
         nd = ndY;
-        o = row * kFYDW;
+        o = row * G::kYDW;
       } else if (row < p.nr + p.nrc) {
         g = pCb + (int64_t)(p.ilo + row - p.nr) * pitchC + jalC;
         nd = ndC;
-        o = kFRows * kFYDW + (row - p.nr) * G::kCDW;
+        o = kFRows * G::kYDW + (row - p.nr) * G::kCDW;
       } else {
         g = pCr + (int64_t)(p.ilo + row - p.nr - p.nrc) * pitchC + jalC;
         nd = ndC;
-        o = kFRows * kFYDW + G::kCRows * G::kCDW + (row - p.nr - p.nrc) * G::kCDW;
+        o = kFRows * G::kYDW + G::kCRows * G::kCDW + (row - p.nr - p.nrc) * G::kCDW;
       }
     };
     auto issue = [&](const Step& p) {
@@ -326,11 +331,11 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
           i = ci - p.ilo;
           f = cfr - p.ilo;
         }
-        L.rinfo[t][0] = 4 * (t * kFYDW) - jalY;
-        L.rinfo[t][1] = 4 * (kFRows * kFYDW + i * G::kCDW) - jalC;
-        L.rinfo[t][2] = 4 * (kFRows * kFYDW + f * G::kCDW) - jalC;
-        L.rinfo[t][3] = 4 * (kFRows * kFYDW + G::kCRows * G::kCDW + i * G::kCDW) - jalC;
-        L.rinfo[t][4] = 4 * (kFRows * kFYDW + G::kCRows * G::kCDW + f * G::kCDW) - jalC;
+        L.rinfo[t][0] = 4 * (t * G::kYDW) - jalY;
+        L.rinfo[t][1] = 4 * (kFRows * G::kYDW + i * G::kCDW) - jalC;
+        L.rinfo[t][2] = 4 * (kFRows * G::kYDW + f * G::kCDW) - jalC;
+        L.rinfo[t][3] = 4 * (kFRows * G::kYDW + G::kCRows * G::kCDW + i * G::kCDW) - jalC;
+        L.rinfo[t][4] = 4 * (kFRows * G::kYDW + G::kCRows * G::kCDW + f * G::kCDW) - jalC;
       }
     };
     Step cur = plan_step(r_lo);
@@ -355,7 +360,7 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
         // items of one step row per wave (64 item slots per row, 128 when the tile needs more than 64
         // groups): a wave's chroma and luma reads then never straddle two rows, whose words met
         // bank conflicts, and its row is uniform
-        static_assert(kMaxSpan / 8 + 2 <= 128, "a row's items fit two waves");
+        static_assert(G::kSpan / 8 + 2 <= 128, "a row's items fit two waves");
         const int rsh = ng > 64 ? 7 : 6;
         for (int it = t; it < (nr << rsh); it += kFThreads) {
           const int q = __builtin_amdgcn_readfirstlane(it >> rsh);  // step row of the item
@@ -365,10 +370,10 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
           const int oY = L.rinfo[q][0], oBi = L.rinfo[q][1], oRi = L.rinfo[q][3];
           const uint32_t* sw = L.st;
           const uint8_t* sb = reinterpret_cast<const uint8_t*>(L.st);  // (byte offsets: rinfo's are bytes)
-          // the item's 8 luma bytes as one 8-byte read (oY + x is 8-aligned: kFYDW is even, xb and x are
+          // the item's 8 luma bytes as one 8-byte read (oY + x is 8-aligned: G::kYDW is even, xb and x are
           // multiples of 8): consecutive items 8 bytes apart fill all 64 banks, where two dword reads at
           // a 2-dword lane stride met 2-way bank conflicts
-          static_assert(kFYDW % 2 == 0, "8-byte aligned luma rows");
+          static_assert(G::kYDW % 2 == 0, "8-byte aligned luma rows");
           const uint2 yy = *reinterpret_cast<const uint2*>(sb + oY + x);
           const uint32_t y0 = yy.x, y1 = yy.y;
           uint32_t wr[2] = {0, 0}, wg[2] = {0, 0}, wb[2] = {0, 0};
@@ -502,12 +507,12 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
               wb[k >> 1] |= (uint32_t)(b0 | (b1 << 8)) << sh;
             }
           }
-          // one 8-byte store per channel (x - xb and kFRgbW are multiples of 8)
-          static_assert(kFRgbW % 8 == 0, "8-byte aligned RGB rows");
+          // one 8-byte store per channel (x - xb and G::kRgbW are multiples of 8)
+          static_assert(G::kRgbW % 8 == 0, "8-byte aligned RGB rows");
           uint2* o = reinterpret_cast<uint2*>(&L.rgb[q][0][x - xb]);
           o[0] = make_uint2(wr[0], wr[1]);
-          o[kFRgbW / 8] = make_uint2(wg[0], wg[1]);
-          o[kFRgbW / 4] = make_uint2(wb[0], wb[1]);
+          o[G::kRgbW / 8] = make_uint2(wg[0], wg[1]);
+          o[G::kRgbW / 4] = make_uint2(wb[0], wb[1]);
         }
         __syncthreads();
         if (kGlds && more) issue_lds(nxt);
@@ -520,11 +525,11 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
           // (unaligned sub-dword LDS reads are slow) and is realigned with v_alignbyte.
           const int r = ra + q;
           if (LAY == kRsGray) {
-            ring[(r & rmask) * rstride] = (uint32_t)htaps<KT>(hw + q * kFYDW, hsh, cf);
+            ring[(r & rmask) * rstride] = (uint32_t)htaps<KT>(hw + q * G::kYDW, hsh, cf);
           } else {
-            const int s0 = htaps<KT>(hw + q * 3 * (kFRgbW / 4), hsh, cf);
-            const int s1 = htaps<KT>(hw + (q * 3 + 1) * (kFRgbW / 4), hsh, cf);
-            const int s2 = htaps<KT>(hw + (q * 3 + 2) * (kFRgbW / 4), hsh, cf);
+            const int s0 = htaps<KT>(hw + q * 3 * (G::kRgbW / 4), hsh, cf);
+            const int s1 = htaps<KT>(hw + (q * 3 + 1) * (G::kRgbW / 4), hsh, cf);
+            const int s2 = htaps<KT>(hw + (q * 3 + 2) * (G::kRgbW / 4), hsh, cf);
             ring[(r & rmask) * rstride] = pack3(s0, s1, s2);
           }
           // V. output rows whose window ends at row r

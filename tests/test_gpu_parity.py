@@ -175,6 +175,29 @@ def test_4k_vs_oracle(engine):
     np.testing.assert_array_equal(got[0].cpu().numpy(), O.pipeline(jpg, (512, 512), flip=True))
 
 
+def test_fused_tile_span_edges_vs_oracle(engine):
+    """Bilinear scales at the 7-tap fused kernels' row bound (sds_amd/csrc/sdsj_common.h rs_span: 768
+    source columns; a 256-column tile at scale s spans 256 s + 2 s + 4): square crops of 755..768 rows
+    to 256 x 256 (tiles of 256 below 2.97, halved above), the 9-tap neighbour just past scale 3, and
+    every chroma layout."""
+    from PIL import Image
+    from tests.golden.synth import encode_jpeg, synth_rgb
+    rng = np.random.default_rng(77)
+    jpgs = []
+    for side, extra in ((755, 40), (760, 0), (765, 120), (768, 32), (771, 8)):
+        rgb = synth_rgb(rng, side + extra, side)
+        for sub in (2, 1, 0):
+            jpgs.append(encode_jpeg(rgb, 90, subsampling=sub))
+        jpgs.append(encode_jpeg(np.array(Image.fromarray(rgb).convert("L")), 90))
+    for res in ((256, 256), (256, 200)):
+        flip = [bool(v) for v in rng.integers(0, 2, len(jpgs))]
+        got, st = engine.decode_resize(jpgs, res, flip=flip)
+        assert (st == 0).all()
+        for k, j in enumerate(jpgs):
+            np.testing.assert_array_equal(got[k].cpu().numpy(), O.pipeline(j, res, flip=flip[k]),
+                                          err_msg=f"image {k} res {res}")
+
+
 @pytest.mark.parametrize("rst", [0, 3])
 def test_tile_parallel_unstuff_vs_oracle(engine, rst):
     """Images of more than kUsSerialTiles (64) 8 KiB tiles take the tile-parallel unstuff passes: noise
