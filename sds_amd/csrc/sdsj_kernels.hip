@@ -849,7 +849,13 @@ __device__ void us_finish(ImgDesc* d, const SegView& sv, int t, int64_t ulen, in
 }
 
 // Images of at most kUsSerialTiles tiles (route kRtUsSmall): one workgroup per image, tile after tile.
-__global__ void __launch_bounds__(kUnstuffThreads) k_us_serial(const uint8_t* __restrict__ blob,
+// 6 waves per SIMD (80 VGPRs, from 84 at the default 5): -2 % per launch (8: 64 VGPRs with spills, +6 %;
+// profiles/r05_ab.txt)
+#ifndef SDSJ_US_WAVES
+#define SDSJ_US_WAVES 6
+#endif
+#define SDSJ_US_OCC __attribute__((amdgpu_waves_per_eu(SDSJ_US_WAVES)))
+__global__ void __launch_bounds__(kUnstuffThreads) SDSJ_US_OCC k_us_serial(const uint8_t* __restrict__ blob,
                                                                const int64_t* __restrict__ offsets,
                                                                ImgDesc* __restrict__ descs, uint8_t* __restrict__ scratch,
                                                                const int32_t* __restrict__ routes, int cap) {

@@ -535,7 +535,10 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
           // V. output rows whose window ends at row r
           while (nvend <= r + 1) {
             const int vmin = nvmin, vcnt = nvend - nvmin;
-            const int32_t* wk = L.vw[nb - oy0];
+            // (the output row through readfirstlane: its weights and store bases stay scalar, not 64-bit
+            // pointers the vector unit re-derives for every row)
+            const int nbu = __builtin_amdgcn_readfirstlane(nb);
+            const int32_t* wk = L.vw[nbu - oy0];
             int32_t v0 = 1 << 21, v1 = 1 << 21, v2 = 1 << 21;
             if constexpr (kRing8) {
               // all taps unrolled (KT of them, or 8 when ksv > KT): their ring and weight reads issue
@@ -564,9 +567,9 @@ __device__ void rsf_image(int img, int strip, int tz0, int ntz, const ImgDesc* _
             }
             if (LAY == kRsGray) {
               const int c = rs_clip8(v0);
-              put3_row(out, om, lut, (int64_t)nb * ow, ox, c, c, c);
+              put3_row(out, om, lut, (int64_t)nbu * ow, ox, c, c, c);
             } else {
-              put3_row(out, om, lut, (int64_t)nb * ow, ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
+              put3_row(out, om, lut, (int64_t)nbu * ow, ox, rs_clip8(v0), rs_clip8(v1), rs_clip8(v2));
             }
             nb++;
             if (nb < oy1) window(nb, nvmin, nvend);
