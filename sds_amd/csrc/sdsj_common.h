@@ -80,7 +80,8 @@ constexpr int kRingMaxRows = 16;      // vertical windows longer than this use t
 #endif
 constexpr int kVTapsF = SDSJ_VTAPS_F;  // vertical taps the specialised fused kernels (k_rs420) stage; more: k_resample
 // k_rs420<KT> with KT <= 7 horizontal taps (downscales up to ~3x with bilinear) carry a smaller ring and
-// weight table (8 rows / 8 vertical taps: 6 KB less LDS, 5 workgroups per CU instead of 4); images whose
+// weight table (8 rows / 8 vertical taps: 6 KB less LDS, 5 workgroups per CU instead of 4; 6 with rs_span's
+// narrower rows below); images whose
 // vertical window needs more take k_resample
 SDSJ_HD constexpr int rs_ring_rows(int kt) { return kt <= 7 ? 8 : kRingMaxRows; }
 SDSJ_HD constexpr int rs_vtaps(int kt) { return kt <= 7 ? 8 : kVTapsF; }
