@@ -232,6 +232,97 @@ def cpu_share() -> tuple[int, str]:
     return host_cores(), "nproc (sched_getaffinity)"
 
 
+# ---------------------------------------------------------------- output verification
+def _pil_u8_sha(args) -> str:
+    """SHA-256 of the reference pipeline's uint8 CHW output for one JPEG (functional.py:94-110 op order,
+    no flip / normalise): the check of the engine's per-pool-image reference outputs."""
+    import hashlib
+    import io
+
+    from PIL import Image
+    jpg, res = args
+    img = Image.open(io.BytesIO(jpg)).convert("RGB")
+    w, h = img.size
+    if w > h:
+        left = (w - h) // 2
+        img = img.crop((left, 0, left + h, h))
+    else:
+        top = (h - w) // 2
+        img = img.crop((0, top, w, top + w))
+    if img.size != (res, res):
+        img = img.resize((res, res), Image.BILINEAR)
+    return hashlib.sha256(np.ascontiguousarray(np.asarray(img).transpose(2, 0, 1)).tobytes()).hexdigest()
+
+
+def verify_rows(eng, blob, d_offs, d_lens, out, status, flips, rows_ext, period, pool, nrows, B, res, mixed,
+                last_start, dev_step, cursor, workers) -> dict:
+    """Checks decoded rows on the device against per-pool-image references.
+
+    The references: each distinct pool image of the rank's period, decoded once by the engine (uint8 CHW,
+    no flip) and checked against PIL on the host by SHA-256 (_pil_u8_sha).  A row's expected output is
+    its pool image's reference, flipped where the row's flag says so and mapped through the normalise LUT
+    (``x.float() / 127.5 - 1`` per byte value, evaluated on the host) for configs[2].  Checked: every row of
+    the batch ``out`` holds (rows [last_start, last_start + B), the last timed batch) and then every resident
+    row of the rank -- ceil(nrows / B) batches from row 0 through ``dev_step``."""
+    import hashlib
+
+    import torch
+    P = len(period)
+    dev = out.device
+    ref = torch.empty((P, 3, res, res), dtype=torch.uint8, device=dev)
+    for a in range(0, P, B):  # (rows 0 .. P-1 hold the period's images in order)
+        b = min(P, a + B)
+        _, st = eng.decode_resize_device(blob, d_offs[a:b], d_lens[a:b], (res, res), out=ref[a:b])
+        if int((st != 0).sum().item()):
+            raise SystemExit("a pool image failed to decode in the reference pass")
+    torch.cuda.synchronize(dev)
+    ref_h = ref.cpu().numpy()
+    ref_sha = [hashlib.sha256(ref_h[k].tobytes()).hexdigest() for k in range(P)]
+    items = [(pool[p], res) for p in period]
+    pil_sha = [_pil_u8_sha(it) for it in items] if workers <= 1 or P < 32 else \
+        _pool_map(_pil_u8_sha, items, min(workers, 32), chunksize=8)
+    refs_ok = sum(int(a == b) for a, b in zip(ref_sha, pil_sha))
+    lut = (torch.arange(256, dtype=torch.float32) / 127.5 - 1.0).to(dev) if mixed else None
+    pidx = torch.from_numpy((rows_ext % P).astype(np.int64)).to(dev)
+
+    def check(start: int) -> int:
+        """rows of `out` (batch starting at row `start`) equal to their expected output"""
+        good = 0
+        ch = 512 if mixed else 8192
+        for a in range(0, B, ch):
+            b = min(B, a + ch)
+            exp = ref[pidx[start + a:start + b]]
+            if mixed:
+                f = flips[start + a:start + b].bool().view(-1, 1, 1, 1)
+                exp = lut[torch.where(f, exp.flip(-1), exp).long()]
+            eq = (out[a:b] == exp).flatten(1).all(1) & (status[a:b] == 0)
+            good += int(eq.sum().item())
+        return good
+
+    res_d = {"method": "per-row device compare with the row's pool-image reference (engine output, uint8, "
+                       "SHA-256-equal to PIL's on the host); configs[2] rows flipped per flag and mapped through "
+                       "the fp32 normalise LUT",
+             "pool_refs": P, "pool_refs_equal_to_pil": refs_ok}
+    ok = refs_ok == P
+    if last_start is not None:
+        g = check(last_start)
+        res_d.update(rows_checked=B, rows_equal=g, last_batch_first_row=int(last_start))
+        ok = ok and g == B
+    walk_batches = (nrows + B - 1) // B
+    cursor[0] = 0
+    wg = 0
+    for k in range(walk_batches):
+        s0 = cursor[0]
+        dev_step()
+        wg += check(s0)
+    res_d["walk"] = {"batches": walk_batches, "rows_checked": walk_batches * B, "rows_equal": wg,
+                     "covers_every_resident_row": walk_batches * B >= nrows}
+    ok = ok and wg == walk_batches * B
+    res_d["equal_to_pil"] = bool(ok)
+    res_d["_ref_sha"] = ref_sha
+    return res_d
+
+
 # ---------------------------------------------------------------- multi-rank launcher
 def _free_port() -> int:
     s = socket.socket()
@@ -316,6 +407,9 @@ def main():
     ap.add_argument("--roofline-steps", type=int, default=5, help="single-lane steps timed for the roofline")
     ap.add_argument("--profile-steps", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl", help="process group (nccl = RCCL)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="create the process group at world size 1 too, so that one GPU runs the collectives of the "
+                         "multi-GPU path (init with device_id, device all_reduce / all_gather over --backend)")
     ap.add_argument("--engine", choices=["hip", "stub"], default="hip", help="stub: CPU stand-in (launcher tests)")
     args = ap.parse_args()
     mixed = args.workload == "mixed512"
@@ -346,8 +440,11 @@ def main():
     # round-robin (torch.cuda.device_count() does not initialise the GPU)
     ndev = 0 if stub else torch.cuda.device_count()
     dev = torch.device("cpu") if stub else torch.device("cuda", local_rank % max(1, ndev))
-    if world > 1:
+    use_pg = world > 1 or args.force_pg
+    if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         if stub:
             dist.init_process_group(args.backend, rank=rank, world_size=world)
         else:
@@ -363,8 +460,13 @@ def main():
     from sds_amd.distributed import compute_index_slice, max_over_ranks
 
     def barrier():
-        if world > 1:
+        if use_pg:
             dist.barrier()
+
+    coll_dev = None if stub or args.backend == "gloo" else dev  # where the collectives' tensors live
+
+    def max_ranks(v: float) -> float:
+        return max_over_ranks(v, device=coll_dev, always=use_pg)
 
     workers = max(1, cpu_share()[0] // max(1, world))
     pool = make_pool(args.pool, workers, _make_mixed_image if mixed else _make_pool_image)
@@ -399,8 +501,9 @@ def main():
     else:
         r0, r1, _ = compute_index_slice(total_rows, rank, world)
     nrows = r1 - r0
+    B = args.batch
     slices = [[r0, r1]]
-    if world > 1:
+    if use_pg:
         slices = [None] * world
         dist.all_gather_object(slices, [r0, r1])
     period = [(r0 + k) % args.pool for k in range(min(args.pool, nrows))]
@@ -416,7 +519,9 @@ def main():
     reps = 1 if stub else (nrows + len(period) - 1) // len(period)
     d_tmpl = torch.from_numpy(template).to(dev)
     blob = d_tmpl.repeat(reps)
-    j = np.arange(nrows)
+    # every batch is a window of B consecutive rows, wrapping past the rank's last row to its first one (the
+    # timed steps walk all resident rows): the row arrays are extended by B rows taken from the start
+    j = np.arange(nrows + B) % nrows
     offs = (j // len(period)) % reps * T + t_offs[j % len(period)]
     lens = t_lens[j % len(period)]
     d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
@@ -424,32 +529,33 @@ def main():
     del d_tmpl
     sync()
 
-    B = args.batch
     if stub:
         eng = StubEngine()
     else:
         from sds_amd.engine import JpegEngine
-        # device scratch from host planning (sdsj_plan_need): the largest sum over any B consecutive
-        # rows (the rows repeat this rank's pool period, so every batch is such a window)
+        # device scratch from host planning (sdsj_plan_need): the largest sum over any window of B
+        # consecutive rows, wrap-around included (every batch is such a window)
         need_of = {p: JpegEngine.scratch_need([pool[p]], (args.res, args.res), normalize=mixed) for p in set(period)}
         cyc = np.array([need_of[p] for p in period], np.int64)
-        full, rem = divmod(B, len(cyc))
-        ext = np.concatenate([[0], np.cumsum(np.concatenate([cyc, cyc]))])
-        win = int(max(ext[k + rem] - ext[k] for k in range(len(cyc)))) if rem else 0
-        eng = JpegEngine(dev, max_batch=B, scratch_bytes=full * int(cyc.sum()) + win + (64 << 20))
+        row_need = cyc[j % len(period)]
+        cum = np.concatenate([[0], np.cumsum(row_need)])
+        win = int((cum[B:B + nrows] - cum[:nrows]).max())
+        eng = JpegEngine(dev, max_batch=B, scratch_bytes=win + (64 << 20))
     out = torch.empty((B, 3, args.res, args.res), dtype=torch.float32 if mixed else torch.uint8, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
-    # hflip flags for every row, seeded (the user HorizontalFlipTransform, p = 0.5)
-    flips = torch.from_numpy((np.random.default_rng(99 + rank).random(nrows) < 0.5).astype(np.uint8)).to(dev)
+    # hflip flags for every row, seeded (the user HorizontalFlipTransform, p = 0.5), extended like the rows
+    h_flips = (np.random.default_rng(99 + rank).random(nrows) < 0.5).astype(np.uint8)[j]
+    flips = torch.from_numpy(h_flips).to(dev)
     cursor = [0]
+    walked = {"rows": 0}  # rows decoded by dev_step since the last reset (the timed region's count)
 
     def dev_step():
+        # the batch = rows [s, s + B) of the rank, modulo nrows: consecutive steps walk every resident row
         s = cursor[0]
-        if s + B > nrows:
-            s = 0
         eng.decode_resize_device(blob, d_offs[s:s + B], d_lens[s:s + B], (args.res, args.res), out=out,
                                  status=status, normalize=mixed, flip=flips[s:s + B] if mixed else None)
-        cursor[0] = s + B
+        cursor[0] = (s + B) % nrows
+        walked["rows"] += B
 
     step = dev_step
     cache_dir = src_dir = None
@@ -501,6 +607,8 @@ def main():
         def e2e_step():
             schedule_ahead(pipe["taken"] + 2 * B)
             paths = [dst_of(key) for key, _ in islice(dl.yield_completed(), B)]
+            if len(paths) != B:  # a row whose copy failed every retry: fail the run, never count it
+                raise SystemExit(f"rank {rank}: the downloader delivered {len(paths)} of {B} rows")
             pipe["taken"] += B
             slot = pipe["k"] % 2
             torch.cuda.current_stream(dev).wait_stream(d2h)  # slot's previous output has left for the host
@@ -517,8 +625,7 @@ def main():
                 e2e_step()
             complete_prev()
             sync()
-            return B * nsteps * world / max_over_ranks(time.perf_counter() - t,
-                                                       device=None if stub or args.backend == "gloo" else dev)
+            return B * nsteps * world / max_ranks(time.perf_counter() - t)
 
         # correctness gate on the device-resident rows first (the engine's first call)
         dev_step()
@@ -548,18 +655,20 @@ def main():
 
     barrier()
     sync()
+    walked["rows"] = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     sync()
     t1 = time.perf_counter()
+    rows_timed = walked["rows"]
+    last_start = (cursor[0] - B) % nrows  # the rows `out` holds: the last timed batch (device-resident path)
     barrier()
     if e2e:  # every batch completed in the pipeline decoded completely; the last one is drained here
         complete_prev()
         sync()
         n_bad = pipe["bad"]
-        dl_rates["warm"] = round(B * args.steps * world / max_over_ranks(t1 - t0, device=None if stub or args.backend ==
-                                                                         "gloo" else dev), 1)
+        dl_rates["warm"] = round(B * args.steps * world / max_ranks(t1 - t0), 1)
         dl.shutdown()
         shutil.rmtree(cache_dir, ignore_errors=True)
         shutil.rmtree(src_dir, ignore_errors=True)
@@ -568,14 +677,15 @@ def main():
     if n_bad:
         raise SystemExit(f"rank {rank}: {n_bad} samples of the last timed batch failed to decode")
     my_elapsed = t1 - t0
-    elapsed = max_over_ranks(my_elapsed, device=None if stub or args.backend == "gloo" else dev)
+    elapsed = max_ranks(my_elapsed)
     per_rank = [my_elapsed]
-    if world > 1:
-        tl = [torch.zeros(1, dtype=torch.float64, device=dev if args.backend == "nccl" and not stub else "cpu")
-              for _ in range(world)]
+    gather_dev = None
+    if use_pg:
+        tl = [torch.zeros(1, dtype=torch.float64, device=coll_dev or "cpu") for _ in range(world)]
         dist.all_gather(tl, torch.tensor([my_elapsed], dtype=torch.float64, device=tl[0].device))
         per_rank = [float(x.item()) for x in tl]
         world_seen = dist.get_world_size()
+        gather_dev = str(tl[0].device)
     else:
         world_seen = 1
     imgs = B * args.steps * world
@@ -591,28 +701,27 @@ def main():
         for _ in range(args.steps):
             step()
         sync()
-        dev_value = B * args.steps * world / max_over_ranks(time.perf_counter() - t0,
-                                                            device=None if stub or args.backend == "gloo" else dev)
+        dev_value = B * args.steps * world / max_ranks(time.perf_counter() - t0)
 
-    # pixel check after timing: the batch holding pool image 0 at its start row, against PIL (the
-    # reference's arithmetic) -- and for configs[1] also the reference-generated golden digest
+    # pixel check after timing (device-resident path): every row of the last timed batch, then every resident
+    # row of the rank (ceil(nrows / B) more batches from row 0), each compared on the device with the output
+    # of its pool image -- decoded once by the engine and checked against PIL (the reference's arithmetic)
+    # on the host -- plus, for configs[1], pool image 0 against the reference-generated golden digest
     pixel_check = None
     if not stub:
-        k0 = (-r0) % args.pool
-        cursor[0] = 0
-        step()
-        sync()
-        got = out[k0].cpu()
-        fl = bool(flips[k0].item()) if mixed else False
-        ref = _pil_pipeline(pool[0], args.res, flip=fl, normalize=mixed)
-        ok = int(status[k0].item()) == 0 and torch.equal(got, ref.contiguous())
-        pixel_check = {"row": r0 + k0, "pool_image": 0, "equal_to_pil": bool(ok)}
-        if not mixed and args.res == 256:  # (the golden digests are of the 256x256 output)
+        pixel_check = verify_rows(eng, blob, d_offs, d_lens, out, status, flips, j, period, pool, nrows, B,
+                                  args.res, mixed, None if e2e else last_start, dev_step, cursor, cpu_share()[0])
+        pixel_check.update(rows_decoded_in_timed_region=rows_timed if not e2e else None,
+                           distinct_rows_in_timed_region=min(nrows, rows_timed) if not e2e else None,
+                           resident_rows=nrows)
+        k0 = next((k for k, p in enumerate(period) if p == 0), None)
+        if not mixed and args.res == 256 and k0 is not None:  # (the golden digests are of the 256x256 output)
             from tests import goldens as G
             meta = G.load_json("g2_synth.json")
             if meta.get("seed") == 1234 and (meta.get("w"), meta.get("h"), meta.get("quality")) == (640, 480, 90):
-                pixel_check["golden_sha256_match"] = G.sha(got.numpy()) == meta["images"][0]["u8_256_sha256"]
-        if not ok or not pixel_check.get("golden_sha256_match", True):
+                pixel_check["golden_sha256_match"] = pixel_check.pop("_ref_sha")[k0] == meta["images"][0]["u8_256_sha256"]
+        pixel_check.pop("_ref_sha", None)
+        if not pixel_check["equal_to_pil"] or not pixel_check.get("golden_sha256_match", True):
             raise SystemExit(f"rank {rank}: pixel check failed: {pixel_check}")
 
     # roofline: every kernel timed alone in a single-lane pass (one dispatch per kernel per batch)
@@ -696,8 +805,9 @@ def main():
                                            "in-memory index (pyarrow not importable)",
                                  "slices": slices}},
             "per_rank_images_per_s": [round(B * args.steps / t, 1) for t in per_rank],
-            "process_group": {"backend": args.backend if world > 1 else None, "world_size": world_seen,
-                              "gpus_visible": ndev if not stub else 0},
+            "process_group": {"backend": dist.get_backend() if use_pg else None, "world_size": world_seen,
+                              "gpus_visible": ndev if not stub else 0, "forced_at_world_size_1": bool(args.force_pg),
+                              "all_gather_device": gather_dev},
             # bound: of the schema's roofs (HBM, MFMA) the path can only be priced against HBM -- it issues
             # no MFMA; `limiter` says from the counters which roof (HBM bytes or VALU issue) it is nearest
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -720,7 +830,7 @@ def main():
             line["downloader"] = dl_rates
             line["roofline"]["note"] = "device-resident kernels of the same rows (the PCIe legs are not kernels)"
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_pg:
         dist.barrier()
         dist.destroy_process_group()
     if index_path and rank == 0:

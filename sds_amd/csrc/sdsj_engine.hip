@@ -56,13 +56,18 @@ struct sdsj_engine {
   int32_t* d_routes_x = nullptr;
   hipStream_t aux[kMaxLanes - 1] = {};
   hipEvent_t ev_mid[kMaxLanes - 1] = {}, ev_join[kMaxLanes - 1] = {};
-  // route hint of the device path (sdsj_kernels.h route_grid): each call copies its lanes' route counts
-  // to pinned memory after k_plan; a later call folds a finished copy into the hint
-  uint64_t hint = kAllRoutes;
+  // route hints of the device path (sdsj_kernels.h route_grid), one per op (the resample route -- taps,
+  // layout -- follows the output size, filter, dtype and layout): each call copies its lanes' route counts
+  // to pinned memory after k_plan; a later call folds a finished copy into the hint of the op it ran
+  static constexpr int kHintSlots = 4;
+  uint64_t hint_key[kHintSlots] = {};
+  uint64_t hint[kHintSlots] = {};
+  int hint_n = 0, hint_next = 0;
   int32_t* h_rcounts = nullptr;  // [kMaxLanes][kNumRoutes]
   hipEvent_t ev_rc[kMaxLanes] = {};
   bool rc_pending = false;
   int rc_lanes = 0;
+  uint64_t rc_key = 0;  // the op of the outstanding readback
   // frames path: host-planned descriptors and route list, staged through pinned memory
   ImgDesc* h_fdescs = nullptr;
   int32_t* h_froutes = nullptr;
@@ -257,6 +262,29 @@ int run_lane(sdsj_engine* e, const Lane& ln, int n, bool small, const uint8_t* d
 // single lane.
 constexpr int kLaneMin = 128;
 
+uint64_t op_key(const sdsj_op& op) {
+  return (uint64_t)(uint32_t)op.out_h | (uint64_t)(uint32_t)op.out_w << 16 | (uint64_t)(op.crop_before_resize != 0) << 32 |
+         (uint64_t)(op.filter & 0xff) << 33 | (uint64_t)(op.out_dtype & 0xf) << 41 | (uint64_t)(op.layout & 0xf) << 45 |
+         1ull << 63;  // (never 0: an empty slot's key)
+}
+
+uint64_t hint_lookup(const sdsj_engine* e, uint64_t key) {
+  for (int k = 0; k < e->hint_n; k++)
+    if (e->hint_key[k] == key) return e->hint[k];
+  return kAllRoutes;
+}
+
+void hint_store(sdsj_engine* e, uint64_t key, uint64_t h) {
+  for (int k = 0; k < e->hint_n; k++)
+    if (e->hint_key[k] == key) {
+      e->hint[k] = h;
+      return;
+    }
+  int k = e->hint_n < sdsj_engine::kHintSlots ? e->hint_n++ : (e->hint_next++ % sdsj_engine::kHintSlots);
+  e->hint_key[k] = key;
+  e->hint[k] = h;
+}
+
 // rm: the routes the chunk's images may take (host planning), or kAllRoutes; small: the chunk was
 // host-planned in latency mode (host paths, n <= kSmallBatch)
 int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, int64_t blob_bytes, const int64_t* d_offsets, const int32_t* d_lengths,
@@ -265,35 +293,49 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, int64_t blob_bytes, 
   int nl = std::min(std::max(e->lanes, 1), kMaxLanes);
   while (nl > 1 && n < nl * kLaneMin) nl--;
   // route hint: the host paths know their routes exactly (rm); the device path uses the routes that held
-  // images in the last batch whose counts have come back (all routes until one has), and requests a
-  // new readback when none is outstanding
+  // images in the last batch of the same op whose counts have come back (all routes until one has, or
+  // when the op changed: another output size selects other resample routes), and requests a new
+  // readback when none is outstanding
   uint64_t hint = rm;
   bool readback = false;
+  const uint64_t key = op_key(op);
   if (rm == kAllRoutes) {
     if (e->rc_pending) {
-      bool done = true;
-      for (int k = 0; k < e->rc_lanes; k++) done = done && hipEventQuery(e->ev_rc[k]) == hipSuccess;
-      if (done) {
+      bool done = true, lost = false;
+      for (int k = 0; k < e->rc_lanes; k++) {
+        const hipError_t q = hipEventQuery(e->ev_rc[k]);
+        if (q == hipErrorNotReady) done = false;
+        else if (q != hipSuccess) lost = true;
+      }
+      if (lost) {  // a failed query: drop this readback rather than wait on it forever
+        (void)hipGetLastError();
+        e->rc_pending = false;
+      } else if (done) {
         uint64_t h = 0;
         for (int k = 0; k < e->rc_lanes; k++)
           for (int r = 0; r < kNumRoutes; r++)
             if (e->h_rcounts[k * kNumRoutes + r] > 0) h |= 1ull << r;
         if (h & (1ull << kRtEnt11M)) h |= 1ull << kRtEnt11G;
-        e->hint = h;
+        hint_store(e, e->rc_key, h);
         e->rc_pending = false;
       }
     }
-    hint = e->hint;
+    hint = hint_lookup(e, key);
     readback = !e->rc_pending;
-    if (readback) {
-      e->rc_pending = true;
-      e->rc_lanes = nl;
-    }
   }
   const Lane first{e->descs, e->tables, e->d_etab, e->d_routes, e->d_total, nullptr};
-  if (nl == 1)
-    return run_lane(e, first, n, small, d_blob, blob_bytes, d_offsets, d_lengths, op, d_flip, d_out, d_status, s, nullptr,
-                    rm, hint, readback ? 0 : -1);
+  auto readback_queued = [&](int lanes) {  // every lane recorded its ev_rc: the next call may fold them
+    if (!readback) return;
+    e->rc_pending = true;
+    e->rc_lanes = lanes;
+    e->rc_key = key;
+  };
+  if (nl == 1) {
+    const int st = run_lane(e, first, n, small, d_blob, blob_bytes, d_offsets, d_lengths, op, d_flip, d_out, d_status, s,
+                            nullptr, rm, hint, readback ? 0 : -1);
+    if (st == SDSJ_OK) readback_queued(1);
+    return st;
+  }
   for (int k = 0; k + 1 < nl; k++)
     if (!e->aux[k]) {
       SDSJ_HIP(e, hipStreamCreateWithFlags(&e->aux[k], hipStreamNonBlocking));
@@ -316,6 +358,7 @@ int run_chunk(sdsj_engine* e, int n, const uint8_t* d_blob, int64_t blob_bytes, 
                       k + 1 < nl ? e->ev_mid[k] : nullptr, rm, hint, readback ? k : -1);
     if (st != SDSJ_OK) return st;
   }
+  readback_queued(nl);
   for (int k = 0; k + 1 < nl; k++) {
     SDSJ_HIP(e, hipEventRecord(e->ev_join[k], e->aux[k]));
     SDSJ_HIP(e, hipStreamWaitEvent(s, e->ev_join[k], 0));

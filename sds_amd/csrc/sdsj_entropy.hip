@@ -1394,9 +1394,12 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       p0 = S.dc_ex[0];
       p1 = S.dc_ex[1];
       p2 = S.dc_ex[2];
-      // entries are block boundaries (z = 0): the speculative and the sync passes stop only there
+      // entries are block boundaries (z = 0): the speculative and the sync passes stop only there.  The
+      // pass relies on that invariant (z starts at 0, no mid-block entry state); an entry that breaks it
+      // fails the image (CORRUPT) instead of writing wrong coefficients
       blk = S.entry_bz >> 8;
       z = 0;
+      if (S.entry_bz & 0xFF) d->status = SDSJ_CORRUPT;
       c = ctx_c(K, blk);
       if constexpr (LB == 11) {
         // predictors in component order from the entry block's component: pc = its own, p0 / p1 the
@@ -1426,7 +1429,8 @@ __device__ void entwrite_image(int img, int grp, ImgDesc* __restrict__ descs, co
       bits_init(b, src, S.entry_p, S.lim_bit);
       // the interval's last subsequence decodes every remaining block; when its data runs out
       // (bits past lim, read as zeros) it finishes that MCU and stops: jdhuff.c insufficient_data
-      run = g < gend && (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
+      run = g < gend && (S.entry_bz & 0xFF) == 0 &&
+            (last_of_seg ? !(z == 0 && blk == 0 && b.pos > lim) : (b.pos < end_bit || z != 0));
       // one stop rule for both kinds: at a block boundary (z = 0) whose MCU position blk is in stop_blk
       // (the interval's last subsequence: MCU boundaries only) once pos >= stop_pos
       stop_pos = last_of_seg ? lim + 1 : end_bit;

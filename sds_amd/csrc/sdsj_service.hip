@@ -74,18 +74,25 @@ struct Client {
   std::atomic<bool> closed{false};
   std::mutex mu;  // base / size / unmap
 
-  void reply(uint64_t seq, int status) {
+  // max_wait_ms bounds the wait for a full socket buffer: a client that stops reading its replies while
+  // still connected is dropped (closed) after that long in total instead of blocking the caller -- an
+  // engine thread (kReplyWaitMs), or the epoll thread that serves every client (kEpollReplyWaitMs).
+  static constexpr int kReplyWaitMs = 10000, kEpollReplyWaitMs = 20;
+  void reply(uint64_t seq, int status, int max_wait_ms = kReplyWaitMs) {
     if (closed.load()) return;
     sdsj_svc_rep rep{seq, status, 0};
+    const double deadline = now_us() + 1e3 * max_wait_ms;
     for (;;) {  // (SOCK_SEQPACKET: a packet is sent whole; concurrent senders do not interleave)
       const ssize_t w = send(fd, &rep, sizeof(rep), MSG_NOSIGNAL);
       if (w == (ssize_t)sizeof(rep)) return;
       if (w < 0 && errno == EINTR) continue;
       if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {  // socket buffer full: wait until writable
+        const int left_ms = (int)((deadline - now_us()) / 1e3);
         pollfd p{fd, POLLOUT, 0};
-        if (poll(&p, 1, 1000) >= 0 && !(p.revents & (POLLERR | POLLHUP | POLLNVAL))) continue;
+        if (left_ms > 0 && poll(&p, 1, std::min(left_ms, 1000)) >= 0 && !(p.revents & (POLLERR | POLLHUP | POLLNVAL)))
+          continue;
       }
-      closed.store(true);  // the worker went away (EPIPE, ECONNRESET, ...): its later requests are dropped
+      closed.store(true);  // the worker went away (EPIPE, ECONNRESET, ...) or stopped reading: later requests are dropped
       return;
     }
   }
@@ -275,13 +282,13 @@ class Service {
           }
         }
         if (passed >= 0) close(passed);
-        c->reply(r.seq, st);
+        c->reply(r.seq, st, Client::kEpollReplyWaitMs);
       } else if (r.kind == SDSJ_SVC_DECODE || r.kind == SDSJ_SVC_FRAME) {
         const bool frame = r.kind == SDSJ_SVC_FRAME;
         const int64_t in = frame ? (int64_t)r.width * r.height * 3 : r.in_len;
         if (!c->region_ok(0, in) || !c->region_ok(r.out_off, out_bytes(r.op)) || r.op.out_h <= 0 || r.op.out_w <= 0 ||
             (frame && (r.width <= 0 || r.height <= 0 || r.in_len < in))) {
-          c->reply(r.seq, SDSJ_EINVAL);
+          c->reply(r.seq, SDSJ_EINVAL, Client::kEpollReplyWaitMs);
           continue;
         }
         c->inflight++;
@@ -289,7 +296,7 @@ class Service {
         pending_.push_back(Req{c, r});
         queued++;
       } else {
-        c->reply(r.seq, SDSJ_EINVAL);
+        c->reply(r.seq, SDSJ_EINVAL, Client::kEpollReplyWaitMs);
       }
     }
     // one request wakes one idle engine thread (waking them all cost each request a herd of wake-ups

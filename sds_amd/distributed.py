@@ -23,11 +23,12 @@ def env_rank() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
-def max_over_ranks(value: float, device=None) -> float:
-    """Maximum of a per-rank scalar (the bench's timed region), via all_reduce(MAX)."""
+def max_over_ranks(value: float, device=None, always: bool = False) -> float:
+    """Maximum of a per-rank scalar (the bench's timed region), via all_reduce(MAX).  ``always``: run the
+    collective at world size 1 too (a process group created only to exercise its backend)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()) or (dist.get_world_size() == 1 and not always):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -350,6 +350,73 @@ class GpuResizeVideoTransform(BaseTransform):
         return sample
 
 
+class GpuUndistortFramesTransform(BaseTransform):
+    """UndistortFramesTransform (presets.py:164-188) on the GPU frame path.
+
+    When the sample's original resolution (``original_resolution_fields`` = (height field, width field))
+    and the frames' aspect ratios differ by more than 0.02, the frames are resized to
+    ``(round(cur_w / orig_ar), cur_w)`` by lean_resize_frames with its defaults (centre crop, Pillow
+    bilinear, functional.py:42-86) -- a uint8-rounded resize of its own, ahead of the video resize (the
+    reference rounds between the two, so the two passes are not fused).  ``sample[output_field]`` then
+    holds the undistorted frames as a device uint8 [T, H', W, 3] tensor, which GpuResizeVideoTransform
+    takes as its input.  Otherwise (no original resolution, or aspect ratios within the tolerance) the
+    sample is returned untouched, as in the reference -- ``output_field`` is then not written either.
+
+    Frames are what the reference reads ``.size`` from: PIL images (PyAV's ``to_image``); HWC uint8
+    arrays and a uint8 [T, H, W, 3] tensor are accepted as well."""
+
+    def __init__(self, input_field: str, original_resolution_fields: tuple, output_field: Optional[str] = None,
+                 device=None):
+        super().__init__(input_field, output_field)
+        self.original_resolution_fields = tuple(original_resolution_fields)
+        self.device = device
+
+    @staticmethod
+    def _frame_size(frames) -> tuple[int, int]:
+        """(width, height) of the first frame, as the reference's ``frames[0].size``."""
+        if isinstance(frames, torch.Tensor):
+            return int(frames.shape[2]), int(frames.shape[1])
+        f = frames[0]
+        if hasattr(f, "size") and isinstance(f.size, tuple):
+            return f.size
+        a = np.asarray(f)
+        return int(a.shape[1]), int(a.shape[0])
+
+    @staticmethod
+    def target(orig_height, orig_width, cur_width: int, cur_height: int) -> Optional[tuple[int, int]]:
+        """presets.py:178-186: the (height, width) the frames are resized to, or None to leave them."""
+        if orig_height is None or orig_width is None:
+            return None  # no original resolution: skip undistortion
+        assert isinstance(orig_height, (int, float)) and isinstance(orig_width, (int, float)), \
+            f"Original resolution fields must be numeric, got {type(orig_height)} and {type(orig_width)}."
+        orig_aspect_ratio = orig_width / orig_height
+        cur_aspect_ratio = cur_width / cur_height
+        if abs(orig_aspect_ratio - cur_aspect_ratio) > 0.02:  # the reference's tolerance
+            return round(cur_width / orig_aspect_ratio), cur_width
+        return None
+
+    def __call__(self, sample: SampleData) -> SampleData:
+        orig_h = sample.get(self.original_resolution_fields[0])
+        orig_w = sample.get(self.original_resolution_fields[1])
+        if orig_h is None or orig_w is None:
+            return sample
+        w, h = self._frame_size(sample[self.input_field])
+        res = self.target(orig_h, orig_w, w, h)
+        if res is None:
+            return sample
+        eng = get_engine(self.device)
+        frames = _frames_to_device(sample[self.input_field], torch.device("cuda", eng.device))
+        if res == (h, w):  # lean_resize_frames's same-size shortcut (functional.py:78-80): the frames as they are
+            sample[self.output_field] = frames
+            return sample
+        out, status = eng.resize_frames(frames, res, crop_before_resize=True, filter="bilinear", layout="hwc")
+        bad = torch.nonzero(status != 0)
+        if bad.numel():
+            raise_for_status(int(status[int(bad[0])]), int(bad[0]))
+        sample[self.output_field] = out
+        return sample
+
+
 class ReshapeImageAsVideoTransform(BaseTransform):
     """presets.py:60-66 -> functional.py:88-92."""
 
