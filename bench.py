@@ -604,18 +604,31 @@ def main():
                 hosts[prev].copy_(o, non_blocking=True)
             pipe["prev"] = None
 
+        # host wall time per phase of the step (seconds, summed; reset with the timed region): scheduling the
+        # downloads ahead, taking the batch's completed rows from the downloader, engine.submit (file reads
+        # into the pinned slot, host planning, H2D + decode launches), completing the previous batch (its
+        # wait, the D2H issue)
+        ph = {"schedule": 0.0, "handoff": 0.0, "submit": 0.0, "complete": 0.0}
+
         def e2e_step():
+            t0 = time.perf_counter()
             schedule_ahead(pipe["taken"] + 2 * B)
+            t1 = time.perf_counter()
             paths = [dst_of(key) for key, _ in islice(dl.yield_completed(), B)]
             if len(paths) != B:  # a row whose copy failed every retry: fail the run, never count it
                 raise SystemExit(f"rank {rank}: the downloader delivered {len(paths)} of {B} rows")
+            t2 = time.perf_counter()
             pipe["taken"] += B
             slot = pipe["k"] % 2
             torch.cuda.current_stream(dev).wait_stream(d2h)  # slot's previous output has left for the host
             eng.submit(slot, paths, (args.res, args.res), files=True, out=outs[slot])
+            t3 = time.perf_counter()
             if pipe["prev"] is not None:
                 complete_prev()
+            t4 = time.perf_counter()
             pipe["prev"], pipe["k"] = slot, pipe["k"] + 1
+            for k, a, b in (("schedule", t0, t1), ("handoff", t1, t2), ("submit", t2, t3), ("complete", t3, t4)):
+                ph[k] += b - a
 
         def e2e_epoch_rate(nsteps):
             barrier()
@@ -656,6 +669,9 @@ def main():
     barrier()
     sync()
     walked["rows"] = 0
+    if e2e:
+        for k in ph:
+            ph[k] = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -828,6 +844,8 @@ def main():
             line["device_resident_value"] = round(dev_value, 1)
             line["e2e_over_device_resident"] = round(value / dev_value, 4)
             line["downloader"] = dl_rates
+            line["e2e_host_ms_per_step"] = {k: round(v / args.steps * 1e3, 3) for k, v in ph.items()}
+            line["e2e_host_ms_per_step"]["step"] = round(elapsed / args.steps * 1e3, 3)
             line["roofline"]["note"] = "device-resident kernels of the same rows (the PCIe legs are not kernels)"
         print(json.dumps(line), flush=True)
     if use_pg:

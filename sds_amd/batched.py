@@ -14,6 +14,14 @@ on the training process's GPU:
     for batch in decode.stream(loader):   # the same, batch k + 1 staged and copied while k decodes
         ...
 
+torch's default collate leaves ``bytes`` fields as a list of B ``bytes``, which a DataLoader pickles
+through its result queue (a pipe), and the consumer copies each again.  ``collate_encoded``
+packs the image field into an ``EncodedBatch`` instead (one shared-memory uint8 tensor of the samples'
+bytes back to back + offsets / lengths), which crosses to the training process as a file descriptor,
+and the engine stages it from there:
+
+    loader = DataLoader(ds, batch_size=B, num_workers=W, collate_fn=collate_encoded("jpg"))
+
 torch's default collate leaves ``bytes`` fields as a list, so ``batch[image_field]`` arrives as the
 B encoded images.  Values equal the per-sample pipeline's (presets.py:716-744) stacked the way
 default_collate stacks them.  Samples the JPEG kernels do not decode (other formats, CMYK / arithmetic
@@ -30,7 +38,7 @@ import torch
 
 from . import _lib
 from . import functional as F
-from .engine import ImageDecodeError, UnsupportedImageError, get_engine, raise_for_status
+from .engine import EncodedBatch, ImageDecodeError, UnsupportedImageError, get_engine, raise_for_status
 from .presets import LoadFromDiskTransform, SampleTransform, _frames_to_device, pil_decode
 
 
@@ -41,8 +49,30 @@ def create_deferred_image_pipeline(image_field: str) -> Sequence[SampleTransform
     return [LoadFromDiskTransform([image_field])]
 
 
+class collate_encoded:
+    """A DataLoader ``collate_fn`` for the batched consumer: ``image_field`` (the encoded bytes that
+    create_deferred_image_pipeline leaves) becomes an ``EncodedBatch`` -- in shared memory when collated in
+    a worker, as default_collate allocates its tensors there --, every other field goes through
+    ``collate_fn`` (default_collate).  Picklable, so spawn-started workers can run it."""
+
+    def __init__(self, image_field: str, collate_fn=None):
+        self.image_field = image_field
+        self.collate_fn = collate_fn
+
+    def __call__(self, samples: Sequence[dict]) -> dict:
+        from torch.utils.data import default_collate, get_worker_info
+        rest = [{k: v for k, v in s.items() if k != self.image_field} for s in samples]
+        out = (self.collate_fn or default_collate)(rest)
+        enc = EncodedBatch.pack([s[self.image_field] for s in samples], shared=get_worker_info() is not None)
+        # (the image field keeps its place among the sample's keys)
+        keys = list(samples[0].keys()) if samples else []
+        return {k: (enc if k == self.image_field else out[k]) for k in keys}
+
+
 def _select(value: Any, keep: list[int], n: int) -> Any:
     """The kept rows of one collated field (tensors along dim 0, lists/tuples by index)."""
+    if isinstance(value, EncodedBatch) and len(value) == n:
+        return value.select(keep)
     if isinstance(value, torch.Tensor) and value.ndim > 0 and value.shape[0] == n:
         return value[torch.as_tensor(keep, dtype=torch.long, device=value.device)]
     if isinstance(value, list) and len(value) == n:
@@ -95,7 +125,8 @@ class GpuDecodeBatch:
         encoded = batch[self.image_field]
         if isinstance(encoded, (bytes, bytearray, memoryview)):
             encoded = [encoded]
-        encoded = [bytes(e) for e in encoded]
+        if not isinstance(encoded, EncodedBatch):  # (an EncodedBatch goes to the engine as it is)
+            encoded = [bytes(e) for e in encoded]
         flip = [bool(torch.rand(1) < self.hflip_prob) for _ in encoded] if self.hflip_prob > 0.0 else None
         return encoded, flip
 
@@ -188,4 +219,5 @@ class GpuDecodeBatch:
         return batch
 
 
-__all__ = ["GpuDecodeBatch", "create_deferred_image_pipeline", "ImageDecodeError", "UnsupportedImageError"]
+__all__ = ["GpuDecodeBatch", "create_deferred_image_pipeline", "collate_encoded", "EncodedBatch", "ImageDecodeError",
+           "UnsupportedImageError"]

@@ -44,6 +44,81 @@ def raise_for_status(status: int, index: int = 0) -> None:
     raise ImageDecodeError(status, index)
 
 
+class EncodedBatch:
+    """A batch of encoded samples packed back to back in one host uint8 tensor (``data``), with int64
+    ``offsets`` / ``lengths`` per sample -- the transport of the batched consumer (sds_amd/batched.py
+    ``collate_encoded``).  Built in a DataLoader worker, ``data`` lives in shared memory, so the batch
+    crosses to the training process as a file descriptor instead of B pickled ``bytes`` objects, and the
+    engine stages it straight from there (no per-sample copies in Python).  Indexing gives one sample's
+    bytes (the PIL fallback's input); ``len`` is the sample count."""
+
+    __slots__ = ("data", "offsets", "lengths")
+
+    def __init__(self, data: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor):
+        if data.dtype != torch.uint8 or data.device.type != "cpu" or not data.is_contiguous() or data.dim() != 1:
+            raise ValueError("data must be a contiguous 1-D uint8 CPU tensor")
+        if offsets.shape != lengths.shape or offsets.dim() != 1:
+            raise ValueError("offsets and lengths must be 1-D tensors of one entry per sample")
+        off, ln = offsets.numpy(), lengths.numpy()
+        if len(off) and (off.min() < 0 or ln.min() < 0 or (off + ln).max() > data.numel()):
+            raise ValueError("a sample lies outside data")
+        self.data, self.offsets, self.lengths = data, offsets, lengths
+
+    @staticmethod
+    def pack(samples: Sequence, shared: bool = False) -> "EncodedBatch":
+        """Packs encoded samples (bytes-like); ``shared``: allocate ``data`` in shared memory (what a
+        DataLoader worker sends without a copy, as default_collate does for tensors)."""
+        lens = np.fromiter((len(s) for s in samples), dtype=np.int64, count=len(samples))
+        offs = np.zeros(len(samples), np.int64)
+        if len(samples) > 1:
+            np.cumsum(lens[:-1], out=offs[1:])
+        total = int(lens.sum())
+        if shared:
+            storage = torch.empty(0, dtype=torch.uint8)._typed_storage()._new_shared(max(total, 1), device="cpu")
+            data = torch.empty(0, dtype=torch.uint8).new(storage)[:total]
+        else:
+            data = torch.empty(total, dtype=torch.uint8)
+        buf = data.numpy()
+        for s, o, n in zip(samples, offs, lens):
+            buf[o:o + n] = np.frombuffer(s, dtype=np.uint8)
+        return EncodedBatch(data, torch.from_numpy(offs), torch.from_numpy(lens))
+
+    def __len__(self) -> int:
+        return int(self.offsets.numel())
+
+    def __getitem__(self, i: int) -> bytes:
+        o, n = int(self.offsets[i]), int(self.lengths[i])
+        return self.data.numpy()[o:o + n].tobytes()
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+    def select(self, keep: Sequence[int]) -> "EncodedBatch":
+        """The kept samples (views into the same ``data``)."""
+        k = torch.as_tensor(list(keep), dtype=torch.long)
+        return EncodedBatch(self.data, self.offsets[k], self.lengths[k])
+
+    def pointers(self):
+        """(uint64 sample addresses, uint64 lengths) for the C-ABI's pointer / length arrays; valid while
+        ``data`` lives."""
+        return (np.uint64(self.data.data_ptr()) + self.offsets.numpy().astype(np.uint64),
+                self.lengths.numpy().astype(np.uint64))
+
+
+def _c_samples(samples):
+    """The C-ABI's (const uint8_t* const* jpg, const size_t* len) for a list of bytes or an EncodedBatch;
+    the third value keeps the arrays alive."""
+    n = len(samples)
+    if isinstance(samples, EncodedBatch):
+        ptr, ln = samples.pointers()
+        ptr, ln = np.ascontiguousarray(ptr), np.ascontiguousarray(ln)
+        return (ctypes.cast(ptr.ctypes.data, ctypes.POINTER(ctypes.c_char_p)),
+                ctypes.cast(ln.ctypes.data, ctypes.POINTER(ctypes.c_size_t)), (ptr, ln, samples))
+    ptrs = (ctypes.c_char_p * max(n, 1))(*samples)
+    lens = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in samples])
+    return ptrs, lens, None
+
+
 def _device_index(device) -> int:
     if device is None:
         return torch.cuda.current_device()
@@ -132,7 +207,8 @@ class JpegEngine:
     def decode_resize(self, jpgs: Sequence[bytes], resolution, *, crop_before_resize: bool = True,
                       filter: str = "bilinear", normalize: bool = False, flip: Optional[Sequence[bool]] = None,
                       layout: str = "chw", out: Optional[torch.Tensor] = None) -> tuple[torch.Tensor, np.ndarray]:
-        """Decodes host JPEG bytes into a [n, 3, H, W] (or [n, H, W, 3]) device tensor.
+        """Decodes host JPEG bytes (a list of bytes, or an EncodedBatch) into a [n, 3, H, W] (or
+        [n, H, W, 3]) device tensor.
 
         Returns (tensor, per-sample status array).  Failed samples are zero-filled; use
         ``raise_for_status`` to turn a status into the reference's OSError semantics.
@@ -148,8 +224,7 @@ class JpegEngine:
         status = (ctypes.c_int32 * max(n, 1))()
         if n == 0:
             return out, np.zeros(0, np.int32)
-        ptrs = (ctypes.c_char_p * n)(*jpgs)
-        lens = (ctypes.c_size_t * n)(*[len(b) for b in jpgs])
+        ptrs, lens, _keep = _c_samples(jpgs)
         flip_arr = None
         if flip is not None:
             flip_arr = (ctypes.c_uint8 * n)(*[1 if f else 0 for f in flip])
@@ -167,7 +242,7 @@ class JpegEngine:
                layout: str = "chw", out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Stages a batch into pinned slot ``slot`` (0 or 1) and enqueues H2D + decode without waiting.
 
-        ``samples``: encoded bytes, or file paths with ``files=True`` (read straight into the pinned
+        ``samples``: encoded bytes (a list, or an EncodedBatch), or file paths with ``files=True`` (read straight into the pinned
         slot, as LoadFromDiskTransform presets.py:613-626 reads the downloader's local cache).  Returns
         the output tensor, valid after ``wait(slot)``; submitting batch k + 1 to the other slot before
         waiting for batch k overlaps its host staging and H2D copy with batch k's decode."""
@@ -192,8 +267,7 @@ class JpegEngine:
                 rc = self.lib.sdsj_submit_files(self._h, slot, n, paths, ctypes.byref(op), fl,
                                                 ctypes.c_void_p(out.data_ptr()), stream)
             else:
-                ptrs = (ctypes.c_char_p * max(n, 1))(*samples)
-                lens = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in samples])
+                ptrs, lens, _keep = _c_samples(samples)  # (staged into the pinned slot before the call returns)
                 rc = self.lib.sdsj_submit_batch(self._h, slot, n, ptrs, lens, ctypes.byref(op), fl,
                                                 ctypes.c_void_p(out.data_ptr()), stream)
         self._check(rc, "sdsj_submit_files" if files else "sdsj_submit_batch")

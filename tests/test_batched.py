@@ -178,3 +178,49 @@ def test_gpu_stream_matches_oracle():
         for k, i in enumerate(b["index"].tolist()):
             ref = O.pipeline(open(samples[i]["jpg"], "rb").read(), (128, 96))
             np.testing.assert_array_equal(b["image"][k].cpu().numpy(), ref)
+
+
+def _loader_batches(samples, collate, workers: int, bs: int):
+    from torch.utils.data import DataLoader
+
+    from sds_amd.batched import create_deferred_image_pipeline
+    from tests.loader_cases import FolderDataset
+    ds = FolderDataset([s["jpg"] for s in samples], create_deferred_image_pipeline("jpg"))
+    return list(DataLoader(ds, batch_size=bs, num_workers=workers, collate_fn=collate,
+                           multiprocessing_context="fork" if workers else None))
+
+
+def test_collate_encoded_packs_the_image_field_in_shared_memory():
+    """collate_encoded in DataLoader workers: the image field arrives as one EncodedBatch whose bytes are the
+    samples' (in order, shared memory), the other fields exactly as default_collate gives them."""
+    from sds_amd.batched import EncodedBatch, collate_encoded
+    samples = _samples(False)
+    got = _loader_batches(samples, collate_encoded("jpg"), 1, 3)
+    ref = _loader_batches(samples, None, 0, 3)
+    assert len(got) == len(ref) == 2
+    for g, r in zip(got, ref):
+        assert list(g.keys()) == list(r.keys())
+        assert isinstance(g["jpg"], EncodedBatch) and g["jpg"].data.is_shared()
+        assert [g["jpg"][k] for k in range(len(g["jpg"]))] == list(r["jpg"])
+        assert all(torch.equal(g[k], r[k]) if isinstance(r[k], torch.Tensor) else g[k] == r[k]
+                   for k in r if k != "jpg")
+
+
+def test_encoded_batch_transport_equals_the_list_transport(standin):
+    """GpuDecodeBatch on EncodedBatch inputs (synchronous and stream) yields what the list-of-bytes batches
+    give -- values, the damaged sample dropped from every field (the EncodedBatch too), hflip coins."""
+    from sds_amd.batched import EncodedBatch, GpuDecodeBatch, collate_encoded
+    samples = _samples(True)
+    packed = _loader_batches(samples, collate_encoded("jpg"), 0, 2)
+    plain = _loader_batches(samples, None, 0, 2)
+    dec = GpuDecodeBatch("jpg", (40, 40), hflip_prob=0.5)
+    for mode in ("sync", "stream"):
+        torch.manual_seed(5)
+        a = [dec(dict(b)) for b in plain] if mode == "sync" else list(dec.stream(dict(b) for b in plain))
+        torch.manual_seed(5)
+        b = [dec(dict(x)) for x in packed] if mode == "sync" else list(dec.stream(dict(x) for x in packed))
+        assert [x["index"].tolist() for x in b] == [[0, 1], [3], [4]]
+        for x, y in zip(a, b):
+            assert torch.equal(x["image"], y["image"]) and torch.equal(x["index"], y["index"])
+            assert isinstance(y["jpg"], EncodedBatch) and list(y["jpg"]) == list(x["jpg"])
+    assert standin.slots == {}
