@@ -39,7 +39,8 @@ class ImgDescC(ctypes.Structure):
                 ("rgb_pitch", i32), ("ent_groups", i32),
                 ("progressive", i32), ("lat", i32), ("sos_pos", i64), ("off_ptab", i64),
                 ("off_tiles", i64), ("ntiles", i32), ("rs_lay", i32), ("plan_base", i64),
-                ("smooth", i32), ("sm_good", i32), ("sm_bits", ctypes.c_int8 * 60), ("sm_pad", ctypes.c_int8 * 4)]
+                ("smooth", i32), ("sm_good", i32), ("sm_bits", ctypes.c_int8 * 60), ("mh", ctypes.c_int8),
+                ("sm_pad", ctypes.c_int8 * 3), ("etab", i32), ("etab_pad", i32)]
 
 
 def _memcpy_d2h(ptr: int, nbytes: int) -> np.ndarray:
