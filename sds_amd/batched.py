@@ -168,8 +168,11 @@ class GpuDecodeBatch:
                 k += 1
                 eng.submit(slot, encoded, self.resolution, flip=flip, **self._opts())
                 prev, pending = pending, (slot, batch, encoded, flip)
+                batch = encoded = None  # (the consumer's reference is then the batch's last one)
                 if prev is not None:
-                    yield self._collect(eng, prev)
+                    out, prev = self._collect(eng, prev), None
+                    yield out
+                    out = None
             if pending is not None:
                 prev, pending = pending, None
                 yield self._collect(eng, prev)

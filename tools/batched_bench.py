@@ -89,8 +89,21 @@ def main():
                   "seconds": round(dt, 2), "first_batch": first})
         # phase table of the stream loop: loader wait, submit (host staging, planning, launches), wait
         eng = Bm.get_engine("cuda")
-        ph = {"loader_next": 0.0, "submit": 0.0, "wait": 0.0}
+        ph = {"loader_next": 0.0, "inputs": 0.0, "submit": 0.0, "wait": 0.0, "finish": 0.0, "release": 0.0}
         orig_submit, orig_wait = eng.submit, eng.wait
+        orig_inputs, orig_finish = dec._inputs, dec._finish
+
+        def inputs(*a, **k):
+            t = time.perf_counter()
+            r = orig_inputs(*a, **k)
+            ph["inputs"] += time.perf_counter() - t
+            return r
+
+        def finish(*a, **k):
+            t = time.perf_counter()
+            r = orig_finish(*a, **k)
+            ph["finish"] += time.perf_counter() - t
+            return r
 
         def submit(*a, **k):
             t = time.perf_counter()
@@ -112,6 +125,7 @@ def main():
                 yield b
 
         eng.submit, eng.wait = submit, wait
+        dec._inputs, dec._finish = inputs, finish
         try:
             it = dec.stream(timed(epochs(ld)))
             n, t0 = 0, None
@@ -123,6 +137,9 @@ def main():
                         ph[k] = 0.0
                     continue
                 n += b["image"].shape[0]
+                t = time.perf_counter()
+                del b  # the consumer drops the batch: its shared-memory storage is unmapped here
+                ph["release"] += time.perf_counter() - t
                 if time.perf_counter() - t0 >= seconds:
                     break
             torch.cuda.synchronize()
@@ -130,6 +147,7 @@ def main():
             it.close()
         finally:
             eng.submit, eng.wait = orig_submit, orig_wait
+            dec._inputs, dec._finish = orig_inputs, orig_finish
         emit({"mode": f"phases_stream_{tr}", "images_per_s": round(n / dt, 1),
               "ms_per_batch": {k: round(v / max(1, n / bs) * 1e3, 3) for k, v in ph.items()},
               "ms_per_batch_total": round(dt / max(1, n / bs) * 1e3, 3)})
