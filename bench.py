@@ -431,6 +431,12 @@ def main():
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
+    # stdout carries exactly one line, the JSON result: everything else written to file descriptor 1 --
+    # RCCL's version banner, gloo's connection messages, library warnings -- goes to stderr
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -850,7 +856,7 @@ def main():
             line["e2e_host_ms_per_step"] = {k: round(v / args.steps * 1e3, 3) for k, v in ph.items()}
             line["e2e_host_ms_per_step"]["step"] = round(elapsed / args.steps * 1e3, 3)
             line["roofline"]["note"] = "device-resident kernels of the same rows (the PCIe legs are not kernels)"
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     if use_pg:
         dist.barrier()
         dist.destroy_process_group()

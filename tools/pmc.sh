@@ -3,13 +3,14 @@
 # tools/pmc_summary.py then folds the CSVs into gpurun_out/pmc.json (mean per dispatch per kernel).
 # SDSJ_LANES (default 1 here) is the engine's lane count for the whole run: at 1, one dispatch of a
 # kernel covers the whole batch, the unit bench.py's roofline prices.
+# (--no-pixel-check: the check's reference and walk batches would enter the per-dispatch means)
 # usage: tools/pmc.sh [extra bench args]
 set -e
 export TMPDIR=/tmp
 export SDSJ_LANES=${SDSJ_LANES:-1}
 BATCH=${BATCH:-65536}  # bench.py's default configs[1] batch (the PMC summary is per dispatch of one lane)
 ROWS=$(( BATCH + 4096 ))
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-steps 1 --rows $ROWS --batch $BATCH $*"
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-pixel-check --roofline-steps 1 --rows $ROWS --batch $BATCH $*"
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU" \
