@@ -32,8 +32,12 @@ OSError makes ``_iter_chunks_`` skip it, dataset.py:366-371) is dropped from eve
 """
 from __future__ import annotations
 
+import os
+import time
+import weakref
 from typing import Any, Iterable, Iterator, Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -49,21 +53,144 @@ def create_deferred_image_pipeline(image_field: str) -> Sequence[SampleTransform
     return [LoadFromDiskTransform([image_field])]
 
 
+# -- the workers' slot rings (collate_encoded) ---------------------------------------------------------
+# A fresh shared-memory tensor per batch costs both processes a page fault per 4 KiB of it and the
+# training process an unmap per batch -- on one MI355X box that was about half of the consumer's time per
+# 256-image batch (tools/batched_bench.py phases, profiles/r06_f1_*).  So each worker keeps a ring of
+# `slots` shared-memory slots, sent to the training process once with its first batch; a batch then
+# travels as (worker, slot, offsets, lengths), and its EncodedBatch views the slot.  A slot is busy from
+# the worker's write until the training process drops the EncodedBatch (and every selection of it):
+# a weakref finalizer clears its flag in the ring's header, which the worker polls.  When no slot is
+# free within `wait_s` (a consumer holding many batches), or the batch outgrows a slot, the worker falls
+# back to a one-off shared-memory tensor, so nothing can deadlock.
+_RING_HDR = 64  # bytes per slot flag (one cache line each)
+_rings: dict = {}  # training process: ring serial (worker pid, n) -> ring tensor
+_ring_serial = [0]
+
+
+class _WorkerRing:
+    def __init__(self, slots: int, slot_bytes: int):
+        self.slots, self.slot_bytes = slots, slot_bytes
+        self.tensor = torch.empty(_RING_HDR * slots + slots * slot_bytes, dtype=torch.uint8).share_memory_()
+        self.flags = self.tensor[:_RING_HDR * slots].numpy().view(np.int32)[::_RING_HDR // 4]
+        self.flags[:] = 0
+        _ring_serial[0] += 1
+        self.serial = (os.getpid(), _ring_serial[0])
+        self.sent = False
+        self.next = 0
+
+    def claim(self, wait_s: float):
+        t0 = None
+        while True:
+            for i in range(self.slots):
+                s = (self.next + i) % self.slots
+                if self.flags[s] == 0:
+                    self.flags[s] = 1
+                    self.next = s + 1
+                    return s
+            t0 = t0 if t0 is not None else time.perf_counter()
+            if time.perf_counter() - t0 > wait_s:
+                return None
+            time.sleep(0.0002)
+
+    def data_off(self, slot: int) -> int:
+        return _RING_HDR * self.slots + slot * self.slot_bytes
+
+
+def _release_slot(ring: torch.Tensor, slots: int, slot: int) -> None:
+    ring[:_RING_HDR * slots].numpy().view(np.int32)[slot * (_RING_HDR // 4)] = 0
+
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+        return True
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+
+
+def _rebuild_ring_batch(serial, ring, slots, slot, off, total, offs, lens) -> EncodedBatch:
+    """Training process side of a ring batch: the ring arrives with the worker's first batch (torch shares
+    its storage), later batches look it up.  Rings of workers that have exited are dropped from the
+    registry (their live batches keep their own reference)."""
+    if ring is not None:
+        for k in [k for k in _rings if not _pid_alive(k[0])]:
+            del _rings[k]
+        _rings[serial] = ring
+    ring = _rings.get(serial)
+    if ring is None:  # (cannot happen: a worker's batches arrive in order, its ring first)
+        raise RuntimeError("encoded batch from an unknown slot ring")
+    eb = EncodedBatch(ring[off:off + total], torch.from_numpy(np.frombuffer(offs, np.int64).copy()),
+                      torch.from_numpy(np.frombuffer(lens, np.int64).copy()))
+    weakref.finalize(eb, _release_slot, ring, slots, slot)
+    return eb
+
+
+class _RingBatch(EncodedBatch):
+    """Worker side: an EncodedBatch in a ring slot, pickled as its ring coordinates."""
+
+    __slots__ = ("_ring", "_slot")
+
+    def __reduce__(self):
+        r = self._ring
+        ring = None if r.sent else r.tensor
+        r.sent = True
+        off = r.data_off(self._slot)
+        return (_rebuild_ring_batch, (r.serial, ring, r.slots, self._slot, off, int(self.data.numel()),
+                                      self.offsets.numpy().tobytes(), self.lengths.numpy().tobytes()))
+
+
 class collate_encoded:
     """A DataLoader ``collate_fn`` for the batched consumer: ``image_field`` (the encoded bytes that
-    create_deferred_image_pipeline leaves) becomes an ``EncodedBatch`` -- in shared memory when collated in
-    a worker, as default_collate allocates its tensors there --, every other field goes through
-    ``collate_fn`` (default_collate).  Picklable, so spawn-started workers can run it."""
+    create_deferred_image_pipeline leaves) becomes an ``EncodedBatch``; every other field goes through
+    ``collate_fn`` (default_collate).  In a worker the bytes go into the worker's ring of shared-memory
+    slots (above; ``slots`` per worker, each sized for 1.5x the worker's first batch); in the main process
+    into a private tensor.  Picklable, so spawn-started workers can run it."""
 
-    def __init__(self, image_field: str, collate_fn=None):
+    def __init__(self, image_field: str, collate_fn=None, slots: int = 8, wait_s: float = 0.05):
         self.image_field = image_field
         self.collate_fn = collate_fn
+        self.slots = int(slots)
+        self.wait_s = float(wait_s)
+        self._ring = None  # (per worker process, created on its first batch)
+
+    def __getstate__(self):
+        d = dict(self.__dict__)
+        d["_ring"] = None
+        return d
+
+    def _pack(self, items: list) -> EncodedBatch:
+        from torch.utils.data import get_worker_info
+        wi = get_worker_info()
+        if wi is None or self.slots <= 0:
+            return EncodedBatch.pack(items, shared=wi is not None)
+        total = sum(len(b) for b in items)
+        if self._ring is None:
+            self._ring = _WorkerRing(self.slots, max(1 << 20, (total * 3 // 2 + 4095) // 4096 * 4096))
+        r = self._ring
+        slot = r.claim(self.wait_s) if total <= r.slot_bytes else None
+        if slot is None:
+            return EncodedBatch.pack(items, shared=True)
+        off = r.data_off(slot)
+        data = r.tensor[off:off + total]
+        lens = np.fromiter((len(b) for b in items), dtype=np.int64, count=len(items))
+        offs = np.zeros(len(items), np.int64)
+        if len(items) > 1:
+            np.cumsum(lens[:-1], out=offs[1:])
+        buf = data.numpy()
+        for b, o, n in zip(items, offs, lens):
+            buf[o:o + n] = np.frombuffer(b, dtype=np.uint8)
+        eb = _RingBatch(data, torch.from_numpy(offs), torch.from_numpy(lens))
+        eb._ring, eb._slot = r, slot
+        return eb
 
     def __call__(self, samples: Sequence[dict]) -> dict:
-        from torch.utils.data import default_collate, get_worker_info
+        from torch.utils.data import default_collate
         rest = [{k: v for k, v in s.items() if k != self.image_field} for s in samples]
         out = (self.collate_fn or default_collate)(rest)
-        enc = EncodedBatch.pack([s[self.image_field] for s in samples], shared=get_worker_info() is not None)
+        enc = self._pack([s[self.image_field] for s in samples])
         # (the image field keeps its place among the sample's keys)
         keys = list(samples[0].keys()) if samples else []
         return {k: (enc if k == self.image_field else out[k]) for k in keys}

@@ -52,9 +52,9 @@ class EncodedBatch:
     engine stages it straight from there (no per-sample copies in Python).  Indexing gives one sample's
     bytes (the PIL fallback's input); ``len`` is the sample count."""
 
-    __slots__ = ("data", "offsets", "lengths")
+    __slots__ = ("data", "offsets", "lengths", "_keep", "__weakref__")
 
-    def __init__(self, data: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor):
+    def __init__(self, data: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor, keep=None):
         if data.dtype != torch.uint8 or data.device.type != "cpu" or not data.is_contiguous() or data.dim() != 1:
             raise ValueError("data must be a contiguous 1-D uint8 CPU tensor")
         if offsets.shape != lengths.shape or offsets.dim() != 1:
@@ -63,6 +63,7 @@ class EncodedBatch:
         if len(off) and (off.min() < 0 or ln.min() < 0 or (off + ln).max() > data.numel()):
             raise ValueError("a sample lies outside data")
         self.data, self.offsets, self.lengths = data, offsets, lengths
+        self._keep = keep  # (an object whose lifetime guards ``data``: the batch a selection came from)
 
     @staticmethod
     def pack(samples: Sequence, shared: bool = False) -> "EncodedBatch":
@@ -96,7 +97,7 @@ class EncodedBatch:
     def select(self, keep: Sequence[int]) -> "EncodedBatch":
         """The kept samples (views into the same ``data``)."""
         k = torch.as_tensor(list(keep), dtype=torch.long)
-        return EncodedBatch(self.data, self.offsets[k], self.lengths[k])
+        return EncodedBatch(self.data, self.offsets[k], self.lengths[k], keep=self)
 
     def pointers(self):
         """(uint64 sample addresses, uint64 lengths) for the C-ABI's pointer / length arrays; valid while

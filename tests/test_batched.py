@@ -224,3 +224,39 @@ def test_encoded_batch_transport_equals_the_list_transport(standin):
             assert torch.equal(x["image"], y["image"]) and torch.equal(x["index"], y["index"])
             assert isinstance(y["jpg"], EncodedBatch) and list(y["jpg"]) == list(x["jpg"])
     assert standin.slots == {}
+
+
+def test_collate_encoded_slot_ring_reuses_and_releases_slots():
+    """collate_encoded's worker rings: a worker's batches travel as slot coordinates after the first (which
+    carries the ring); a slot returns to its worker once the training process drops the EncodedBatch and
+    every selection of it; bytes stay those of each batch's samples across slot reuse; a worker whose
+    slots are all held falls back to one-off shared memory instead of waiting forever."""
+    import gc
+
+    from torch.utils.data import DataLoader
+
+    from sds_amd import batched as Bm
+    from sds_amd.batched import EncodedBatch, collate_encoded, create_deferred_image_pipeline
+    from tests.loader_cases import FolderDataset
+    samples = _samples(False)
+    paths = [s["jpg"] for s in samples] * 6  # 30 samples
+    want = [open(p, "rb").read() for p in paths]
+    ds = FolderDataset(paths, create_deferred_image_pipeline("jpg"))
+    ld = DataLoader(ds, batch_size=2, num_workers=1, multiprocessing_context="fork",
+                    collate_fn=collate_encoded("jpg", slots=2, wait_s=0.01), prefetch_factor=2)
+    held, k = [], 0
+    for b in ld:  # drop every batch at once: slots are reused
+        e = b["jpg"]
+        assert isinstance(e, EncodedBatch) and list(e) == want[k:k + len(e)]
+        k += len(e)
+        del b, e
+        gc.collect()
+    assert k == len(want)
+    assert len(Bm._rings) >= 1
+    k = 0
+    for b in ld:  # hold every batch (and a selection of each): the worker falls back once its slots are held
+        e = b["jpg"]
+        held.append((b, e.select([0])))
+        k += len(e)
+    assert [list(x["jpg"]) for x, _ in held] == [want[i:i + 2] for i in range(0, len(want), 2)]
+    assert [list(s) for _, s in held] == [[want[i]] for i in range(0, len(want), 2)]
