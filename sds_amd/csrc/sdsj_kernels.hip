@@ -462,7 +462,8 @@ constexpr int kZeroChunks = 16;
 constexpr int kZeroGrid = 2048;
 __global__ void __launch_bounds__(256) k_zerofill(int n, const ImgDesc* __restrict__ descs, sdsj_op op,
                                                   void* __restrict__ out, const float* __restrict__ lut) {
-  __shared__ uint8_t fill[256];
+  __shared__ int32_t fill[256];  // the window's flagged items, compacted
+  __shared__ int nfill;
   const int t = threadIdx.x;
   const int64_t total = (int64_t)op.out_h * op.out_w * 3, per = (total + kZeroChunks - 1) / kZeroChunks;
   const int64_t items = (int64_t)n * kZeroChunks;
@@ -473,10 +474,12 @@ __global__ void __launch_bounds__(256) k_zerofill(int n, const ImgDesc* __restri
       const ImgDesc* d = &descs[w / kZeroChunks];
       f = d->status != SDSJ_OK || d->geo == kGeoZeros;
     }
-    fill[t] = f ? 1 : 0;
+    if (t == 0) nfill = 0;
     __syncthreads();
-    for (int k = 0; k < 256; k++) {
-      if (!fill[k]) continue;
+    if (f) fill[atomicAdd(&nfill, 1)] = t;  // (a window without failures: one barrier, no loop -- the scan
+    __syncthreads();                         //  of all 256 flags cost a single-image call ~10 us)
+    for (int q = 0; q < nfill; q++) {
+      const int k = fill[q];
       const int64_t wk = blockIdx.x + (k0 + k) * gridDim.x;
       const int img = (int)(wk / kZeroChunks), ch = (int)(wk % kZeroChunks);
       const int64_t e0 = ch * per, e1 = e0 + per < total ? e0 + per : total;
