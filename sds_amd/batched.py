@@ -78,18 +78,23 @@ class _WorkerRing:
         self.serial = (os.getpid(), _ring_serial[0])
         self.sent = False
         self.next = 0
+        self.starved = False  # the last claim found every slot held: do not wait again until one frees
 
     def claim(self, wait_s: float):
         t0 = None
+        if self.starved:
+            wait_s = 0.0
         while True:
             for i in range(self.slots):
                 s = (self.next + i) % self.slots
                 if self.flags[s] == 0:
                     self.flags[s] = 1
                     self.next = s + 1
+                    self.starved = False
                     return s
             t0 = t0 if t0 is not None else time.perf_counter()
-            if time.perf_counter() - t0 > wait_s:
+            if time.perf_counter() - t0 >= wait_s:
+                self.starved = True  # (a consumer holding its batches: fall back without waiting each time)
                 return None
             time.sleep(0.0002)
 
