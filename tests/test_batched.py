@@ -260,3 +260,24 @@ def test_collate_encoded_slot_ring_reuses_and_releases_slots():
         k += len(e)
     assert [list(x["jpg"]) for x, _ in held] == [want[i:i + 2] for i in range(0, len(want), 2)]
     assert [list(s) for _, s in held] == [[want[i]] for i in range(0, len(want), 2)]
+
+
+def test_collate_encoded_with_spawned_persistent_workers():
+    """The slot rings under spawn-started, persistent workers (the collate function is pickled to them
+    without its ring; each creates its own): two epochs, every batch's bytes those of its samples."""
+    from torch.utils.data import DataLoader
+
+    from sds_amd.batched import EncodedBatch, collate_encoded, create_deferred_image_pipeline
+    from tests.loader_cases import FolderDataset
+    samples = _samples(False)
+    paths = [s["jpg"] for s in samples] * 4  # 20 samples
+    want = sorted(open(p, "rb").read() for p in paths)
+    ds = FolderDataset(paths, create_deferred_image_pipeline("jpg"))
+    ld = DataLoader(ds, batch_size=3, num_workers=2, multiprocessing_context="spawn", persistent_workers=True,
+                    collate_fn=collate_encoded("jpg", slots=3))
+    for _ in range(2):
+        got = []
+        for b in ld:
+            assert isinstance(b["jpg"], EncodedBatch)
+            got += list(b["jpg"])
+        assert sorted(got) == want
