@@ -36,6 +36,8 @@ class LocalDownloader:
 
     @staticmethod
     def _path(url: str) -> str:
+        if "://" not in url and not url.startswith("file:"):  # a plain local path (no scheme to resolve)
+            return url
         u = urllib.parse.urlparse(url)
         if u.scheme not in ("", "file"):
             raise ValueError(f"only local sources are restated here, got scheme {u.scheme!r} ({url})")
@@ -64,7 +66,10 @@ def run_downloading_task(task: DownloadingTask) -> tuple[int, int]:
     """downloader.py:117-131: (total size of the sample's files, bytes actually copied)."""
     existing, downloaded = 0, 0
     for url, dst in zip(task.source_urls, task.destinations):
-        cur = os.path.getsize(dst) if os.path.exists(dst) else 0
+        try:  # (os.path.exists + getsize as one stat)
+            cur = os.stat(dst).st_size
+        except FileNotFoundError:
+            cur = 0
         if task.skip_if_exists and cur > 0:
             existing += cur
             continue
