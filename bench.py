@@ -401,9 +401,10 @@ def main():
                          "configs[1] -- and 1,000,000 on several -- configs[3])")
     ap.add_argument("--pool", type=int, default=None, help="distinct encoded images")
     ap.add_argument("--res", type=int, default=None)
-    ap.add_argument("--dl-workers", type=int, default=None,
-                    help="configs[4]: threads of the restated ParallelDownloader (default: this process's CPU share, "
-                         "at least 4 -- the reference's num_downloading_workers default, dataset.py:61)")
+    ap.add_argument("--dl-workers", type=int, default=4,
+                    help="configs[4]: threads of the restated ParallelDownloader (the reference's num_downloading_workers "
+                         "default, dataset.py:61; 4 / 8 / 16 threads: 53-56k / 49-57k / 44-50k images/s warm and "
+                         "10.0-10.3k / 5.8-8.3k / 5.5-6.7k cold, profiles/r06_e2e_dl_workers.txt)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--cpu-files", type=int, default=1000, help="files in the CPU-baseline folder (configs[0])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -591,7 +592,7 @@ def main():
             src_paths[p] = os.path.join(src_dir, f"{p:06d}.jpg")
             with open(src_paths[p], "wb") as f:
                 f.write(pool[p])
-        dl_workers = args.dl_workers or max(4, workers)
+        dl_workers = args.dl_workers
         dl = ParallelDownloader(num_workers=dl_workers, prefetch=2 * B, num_retries=3, skip_if_exists=True)
         dst_of = lambda key: os.path.join(cache_dir, f"{key:08d}-jpg.jpg")  # noqa: E731  (dataset.py:250)
         sched = [0]
