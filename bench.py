@@ -255,7 +255,7 @@ def _pil_u8_sha(args) -> str:
 
 
 def verify_rows(eng, blob, d_offs, d_lens, out, status, flips, rows_ext, period, pool, nrows, B, res, mixed,
-                last_start, dev_step, cursor, workers) -> dict:
+                last_start, dev_step, cursor, workers, e2e_last=None) -> dict:
     """Checks decoded rows on the device against per-pool-image references.
 
     The references: each distinct pool image of the rank's period, decoded once by the engine (uint8 CHW,
@@ -263,7 +263,9 @@ def verify_rows(eng, blob, d_offs, d_lens, out, status, flips, rows_ext, period,
     its pool image's reference, flipped where the row's flag says so and mapped through the normalise LUT
     (``x.float() / 127.5 - 1`` per byte value, evaluated on the host) for configs[2].  Checked: every row of
     the batch ``out`` holds (rows [last_start, last_start + B), the last timed batch) and then every resident
-    row of the rank -- ceil(nrows / B) batches from row 0 through ``dev_step``."""
+    row of the rank -- ceil(nrows / B) batches from row 0 through ``dev_step``.  ``e2e_last`` (configs[4]):
+    (host tensor, row indices) of the last batch the end-to-end pipeline delivered to host memory, checked
+    the same way before the walk."""
     import hashlib
 
     import torch
@@ -308,6 +310,13 @@ def verify_rows(eng, blob, d_offs, d_lens, out, status, flips, rows_ext, period,
         g = check(last_start)
         res_d.update(rows_checked=B, rows_equal=g, last_batch_first_row=int(last_start))
         ok = ok and g == B
+    if e2e_last is not None:
+        host, rows = e2e_last
+        idx = torch.from_numpy(np.asarray(rows, dtype=np.int64) % P).to(dev)
+        eq = (host.to(dev) == ref[idx]).flatten(1).all(1)
+        g = int(eq.sum().item())
+        res_d.update(e2e_rows_checked=len(rows), e2e_rows_equal=g)
+        ok = ok and g == len(rows)
     walk_batches = (nrows + B - 1) // B
     cursor[0] = 0
     wg = 0
@@ -401,6 +410,9 @@ def main():
                          "configs[1] -- and 1,000,000 on several -- configs[3])")
     ap.add_argument("--pool", type=int, default=None, help="distinct encoded images")
     ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--e2e-out", choices=["device", "pinned"], default="device",
+                    help="configs[4]: decode into HBM and copy back on a D2H stream (device), or let the kernels "
+                         "store the pixels straight into pinned host memory over PCIe (pinned)")
     ap.add_argument("--dl-workers", type=int, default=4,
                     help="configs[4]: threads of the restated ParallelDownloader (the reference's num_downloading_workers "
                          "default, dataset.py:61; 4 / 8 / 16 threads: 53-56k / 49-57k / 44-50k images/s warm and "
@@ -603,19 +615,25 @@ def main():
                 dl.schedule_task(r0 + j, [src_paths[period[j % len(period)]]], [dst_of(r0 + j)])
                 sched[0] += 1
 
-        outs = [out, torch.empty_like(out)]
         hosts = [torch.empty(out.shape, dtype=out.dtype, pin_memory=True) for _ in range(2)]
+        zero_copy = args.e2e_out == "pinned"
+        outs = hosts if zero_copy else [out, torch.empty_like(out)]
         d2h = torch.cuda.Stream(dev)
-        pipe = {"k": 0, "prev": None, "bad": 0, "done": 0, "taken": 0}
+        # the decode runs on a stream of its own, not the legacy default stream (which synchronises with
+        # every blocking stream).  The device still serialises each D2H (a 15.0 ms blit kernel per
+        # 1,024 rows) with the next batch's 3.1 ms decode: profiles/r06_e2e_trace.txt
+        work = torch.cuda.Stream(dev)
+        pipe = {"k": 0, "prev": None, "bad": 0, "done": 0, "taken": 0, "keys": [None, None], "last": None}
 
         def complete_prev():
             prev = pipe["prev"]
             o, st = eng.wait(prev)
             pipe["bad"] += int((st != 0).sum())
             pipe["done"] += len(st)
-            with torch.cuda.stream(d2h):
-                hosts[prev].copy_(o, non_blocking=True)
-            pipe["prev"] = None
+            if not zero_copy:
+                with torch.cuda.stream(d2h):
+                    hosts[prev].copy_(o, non_blocking=True)
+            pipe["prev"], pipe["last"] = None, prev
 
         # host wall time per phase of the step (seconds, summed; reset with the timed region): scheduling the
         # downloads ahead, taking the batch's completed rows from the downloader, engine.submit (file reads
@@ -627,14 +645,17 @@ def main():
             t0 = time.perf_counter()
             schedule_ahead(pipe["taken"] + 2 * B)
             t1 = time.perf_counter()
-            paths = [dst_of(key) for key, _ in islice(dl.yield_completed(), B)]
+            keys = [key for key, _ in islice(dl.yield_completed(), B)]
+            paths = [dst_of(key) for key in keys]
             if len(paths) != B:  # a row whose copy failed every retry: fail the run, never count it
                 raise SystemExit(f"rank {rank}: the downloader delivered {len(paths)} of {B} rows")
             t2 = time.perf_counter()
             pipe["taken"] += B
             slot = pipe["k"] % 2
-            torch.cuda.current_stream(dev).wait_stream(d2h)  # slot's previous output has left for the host
-            eng.submit(slot, paths, (args.res, args.res), files=True, out=outs[slot])
+            with torch.cuda.stream(work):
+                work.wait_stream(d2h)  # slot's previous output has left for the host
+                eng.submit(slot, paths, (args.res, args.res), files=True, out=outs[slot])
+            pipe["keys"][slot] = keys
             t3 = time.perf_counter()
             if pipe["prev"] is not None:
                 complete_prev()
@@ -739,7 +760,9 @@ def main():
     pixel_check = None
     if not stub and not args.no_pixel_check:
         pixel_check = verify_rows(eng, blob, d_offs, d_lens, out, status, flips, j, period, pool, nrows, B,
-                                  args.res, mixed, None if e2e else last_start, dev_step, cursor, cpu_share()[0])
+                                  args.res, mixed, None if e2e else last_start, dev_step, cursor, cpu_share()[0],
+                                  e2e_last=(hosts[pipe["last"]], np.asarray(pipe["keys"][pipe["last"]]) - r0)
+                                  if e2e else None)
         pixel_check.update(rows_decoded_in_timed_region=rows_timed if not e2e else None,
                            distinct_rows_in_timed_region=min(nrows, rows_timed) if not e2e else None,
                            resident_rows=nrows)
@@ -857,6 +880,7 @@ def main():
             line["device_resident_value"] = round(dev_value, 1)
             line["e2e_over_device_resident"] = round(value / dev_value, 4)
             line["downloader"] = dl_rates
+            line["e2e_out"] = args.e2e_out
             line["e2e_host_ms_per_step"] = {k: round(v / args.steps * 1e3, 3) for k, v in ph.items()}
             line["e2e_host_ms_per_step"]["step"] = round(elapsed / args.steps * 1e3, 3)
             line["roofline"]["note"] = "device-resident kernels of the same rows (the PCIe legs are not kernels)"

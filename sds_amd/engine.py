@@ -190,11 +190,14 @@ class JpegEngine:
 
     def _check_out(self, out: torch.Tensor, n: int, op: SdsjOp) -> None:
         """The native side writes n * out_h * out_w * 3 elements of the op's dtype through a raw pointer:
-        ``out`` must be exactly what _alloc_out would give (shape, dtype, contiguous, this engine's device)."""
+        ``out`` must be exactly what _alloc_out would give (shape, dtype, contiguous, this engine's device),
+        or a pinned host tensor of that shape and dtype: pinned host memory is mapped into the device's
+        address space, so the kernels store the pixels straight over PCIe (no separate D2H copy)."""
         shape, dtype = self._out_spec(n, op)
+        where = isinstance(out, torch.Tensor) and (self._on_engine(out) or (out.device.type == "cpu" and out.is_pinned()))
         if not isinstance(out, torch.Tensor) or tuple(out.shape) != shape or out.dtype != dtype or \
-                not out.is_contiguous() or not self._on_engine(out):
-            raise ValueError(f"out must be a contiguous {dtype} tensor of shape {shape} on cuda:{self.device}, got "
+                not out.is_contiguous() or not where:
+            raise ValueError(f"out must be a contiguous {dtype} tensor of shape {shape} on cuda:{self.device} (or pinned host memory), got "
                              f"{getattr(out, 'dtype', type(out))} {tuple(getattr(out, 'shape', ()))} on "
                              f"{getattr(out, 'device', '?')}")
 

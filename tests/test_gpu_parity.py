@@ -106,6 +106,23 @@ def test_hwc_layout_and_flip(engine):
     assert torch.equal(hwc[1].permute(2, 0, 1), chw[1])
 
 
+def test_pinned_host_output(engine):
+    """out= pinned host memory: the kernels store the pixels over PCIe (bench.py --e2e-out pinned); same
+    bytes as the device output, the failed sample zero-filled, and the host output of both lanes' slots"""
+    _, jpgs = G.g2_jpegs()
+    batch = list(jpgs) + [b"not a jpeg"]
+    dev, st_d = engine.decode_resize(batch, (96, 128))
+    host = torch.full((len(batch), 3, 96, 128), 7, dtype=torch.uint8).pin_memory()
+    got, st_h = engine.decode_resize(batch, (96, 128), out=host)
+    torch.cuda.synchronize()
+    assert got.data_ptr() == host.data_ptr() and got.device.type == "cpu"
+    assert (st_h == st_d).all() and st_h[-1] != 0 and (st_h[:-1] == 0).all()
+    assert torch.equal(host, dev.cpu())
+    assert int(host[-1].max()) == 0
+    with pytest.raises(ValueError):
+        engine.decode_resize(batch, (96, 128), out=torch.empty((len(batch), 3, 96, 128), dtype=torch.uint8))
+
+
 def _random_jpegs(seed: int, n: int):
     from tests.golden.synth import encode_jpeg, synth_rgb
     rng = np.random.default_rng(seed)
