@@ -17,6 +17,10 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -87,6 +91,8 @@ struct sdsj_engine {
   int32_t* d_status = nullptr;
   int32_t* h_status = nullptr;
   int io_cap = 0;
+  // persistent staging threads of the host paths (parallel_for), created on first use
+  std::unique_ptr<struct StagePool> pool;
   // asynchronous host path (sdsj_submit_*): per-slot pinned staging, device inputs and events
   struct Slot {
     uint8_t* h_stage = nullptr;
@@ -381,18 +387,79 @@ int stage_threads() {
   return k;
 }
 
+}  // namespace
+
+// The engine's staging threads, kept across calls: starting and joining 7 threads per parallel_for cost
+// as much as the parallel memcpy saved (submit 1.29 ms serial vs 1.44 ms with 8 fresh threads per
+// 256-image batch at 16 DataLoader workers, profiles/r06_f1_stage_threads.jsonl).  One call at a time;
+// worker k runs part k of the current call's range and the caller runs part 0.
+struct StagePool {
+  std::vector<std::thread> th;
+  std::mutex call_m, m;
+  std::condition_variable go, done;
+  std::function<void(int, int)> fn;
+  int n = 0, nt = 0, left = 0;
+  uint64_t gen = 0;
+  bool stop = false;
+  explicit StagePool(int workers) {
+    for (int k = 1; k <= workers; k++) th.emplace_back([this, k] { run(k); });
+  }
+  ~StagePool() {
+    {
+      std::lock_guard<std::mutex> l(m);
+      stop = true;
+    }
+    go.notify_all();
+    for (auto& t : th) t.join();
+  }
+  void run(int k) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void(int, int)> f;
+      int a = 0, b = 0;
+      {
+        std::unique_lock<std::mutex> l(m);
+        go.wait(l, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+        if (k >= nt) continue;
+        f = fn;
+        a = (int)((int64_t)n * k / nt);
+        b = (int)((int64_t)n * (k + 1) / nt);
+      }
+      f(a, b);
+      std::lock_guard<std::mutex> l(m);
+      if (--left == 0) done.notify_one();
+    }
+  }
+  void parallel_for(int n_, int nt_, const std::function<void(int, int)>& body) {
+    std::lock_guard<std::mutex> cl(call_m);
+    {
+      std::lock_guard<std::mutex> l(m);
+      fn = body;
+      n = n_;
+      nt = nt_;
+      left = nt_ - 1;
+      gen++;
+    }
+    go.notify_all();
+    body(0, (int)((int64_t)n_ / nt_));
+    std::unique_lock<std::mutex> l(m);
+    done.wait(l, [&] { return left == 0; });
+  }
+};
+
+namespace {
+
 template <class F>
-void parallel_for(int n, F fn) {
+void parallel_for(sdsj_engine* e, int n, F fn) {
   const int nt = std::min(stage_threads(), std::max(1, n / 16));
   if (nt <= 1) {
     fn(0, n);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(nt - 1);
-  for (int k = 1; k < nt; k++) th.emplace_back(fn, (int)((int64_t)n * k / nt), (int)((int64_t)n * (k + 1) / nt));
-  fn(0, (int)((int64_t)n / nt));
-  for (auto& t : th) t.join();
+  if (!e->pool) e->pool.reset(new StagePool(stage_threads() - 1));
+  e->pool->parallel_for(n, nt, fn);
 }
 
 void slot_free(Slot& sl) {
@@ -463,7 +530,7 @@ int slot_launch(sdsj_engine* e, Slot& sl, int n, size_t bytes, const sdsj_op& op
   std::vector<int64_t> needs(n, 0);
   const bool small = n <= kSmallBatch;
   std::atomic<uint64_t> rmask{0};  // the routes the batch takes (launchers skip the others)
-  parallel_for(n, [&](int i0, int i1) {
+  parallel_for(e, n, [&](int i0, int i1) {
     uint64_t rm = 0;
     for (int i = i0; i < i1; i++) {
       if (sl.h_pre[i] != SDSJ_OK) continue;
@@ -550,7 +617,7 @@ int sdsj_submit_batch(sdsj_engine* e, int slot, int n, const uint8_t* const* jpg
     sl.h_pre[i] = SDSJ_OK;
     off += align_up((int64_t)len[i], 16);
   }
-  parallel_for(n, [&](int i0, int i1) {
+  parallel_for(e, n, [&](int i0, int i1) {
     for (int i = i0; i < i1; i++) memcpy(sl.h_stage + sl.h_offsets[i], jpg[i], len[i]);
   });
   if (n == 0) {
@@ -569,7 +636,7 @@ int sdsj_submit_files(sdsj_engine* e, int slot, int n, const char* const* paths,
   DeviceGuard g(e->device);
   Slot& sl = e->slots[slot];
   std::vector<int64_t> sizes(n);
-  parallel_for(n, [&](int i0, int i1) {
+  parallel_for(e, n, [&](int i0, int i1) {
     for (int i = i0; i < i1; i++) {
       sizes[i] = file_size(paths[i]);
       if (sizes[i] > INT32_MAX) sizes[i] = -1;
@@ -586,7 +653,7 @@ int sdsj_submit_files(sdsj_engine* e, int slot, int n, const char* const* paths,
     sl.h_flip[i] = flip ? flip[i] : 0;
     if (sizes[i] > 0) off += align_up(sizes[i], 16);
   }
-  parallel_for(n, [&](int i0, int i1) {
+  parallel_for(e, n, [&](int i0, int i1) {
     for (int i = i0; i < i1; i++) {
       const bool ok = sizes[i] >= 0 && read_file(paths[i], sl.h_stage + sl.h_offsets[i], sizes[i]);
       sl.h_lengths[i] = ok ? (int32_t)sizes[i] : -1;  // (k_finish reports a negative length as EINVAL, counted "other")
