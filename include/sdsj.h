@@ -103,7 +103,9 @@ int sdsj_engine_destroy(sdsj_engine* eng);
  *   jpg[i], len[i]  : encoded bytes of sample i (borrowed)
  *   flip            : host array of n bytes (1 = horizontal flip) or NULL
  *   out             : device pointer to n * out_h * out_w * 3 elements of op->out_dtype, laid
- *                     out per op->layout, sample-major; allocated by the caller (torch)
+ *                     out per op->layout, sample-major; allocated by the caller (torch).  Pinned
+ *                     host memory (hipHostMalloc / torch pin_memory) is device-accessible and works
+ *                     too: the kernels then store the pixels over PCIe (no separate D2H copy)
  *   status          : host array of n ints, per-sample SDSJ_* code (filled before return)
  * Synchronises `hip_stream` before returning (status is host memory). */
 int sdsj_decode_resize_batch(sdsj_engine* eng, int n, const uint8_t* const* jpg, const size_t* len,
